@@ -1,0 +1,582 @@
+// extern "C" boundary of libhgmres (include/hgmres.h): context / communicator /
+// operator management and the solver entry points that replace the reference's
+// MATLAB functions.  Every entry point converts C++ exceptions into a status code
+// and keeps the message for hgm_last_error().
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "internal.h"
+
+namespace hgm {
+
+// solvers.cpp
+struct GmresSpec {
+    int side;
+    int proj;
+    bool lambda_in_op;
+    bool x_preassigned;
+};
+int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_mat* A, const hgm_mat* B,
+                 const double* b_in, const double* xt_in, double tol, int maxit, double lambda, double* x_out,
+                 double* err_out, double* res_out, int* niters);
+template <typename T>
+int lsqr_t(hgm_ctx*, const hgm_opts*, const hgm_mat*, const hgm_mat*, const double*, const double*, double, int,
+           bool, double, double*, double*, double*, int*);
+template <typename T>
+int lsmr_t(hgm_ctx*, const hgm_opts*, const hgm_mat*, const hgm_mat*, const double*, const double*, double, int,
+           double*, double*, double*, double*, int*);
+int hybrid_lsmr(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, const double* b_in,
+                const double* xt_in, double tol, int maxit, double lambda, double* x_out, double* err_out,
+                double* res_out, int* niters);
+int arnoldi(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b_in, int kg, int side, double btol,
+            int orth, double* H_out, double* beta_out, int* kdone);
+
+enum { PROJ_LS = 0, PROJ_PTR = 1, PROJ_ABRTP = 2 };
+
+void DevBuf::ensure(size_t b) {
+    if (b <= bytes) return;
+    release();
+    if (hipMalloc(&p, b) != hipSuccess) {
+        p = nullptr;
+        bytes = 0;
+        throw Error{HGM_E_NOMEM, "hipMalloc failed for workspace (" + std::to_string(b) + " bytes)"};
+    }
+    bytes = b;
+}
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+
+hipEvent_t Timing::get() {
+    if (!pool.empty()) {
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    HGM_HIP(hipEventCreate(&e));
+    return e;
+}
+void Timing::clear() {
+    for (int k = 0; k < KC_N; ++k) {
+        for (auto& pr : ev[k]) {
+            pool.push_back(pr.first);
+            pool.push_back(pr.second);
+        }
+        ev[k].clear();
+        bytes[k] = 0;
+    }
+}
+
+void timing_begin(hgm_ctx* c, int cls, hipEvent_t* start) {
+    *start = nullptr;
+    if (!c->timing.on || cls < 0 || cls >= KC_N) return;
+    *start = c->timing.get();
+    HGM_HIP(hipEventRecord(*start, c->stream));
+}
+void timing_end(hgm_ctx* c, int cls, hipEvent_t start, double bytes) {
+    if (!start) return;
+    hipEvent_t stop = c->timing.get();
+    HGM_HIP(hipEventRecord(stop, c->stream));
+    c->timing.ev[cls].push_back({start, stop});
+    c->timing.bytes[cls] += bytes;
+}
+
+static void ensure_stage(hgm_ctx* c, size_t bytes) {
+    if (bytes <= c->hstage_bytes) return;
+    if (c->hstage) (void)hipHostFree(c->hstage);
+    c->hstage = nullptr;
+    size_t nb = bytes < 4096 ? 4096 : bytes;
+    HGM_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->hstage), nb, hipHostMallocDefault));
+    c->hstage_bytes = nb;
+}
+
+void Reader::go() {
+    size_t tot = 0;
+    for (auto& it : items) tot += (it.bytes + 15) / 16 * 16;
+    ensure_stage(c, tot);
+    char* h = reinterpret_cast<char*>(c->hstage);
+    size_t off = 0;
+    for (auto& it : items) {
+        if (it.bytes) HGM_HIP(hipMemcpyAsync(h + off, it.dev, it.bytes, hipMemcpyDeviceToHost, c->stream));
+        off += (it.bytes + 15) / 16 * 16;
+    }
+    HGM_HIP(hipStreamSynchronize(c->stream));
+    off = 0;
+    for (auto& it : items) {
+        if (it.bytes) std::memcpy(it.host, h + off, it.bytes);
+        off += (it.bytes + 15) / 16 * 16;
+    }
+    items.clear();
+}
+
+void h2d(hgm_ctx* c, void* dev, const void* host, size_t bytes) {
+    if (bytes == 0) return;
+    // pageable source: hipMemcpyAsync stages it before returning, so the host buffer may be reused
+    HGM_HIP(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, c->stream));
+}
+
+void read_scalars(hgm_ctx* c, int first, int count) {
+    HGM_HIP(hipMemcpyAsync(c->hscal + first, c->dscal + first, sizeof(double) * count, hipMemcpyDeviceToHost,
+                           c->stream));
+    HGM_HIP(hipStreamSynchronize(c->stream));
+}
+
+void sync(hgm_ctx* c) { HGM_HIP(hipStreamSynchronize(c->stream)); }
+
+template <typename T>
+static void allreduce_t(hgm_ctx* c, T* dev, int64_t count, ncclDataType_t dt) {
+    if (c->world <= 1 || count <= 0) return;
+    if (c->nccl) {
+        if (ncclAllReduce(dev, dev, (size_t)count, dt, ncclSum, c->nccl, c->stream) != ncclSuccess)
+            throw Error{HGM_E_COMM, "ncclAllReduce failed"};
+        return;
+    }
+    if (!c->host_ar) throw Error{HGM_E_COMM, "world > 1 but no communicator"};
+    // host all-reduce hook (shard emulation / tests): always exchanged as doubles
+    ensure_stage(c, sizeof(double) * count + sizeof(T) * count);
+    double* h = c->hstage;
+    if (sizeof(T) == sizeof(double)) {
+        HGM_HIP(hipMemcpyAsync(h, dev, sizeof(double) * count, hipMemcpyDeviceToHost, c->stream));
+        HGM_HIP(hipStreamSynchronize(c->stream));
+        if (c->host_ar(h, count, c->host_ar_user) != 0) throw Error{HGM_E_COMM, "host all-reduce failed"};
+        HGM_HIP(hipMemcpyAsync(dev, h, sizeof(double) * count, hipMemcpyHostToDevice, c->stream));
+        HGM_HIP(hipStreamSynchronize(c->stream));
+    } else {
+        std::vector<T> tmp(count);
+        HGM_HIP(hipMemcpyAsync(tmp.data(), dev, sizeof(T) * count, hipMemcpyDeviceToHost, c->stream));
+        HGM_HIP(hipStreamSynchronize(c->stream));
+        for (int64_t i = 0; i < count; ++i) h[i] = (double)tmp[i];
+        if (c->host_ar(h, count, c->host_ar_user) != 0) throw Error{HGM_E_COMM, "host all-reduce failed"};
+        for (int64_t i = 0; i < count; ++i) tmp[i] = (T)h[i];
+        HGM_HIP(hipMemcpyAsync(dev, tmp.data(), sizeof(T) * count, hipMemcpyHostToDevice, c->stream));
+        HGM_HIP(hipStreamSynchronize(c->stream));
+    }
+}
+void allreduce(hgm_ctx* c, double* dev, int64_t count) { allreduce_t<double>(c, dev, count, ncclDouble); }
+void allreduce(hgm_ctx* c, float* dev, int64_t count) { allreduce_t<float>(c, dev, count, ncclFloat); }
+
+}  // namespace hgm
+
+using namespace hgm;
+
+#define HGM_TRY(ctx, body)                                      \
+    try {                                                       \
+        body;                                                   \
+    } catch (const hgm::Error& e) {                             \
+        if (ctx) (ctx)->err = e.msg;                            \
+        return e.code;                                          \
+    } catch (const std::exception& e) {                         \
+        if (ctx) (ctx)->err = e.what();                         \
+        return HGM_E_HIP;                                       \
+    }
+
+static int ctx_init(hgm_ctx* c, int device) {
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess) return HGM_E_HIP;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return HGM_E_HIP;
+    if (hipMalloc(reinterpret_cast<void**>(&c->dscal), sizeof(double) * NSCAL) != hipSuccess) return HGM_E_NOMEM;
+    if (hipMemset(c->dscal, 0, sizeof(double) * NSCAL) != hipSuccess) return HGM_E_HIP;
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->hscal), sizeof(double) * NSCAL, hipHostMallocDefault) !=
+        hipSuccess)
+        return HGM_E_NOMEM;
+    return HGM_OK;
+}
+
+extern "C" {
+
+HGM_API int hgm_version(void) { return HGM_VERSION; }
+
+HGM_API int hgm_device_count(int* count) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    if (count) *count = n;
+    return HGM_OK;
+}
+
+HGM_API int hgm_ctx_create(int device, hgm_ctx** out) {
+    if (!out) return HGM_E_ARG;
+    *out = nullptr;
+    hgm_ctx* c = new hgm_ctx();
+    int st = ctx_init(c, device);
+    if (st != HGM_OK) {
+        hgm_ctx_destroy(c);
+        return st;
+    }
+    *out = c;
+    return HGM_OK;
+}
+
+HGM_API int hgm_comm_unique_id(void* id_out) {
+    if (!id_out) return HGM_E_ARG;
+    static_assert(sizeof(ncclUniqueId) <= HGM_UNIQUE_ID_BYTES, "unique id size");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return HGM_E_COMM;
+    std::memset(id_out, 0, HGM_UNIQUE_ID_BYTES);
+    std::memcpy(id_out, &id, sizeof(id));
+    return HGM_OK;
+}
+
+HGM_API int hgm_ctx_create_dist(int device, int rank, int world, const void* unique_id, hgm_ctx** out) {
+    if (!out || !unique_id || world < 1 || rank < 0 || rank >= world) return HGM_E_ARG;
+    int st = hgm_ctx_create(device, out);
+    if (st != HGM_OK) return st;
+    hgm_ctx* c = *out;
+    c->rank = rank;
+    c->world = world;
+    if (world > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, unique_id, sizeof(id));
+        if (ncclCommInitRank(&c->nccl, world, id, rank) != ncclSuccess) {
+            c->nccl = nullptr;
+            hgm_ctx_destroy(c);
+            *out = nullptr;
+            return HGM_E_COMM;
+        }
+    }
+    return HGM_OK;
+}
+
+HGM_API int hgm_ctx_set_host_allreduce(hgm_ctx* c, int rank, int world, hgm_allreduce_fn fn, void* user) {
+    if (!c || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn)) return HGM_E_ARG;
+    c->rank = rank;
+    c->world = world;
+    c->host_ar = fn;
+    c->host_ar_user = user;
+    return HGM_OK;
+}
+
+HGM_API void hgm_ctx_destroy(hgm_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->nccl) ncclCommDestroy(c->nccl);
+    c->timing.clear();
+    for (auto e : c->timing.pool) (void)hipEventDestroy(e);
+    c->ws.clear();
+    if (c->dscal) (void)hipFree(c->dscal);
+    if (c->hscal) (void)hipHostFree(c->hscal);
+    if (c->hstage) (void)hipHostFree(c->hstage);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+HGM_API const char* hgm_last_error(const hgm_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+HGM_API int hgm_ctx_synchronize(hgm_ctx* c) {
+    if (!c) return HGM_E_ARG;
+    HGM_TRY(c, sync(c));
+    return HGM_OK;
+}
+
+HGM_API void* hgm_ctx_stream(hgm_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+HGM_API int hgm_ctx_rank(const hgm_ctx* c, int* rank, int* world) {
+    if (!c) return HGM_E_ARG;
+    if (rank) *rank = c->rank;
+    if (world) *world = c->world;
+    return HGM_OK;
+}
+
+// ---- matrices ----------------------------------------------------------------
+HGM_API int hgm_mat_create_csr(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, const int64_t* row_ptr,
+                               const int32_t* col_idx, const double* val, int dtype, hgm_mat** out) {
+    if (!c || !out || rows < 0 || cols < 0 || nnz < 0 || !row_ptr || (nnz > 0 && (!col_idx || !val)))
+        return HGM_E_ARG;
+    if (dtype != HGM_F64 && dtype != HGM_F32) return HGM_E_ARG;
+    if (row_ptr[0] != 0 || row_ptr[rows] != nnz) {
+        c->err = "row_ptr must start at 0 and end at nnz";
+        return HGM_E_ARG;
+    }
+    *out = nullptr;
+    hgm_mat* M = nullptr;
+    HGM_TRY(c, {
+        HGM_HIP(hipSetDevice(c->device));
+        M = mat_alloc(c, rows, cols, nnz, dtype);
+        HGM_HIP(hipMemcpyAsync(M->rp, row_ptr, sizeof(int64_t) * (rows + 1), hipMemcpyHostToDevice, c->stream));
+        if (nnz > 0) {
+            HGM_HIP(hipMemcpyAsync(M->ci, col_idx, sizeof(int32_t) * nnz, hipMemcpyHostToDevice, c->stream));
+            if (dtype == HGM_F64) {
+                HGM_HIP(hipMemcpyAsync(M->val, val, sizeof(double) * nnz, hipMemcpyHostToDevice, c->stream));
+            } else {
+                double* tmp = c->buf<double>("mat_f64", nnz);
+                HGM_HIP(hipMemcpyAsync(tmp, val, sizeof(double) * nnz, hipMemcpyHostToDevice, c->stream));
+                convert<float>(c, nnz, tmp, reinterpret_cast<float*>(M->val));
+            }
+        }
+        HGM_HIP(hipStreamSynchronize(c->stream));
+    });
+    *out = M;
+    return HGM_OK;
+}
+
+HGM_API int hgm_mat_create_csc(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, const int64_t* jc,
+                               const int64_t* ir, const double* pr, int dtype, hgm_mat** out) {
+    if (!c || !out || !jc || (nnz > 0 && (!ir || !pr))) return HGM_E_ARG;
+    // CSC of M (rows x cols) == CSR of M^T (cols x rows); build M by a device transpose
+    std::vector<int32_t> ci(nnz > 0 ? nnz : 1);
+    for (int64_t i = 0; i < nnz; ++i) {
+        if (ir[i] < 0 || ir[i] >= rows) {
+            c->err = "ir index out of range";
+            return HGM_E_ARG;
+        }
+        ci[i] = (int32_t)ir[i];
+    }
+    hgm_mat* Mt = nullptr;
+    int st = hgm_mat_create_csr(c, cols, rows, nnz, jc, ci.data(), pr, dtype, &Mt);
+    if (st != HGM_OK) return st;
+    st = hgm_mat_transpose(c, Mt, out);
+    hgm_mat_destroy(Mt);
+    return st;
+}
+
+HGM_API int hgm_mat_transpose(hgm_ctx* c, const hgm_mat* in, hgm_mat** out) {
+    if (!c || !in || !out) return HGM_E_ARG;
+    *out = nullptr;
+    HGM_TRY(c, *out = transpose(c, in));
+    return HGM_OK;
+}
+
+HGM_API int hgm_mat_create_siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype, hgm_mat** out) {
+    if (!c || !out) return HGM_E_ARG;
+    *out = nullptr;
+    HGM_TRY(c, *out = siddon(c, N, n_angles, det_offset, dtype));
+    return HGM_OK;
+}
+
+HGM_API int hgm_mat_info(const hgm_mat* M, int64_t* rows, int64_t* cols, int64_t* nnz, int* dtype) {
+    if (!M) return HGM_E_ARG;
+    if (rows) *rows = M->rows;
+    if (cols) *cols = M->cols;
+    if (nnz) *nnz = M->nnz;
+    if (dtype) *dtype = M->dtype;
+    return HGM_OK;
+}
+
+HGM_API int hgm_mat_download(hgm_ctx* c, const hgm_mat* M, int64_t* row_ptr, int32_t* col_idx, double* val) {
+    if (!c || !M) return HGM_E_ARG;
+    HGM_TRY(c, {
+        if (row_ptr) HGM_HIP(hipMemcpy(row_ptr, M->rp, sizeof(int64_t) * (M->rows + 1), hipMemcpyDeviceToHost));
+        if (col_idx && M->nnz) HGM_HIP(hipMemcpy(col_idx, M->ci, sizeof(int32_t) * M->nnz, hipMemcpyDeviceToHost));
+        if (val && M->nnz) {
+            if (M->dtype == HGM_F64) {
+                HGM_HIP(hipMemcpy(val, M->val, sizeof(double) * M->nnz, hipMemcpyDeviceToHost));
+            } else {
+                double* tmp = c->buf<double>("mat_f64", M->nnz);
+                convert_back<float>(c, M->nnz, reinterpret_cast<const float*>(M->val), tmp);
+                HGM_HIP(hipStreamSynchronize(c->stream));
+                HGM_HIP(hipMemcpy(val, tmp, sizeof(double) * M->nnz, hipMemcpyDeviceToHost));
+            }
+        }
+    });
+    return HGM_OK;
+}
+
+HGM_API void hgm_mat_destroy(hgm_mat* M) {
+    if (!M) return;
+    if (M->ctx && M->ctx->stream) (void)hipStreamSynchronize(M->ctx->stream);
+    mat_free(M);
+}
+
+HGM_API int hgm_spmv(hgm_ctx* c, const hgm_mat* A, const void* x, void* y) {
+    if (!c || !A || !x || !y) return HGM_E_ARG;
+    HGM_TRY(c, {
+        if (A->dtype == HGM_F64)
+            spmv<double>(c, A, (const double*)x, (double*)y, EPI_NONE, 0.0, nullptr, KC_SPMV_A);
+        else
+            spmv<float>(c, A, (const float*)x, (float*)y, EPI_NONE, 0.0f, nullptr, KC_SPMV_A);
+    });
+    return HGM_OK;
+}
+
+HGM_API int hgm_dev_alloc(hgm_ctx* c, int64_t bytes, void** ptr) {
+    if (!c || !ptr || bytes < 0) return HGM_E_ARG;
+    if (hipSetDevice(c->device) != hipSuccess) return HGM_E_HIP;
+    if (hipMalloc(ptr, bytes > 0 ? bytes : 1) != hipSuccess) {
+        c->err = "hipMalloc failed";
+        return HGM_E_NOMEM;
+    }
+    return HGM_OK;
+}
+HGM_API int hgm_dev_free(hgm_ctx* c, void* ptr) {
+    if (!c) return HGM_E_ARG;
+    if (ptr) (void)hipFree(ptr);
+    return HGM_OK;
+}
+HGM_API int hgm_memcpy_h2d(hgm_ctx* c, void* dst, const void* src, int64_t bytes) {
+    if (!c) return HGM_E_ARG;
+    HGM_TRY(c, {
+        HGM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+        HGM_HIP(hipStreamSynchronize(c->stream));
+    });
+    return HGM_OK;
+}
+HGM_API int hgm_memcpy_d2h(hgm_ctx* c, void* dst, const void* src, int64_t bytes) {
+    if (!c) return HGM_E_ARG;
+    HGM_TRY(c, {
+        HGM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+        HGM_HIP(hipStreamSynchronize(c->stream));
+    });
+    return HGM_OK;
+}
+
+// ---- solvers ------------------------------------------------------------------
+#define HGM_SOLVE(ctx, expr)                               \
+    do {                                                   \
+        if (!(ctx)) return HGM_E_ARG;                      \
+        int rc_ = HGM_OK;                                  \
+        HGM_TRY(ctx, {                                     \
+            HGM_HIP(hipSetDevice((ctx)->device));          \
+            rc_ = (expr);                                  \
+        });                                                \
+        return rc_;                                        \
+    } while (0)
+
+HGM_API int hgm_hybrid_ab_gmres_rtp_ex(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* B,
+                                       const double* b, const double* xt, double tol, int maxit, double lambda,
+                                       double* x, double* err, double* res, int* niters) {
+    // n-space Arnoldi on B*A + lambda*I with the AQk Gram projected solve (hybrid_ab_gmres_rtp.m)
+    HGM_SOLVE(c, gmres_family(c, GmresSpec{HGM_SIDE_BA, PROJ_ABRTP, true, false}, o, A, B, b, xt, tol, maxit,
+                              lambda, x, err, res, niters));
+}
+HGM_API int hgm_hybrid_ba_gmres_rtp_ex(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* B,
+                                       const double* b, const double* xt, double tol, int maxit, double lambda,
+                                       double* x, double* err, double* res, int* niters) {
+    HGM_SOLVE(c, gmres_family(c, GmresSpec{HGM_SIDE_BA, PROJ_LS, true, true}, o, A, B, b, xt, tol, maxit,
+                              lambda, x, err, res, niters));
+}
+HGM_API int hgm_gmres_bounds_ex(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* B, const double* b,
+                                const double* xt, double tol, int maxit, double lambda, int side, int hybrid,
+                                double* x, double* err, double* res, int* niters) {
+    if (side != HGM_SIDE_AB && side != HGM_SIDE_BA) return HGM_E_ARG;
+    HGM_SOLVE(c, gmres_family(c, GmresSpec{side, hybrid ? PROJ_PTR : PROJ_LS, false, false}, o, A, B, b, xt, tol,
+                              maxit, hybrid ? lambda : 0.0, x, err, res, niters));
+}
+HGM_API int hgm_lsqr_solver_ex(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, const double* b,
+                               const double* xt, double tol, int maxit, double* x, double* err, double* res,
+                               int* niters) {
+    if (A && A->dtype == HGM_F32)
+        HGM_SOLVE(c, lsqr_t<float>(c, o, A, At, b, xt, tol, maxit, false, 0.0, x, err, res, niters));
+    HGM_SOLVE(c, lsqr_t<double>(c, o, A, At, b, xt, tol, maxit, false, 0.0, x, err, res, niters));
+}
+HGM_API int hgm_lsmr_solver_ex(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, const double* b,
+                               const double* xt, double tol, int maxit, double* x, double* eh, double* rh, double* ah,
+                               int* iters) {
+    if (A && A->dtype == HGM_F32)
+        HGM_SOLVE(c, lsmr_t<float>(c, o, A, At, b, xt, tol, maxit, x, eh, rh, ah, iters));
+    HGM_SOLVE(c, lsmr_t<double>(c, o, A, At, b, xt, tol, maxit, x, eh, rh, ah, iters));
+}
+
+HGM_API int hgm_hybrid_ab_gmres_rtp(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b,
+                                    const double* xt, double tol, int maxit, double lambda, double* x, double* err,
+                                    double* res, int* niters) {
+    return hgm_hybrid_ab_gmres_rtp_ex(c, nullptr, A, B, b, xt, tol, maxit, lambda, x, err, res, niters);
+}
+HGM_API int hgm_hybrid_ba_gmres_rtp(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b,
+                                    const double* xt, double tol, int maxit, double lambda, double* x, double* err,
+                                    double* res, int* niters) {
+    return hgm_hybrid_ba_gmres_rtp_ex(c, nullptr, A, B, b, xt, tol, maxit, lambda, x, err, res, niters);
+}
+HGM_API int hgm_gmres_bounds(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b, const double* xt,
+                             double tol, int maxit, double lambda, int side, int hybrid, double* x, double* err,
+                             double* res, int* niters) {
+    return hgm_gmres_bounds_ex(c, nullptr, A, B, b, xt, tol, maxit, lambda, side, hybrid, x, err, res, niters);
+}
+HGM_API int hgm_lsqr_solver(hgm_ctx* c, const hgm_mat* A, const hgm_mat* At, const double* b, const double* xt,
+                            double tol, int maxit, double* x, double* err, double* res, int* niters) {
+    return hgm_lsqr_solver_ex(c, nullptr, A, At, b, xt, tol, maxit, x, err, res, niters);
+}
+HGM_API int hgm_lsmr_solver(hgm_ctx* c, const hgm_mat* A, const hgm_mat* At, const double* b, const double* xt,
+                            double tol, int maxit, double* x, double* eh, double* rh, double* ah, int* iters) {
+    return hgm_lsmr_solver_ex(c, nullptr, A, At, b, xt, tol, maxit, x, eh, rh, ah, iters);
+}
+HGM_API int hgm_hybrid_lsqr_solver(hgm_ctx* c, const hgm_mat* A, const hgm_mat* At, const double* b,
+                                   const double* xt, double tol, int maxit, double lambda, double* x, double* err,
+                                   double* res, int* niters) {
+    if (A && A->dtype == HGM_F32)
+        HGM_SOLVE(c, lsqr_t<float>(c, nullptr, A, At, b, xt, tol, maxit, true, lambda, x, err, res, niters));
+    HGM_SOLVE(c, lsqr_t<double>(c, nullptr, A, At, b, xt, tol, maxit, true, lambda, x, err, res, niters));
+}
+HGM_API int hgm_hybrid_lsmr_solver(hgm_ctx* c, const hgm_mat* A, const hgm_mat* At, const double* b,
+                                   const double* xt, double tol, int maxit, double lambda, double* x, double* err,
+                                   double* res, int* niters) {
+    HGM_SOLVE(c, hybrid_lsmr(c, nullptr, A, At, b, xt, tol, maxit, lambda, x, err, res, niters));
+}
+
+HGM_API int hgm_arnoldi(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b, int k, int side,
+                        double breakdown_tol, int orth, double* H, double* beta, int* kdone) {
+    if (side != HGM_SIDE_AB && side != HGM_SIDE_BA) return HGM_E_ARG;
+    HGM_SOLVE(c, arnoldi(c, A, B, b, k, side, breakdown_tol, orth, H, beta, kdone));
+}
+
+HGM_API int hgm_gcv_from_H(const double* H, int k, double beta, double lambda, double trace_m, double* gcv) {
+    if (!H || !gcv || k < 1) return HGM_E_ARG;
+    *gcv = dense::gcv_from_H(H, k + 1, k, beta, lambda, trace_m);
+    return HGM_OK;
+}
+
+HGM_API int hgm_gcv_function(hgm_ctx* c, double lambda, const hgm_mat* A, const hgm_mat* B, const double* b,
+                             int64_t m, int k_gcv, int side, double* gcv) {
+    if (!c || !gcv || !A || k_gcv < 1) return HGM_E_ARG;
+    std::vector<double> H((size_t)(k_gcv + 1) * k_gcv);
+    double beta = 0;
+    int kd = 0;
+    int st = hgm_arnoldi(c, A, B, b, k_gcv, side, 1e-12, HGM_MGS, H.data(), &beta, &kd);
+    if (st != HGM_OK) return st;
+    // gcv_function.m:33 k = size(H,2) = k_gcv; trace term m ('ab') or n ('ba') (:46-50)
+    const double trace_m = side == HGM_SIDE_AB ? (double)m : (double)A->cols * 1.0;
+    double tm = trace_m;
+    if (side == HGM_SIDE_BA && c->world > 1) {
+        double nloc = (double)A->cols;
+        std::vector<double> v{nloc};
+        HGM_TRY(c, {
+            double* d = reinterpret_cast<double*>(c->dscal) + 100;
+            HGM_HIP(hipMemcpyAsync(d, v.data(), sizeof(double), hipMemcpyHostToDevice, c->stream));
+            allreduce(c, d, 1);
+            HGM_HIP(hipMemcpyAsync(v.data(), d, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+            HGM_HIP(hipStreamSynchronize(c->stream));
+        });
+        tm = v[0];
+    }
+    *gcv = dense::gcv_from_H(H.data(), k_gcv + 1, k_gcv, beta, lambda, tm);
+    return HGM_OK;
+}
+
+HGM_API int hgm_gcv_fminbnd(const double* H, int k, double beta, double trace_m, double lo, double hi, double tolx,
+                            double* lambda_opt, double* gcv_opt) {
+    if (!H || k < 1 || !lambda_opt || !(hi > lo)) return HGM_E_ARG;
+    *lambda_opt = dense::gcv_fminbnd(H, k, beta, trace_m, lo, hi, tolx, gcv_opt);
+    return HGM_OK;
+}
+
+HGM_API int hgm_kernel_timing(hgm_ctx* c, int enable) {
+    if (!c) return HGM_E_ARG;
+    HGM_TRY(c, {
+        sync(c);
+        c->timing.clear();
+        c->timing.on = enable != 0;
+    });
+    return HGM_OK;
+}
+
+HGM_API int hgm_kernel_timing_read(hgm_ctx* c, int cls, double* total_ms, int64_t* calls, double* bytes) {
+    if (!c || cls < 0 || cls >= KC_N) return HGM_E_ARG;
+    HGM_TRY(c, {
+        sync(c);
+        double tot = 0;
+        for (auto& pr : c->timing.ev[cls]) {
+            float ms = 0;
+            HGM_HIP(hipEventElapsedTime(&ms, pr.first, pr.second));
+            tot += ms;
+        }
+        if (total_ms) *total_ms = tot;
+        if (calls) *calls = (int64_t)c->timing.ev[cls].size();
+        if (bytes) *bytes = c->timing.bytes[cls];
+    });
+    return HGM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,176 @@
+// Internal declarations of libhgmres (MI355X / gfx950).  Not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "hgmres.h"
+
+namespace hgm {
+
+struct Error {
+    int code;
+    std::string msg;
+};
+
+#define HGM_HIP(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            throw ::hgm::Error{HGM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)}; \
+    } while (0)
+
+#define HGM_REQUIRE(cond, msg)                                \
+    do {                                                      \
+        if (!(cond)) throw ::hgm::Error{HGM_E_ARG, (msg)};    \
+    } while (0)
+
+constexpr int BS = 256;              // threads per block (4 waves of 64)
+constexpr int MAX_PARTS = 1024;      // max blocks of a partial-sum reduction
+constexpr int NSCAL = 512;           // device scalar slots per context
+
+// Device allocation that grows on demand and is reused across solves.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t b);
+    void release();
+    ~DevBuf() { release(); }
+};
+
+// Kernel classes timed by hgm_kernel_timing (bench roofline).
+enum KClass { KC_SPMV_A = 0, KC_SPMV_B = 1, KC_MGS = 2, KC_N = 3 };
+
+struct Timing {
+    bool on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[KC_N];
+    double bytes[KC_N] = {0, 0, 0};
+    std::vector<hipEvent_t> pool;
+    hipEvent_t get();
+    void clear();
+};
+
+}  // namespace hgm
+
+struct hgm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int rank = 0, world = 1;
+    ncclComm_t nccl = nullptr;
+    hgm_allreduce_fn host_ar = nullptr;
+    void* host_ar_user = nullptr;
+    std::string err;
+    std::map<std::string, hgm::DevBuf> ws;   // named workspace buffers
+    double* dscal = nullptr;                  // device scalar slots
+    double* hscal = nullptr;                  // pinned host mirror
+    double* hstage = nullptr;                 // pinned host staging (allreduce / small copies)
+    size_t hstage_bytes = 0;
+    hgm::Timing timing;
+
+    template <typename T>
+    T* buf(const std::string& name, size_t count) {
+        auto& b = ws[name];
+        b.ensure(count * sizeof(T) + 256);
+        return reinterpret_cast<T*>(b.p);
+    }
+};
+
+struct hgm_mat {
+    hgm_ctx* ctx = nullptr;
+    int64_t rows = 0, cols = 0, nnz = 0;
+    int dtype = HGM_F64;
+    int64_t* rp = nullptr;   // rows+1
+    int32_t* ci = nullptr;   // nnz
+    void* val = nullptr;     // nnz (double or float)
+    int group = 64;          // lanes per row in the SpMV kernel
+    double fro = -1.0;       // cached ||M||_F (lsmr_solver.m:71 is loop-invariant)
+};
+
+namespace hgm {
+
+// ---------------- kernels (kernels.hip) ----------------
+enum Epi { EPI_NONE = 0, EPI_ADD = 1, EPI_SUB = 2, EPI_RSUB = 3 };
+
+int pick_group(int64_t rows, int64_t nnz);
+// y = epi(M x): EPI_ADD: t + a*z ; EPI_SUB: t - a*z ; EPI_RSUB: z - t  (two roundings, no FMA)
+template <typename T>
+void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, int kclass);
+template <typename T>
+void epilogue(hgm_ctx* c, int64_t n, T* y, int epi, T a, const T* z);
+
+int parts_for(int64_t n);
+// local reductions: write result to *out_dev (device)
+template <typename T> void dot(hgm_ctx* c, int64_t n, const T* a, const T* b, T* out_dev);
+template <typename T> void sumsq(hgm_ctx* c, int64_t n, const T* a, T* out_dev);
+template <typename T> void sumsq_diff(hgm_ctx* c, int64_t n, const T* a, const T* b, T* out_dev);
+// out[j] = Q(:,j)' * w, j < ncols (local)
+template <typename T>
+void multidot(hgm_ctx* c, int64_t n, int ncols, const T* Q, int64_t ldq, const T* w, T* out_dev);
+
+// MGS sweep of v = Q(:,kk+1) against Q(:,0..kk); writes Hcol[0..kk+1] (device) and
+// normalises Q(:,kk+1) unless H(kk+1,kk) == 0.  dist: n-vectors sharded (scalar all-reduce
+// per pass).  kclass timing under KC_MGS.
+template <typename T>
+void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist);
+template <typename T>
+void cgs2(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist);
+
+// x = Q(:,0:k) * y  (mode 0) ; x = x - Q*y (mode 1)
+template <typename T>
+void gemv(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y_dev, T* x, int mode);
+template <typename T> void div_scalar(hgm_ctx* c, int64_t n, const T* in, T* out, T s);
+template <typename T> void lsqr_update(hgm_ctx* c, int64_t n, T* x, T* w, const T* v, T a, T b);
+template <typename T>
+void lsmr_update(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, const T* v, T c_hbar, T c_x, T c_h,
+                 bool first);
+template <typename T> void fill(hgm_ctx* c, int64_t n, T* x, T v);
+template <typename T> void convert(hgm_ctx* c, int64_t n, const double* in, T* out);
+template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, double* out);
+template <typename T> void fro2(hgm_ctx* c, const hgm_mat* M, double* out_dev);
+
+// ---------------- operators (ops.hip) ----------------
+hgm_mat* mat_alloc(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, int dtype);
+void mat_free(hgm_mat* M);
+hgm_mat* transpose(hgm_ctx* c, const hgm_mat* M);
+hgm_mat* siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype);
+
+// ---------------- comm / scalars (capi.cpp) ----------------
+void allreduce(hgm_ctx* c, double* dev, int64_t count);
+void allreduce(hgm_ctx* c, float* dev, int64_t count);
+// batched small device->host reads behind one stream synchronisation
+struct Reader {
+    hgm_ctx* c;
+    struct Item { void* host; const void* dev; size_t bytes; };
+    std::vector<Item> items;
+    explicit Reader(hgm_ctx* cc) : c(cc) {}
+    void add(void* host, const void* dev, size_t bytes) { items.push_back({host, dev, bytes}); }
+    void go();
+};
+void h2d(hgm_ctx* c, void* dev, const void* host, size_t bytes);
+void read_scalars(hgm_ctx* c, int first, int count);   // dscal -> hscal (sync)
+void sync(hgm_ctx* c);
+void timing_begin(hgm_ctx* c, int cls, hipEvent_t* start);
+void timing_end(hgm_ctx* c, int cls, hipEvent_t start, double bytes);
+
+// ---------------- dense host LA (dense.cpp) ----------------
+namespace dense {
+// MATLAB mldivide for square M (col-major n x n): symmetric + positive diagonal ->
+// Cholesky (LU fallback if not PD); otherwise LU with partial pivoting.
+void mldivide_square(int n, const double* M, const double* b, double* x);
+// MATLAB mldivide for rectangular m x n (m > n): Householder QR with column pivoting.
+void qr_ls(int m, int n, const double* M, const double* b, double* x);
+// singular values of a square n x n matrix (one-sided Jacobi), descending.
+void svd_values(int n, const double* M, double* s);
+double gcv_from_H(const double* H, int ldh, int k, double beta, double lambda, double trace_m);
+// MATLAB fminbnd (Brent / Forsythe-Malcolm-Moler fmin) of gcv_from_H over [lo, hi].
+double gcv_fminbnd(const double* H, int k, double beta, double trace_m, double lo, double hi,
+                   double tolx, double* gopt);
+}  // namespace dense
+
+}  // namespace hgm

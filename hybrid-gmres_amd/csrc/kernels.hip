@@ -1,0 +1,533 @@
+// HIP kernels of the Arnoldi/GMRES + Golub-Kahan inner loop, written for gfx950 (CDNA4).
+//
+// Design:
+//  * SpMV: CSR, one G-lane group per row (G = 64 -> one wave per row for the long
+//    ray-major rows of A; G = 8..32 for the short pixel-major rows of B / A^T), loads
+//    of val/col coalesced inside a group, products summed per lane then reduced with a
+//    fixed xor-butterfly (deterministic, no atomics).  Epilogues of the reference's
+//    operator closures are fused into the store: `B*(A*v) + lambda*v`
+//    (hybrid_*_rtp.m:6), `A*v - alpha*u` (lsqr_solver.m:22), `A'*u - beta*v`
+//    (lsqr_solver.m:26) and `b - A*x` (hybrid_*_rtp.m:32/35), each with MATLAB's two
+//    roundings (the file is compiled with -ffp-contract=off).
+//  * MGS (hybrid_*_rtp.m:20-26): one launch per Gram-Schmidt pass j fusing
+//    axpy_j (v -= h_j q_j) with the inner product of the NEXT column (q_{j+1}' v).  The
+//    grid-wide sum of pass j's block partials is re-reduced, in a fixed order, by
+//    every block of pass j+1 (identical bits in every block), so no separate reduce
+//    launch and no host round trip is needed between passes.
+//  * All reductions: per-lane sums -> wave butterfly -> 4-wave LDS sum in fixed order.
+#include "internal.h"
+
+namespace hgm {
+
+template <typename T> struct V2;
+template <> struct V2<double> { using t = double2; };
+template <> struct V2<float> { using t = float2; };
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// Block (256 threads) sum, result broadcast to every thread.  Fixed order.
+template <typename T>
+__device__ __forceinline__ T block_sum_all(T v, T* sh) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    T r = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+    __syncthreads();
+    return r;
+}
+
+// Sum of np partials (np <= MAX_PARTS) — same bits in every block that calls it.
+template <typename T>
+__device__ __forceinline__ T reduce_parts(const T* __restrict__ p, int np, T* sh) {
+    T a = 0;
+    for (int i = threadIdx.x; i < np; i += BS) a += p[i];
+    return block_sum_all(a, sh);
+}
+
+int parts_for(int64_t n) {
+    int64_t nb = (n + 2 * BS * 8 - 1) / (2 * BS * 8);   // >= 8 element pairs per thread
+    if (nb < 1) nb = 1;
+    if (nb > MAX_PARTS) nb = MAX_PARTS;
+    return (int)nb;
+}
+
+// ------------------------------------------------------------------------------
+// SpMV
+// ------------------------------------------------------------------------------
+template <typename T, int EPI>
+__device__ __forceinline__ T apply_epi(T t, T a, const T* __restrict__ z, int64_t i) {
+    if (EPI == EPI_ADD) { T s = a * z[i]; return t + s; }
+    if (EPI == EPI_SUB) { T s = a * z[i]; return t - s; }
+    if (EPI == EPI_RSUB) return z[i] - t;
+    return t;
+}
+
+template <typename T, int G, int EPI>
+__global__ __launch_bounds__(BS) void k_spmv(int64_t rows, const int64_t* __restrict__ rp,
+                                             const int32_t* __restrict__ ci,
+                                             const T* __restrict__ val, const T* __restrict__ x,
+                                             T* __restrict__ y, T a, const T* __restrict__ z) {
+    constexpr int RPB = BS / G;
+    const int64_t row = (int64_t)blockIdx.x * RPB + threadIdx.x / G;
+    const int gl = threadIdx.x & (G - 1);
+    T a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    if (row < rows) {
+        const int64_t s = rp[row], e = rp[row + 1];
+        int64_t i = s + gl;
+        for (; i + 3 * G < e; i += 4 * G) {
+            const int32_t c0 = ci[i], c1 = ci[i + G], c2 = ci[i + 2 * G], c3 = ci[i + 3 * G];
+            const T v0 = val[i], v1 = val[i + G], v2 = val[i + 2 * G], v3 = val[i + 3 * G];
+            a0 += v0 * x[c0];
+            a1 += v1 * x[c1];
+            a2 += v2 * x[c2];
+            a3 += v3 * x[c3];
+        }
+        for (; i < e; i += G) a0 += val[i] * x[ci[i]];
+    }
+    T acc = (a0 + a1) + (a2 + a3);
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    if (gl == 0 && row < rows) y[row] = apply_epi<T, EPI>(acc, a, z, row);
+}
+
+int pick_group(int64_t rows, int64_t nnz) {
+    const double avg = rows > 0 ? (double)nnz / (double)rows : 0.0;
+    if (avg >= 128) return 64;
+    if (avg >= 40) return 32;
+    if (avg >= 16) return 16;
+    if (avg >= 6) return 8;
+    return 4;
+}
+
+template <typename T, int G>
+static void launch_spmv_g(hipStream_t st, const hgm_mat* M, const T* x, T* y, int epi, T a,
+                          const T* z) {
+    const int64_t nb = (M->rows + (BS / G) - 1) / (BS / G);
+    if (nb == 0) return;
+    const T* val = reinterpret_cast<const T*>(M->val);
+    switch (epi) {
+        case EPI_NONE: k_spmv<T, G, EPI_NONE><<<nb, BS, 0, st>>>(M->rows, M->rp, M->ci, val, x, y, a, z); break;
+        case EPI_ADD: k_spmv<T, G, EPI_ADD><<<nb, BS, 0, st>>>(M->rows, M->rp, M->ci, val, x, y, a, z); break;
+        case EPI_SUB: k_spmv<T, G, EPI_SUB><<<nb, BS, 0, st>>>(M->rows, M->rp, M->ci, val, x, y, a, z); break;
+        default: k_spmv<T, G, EPI_RSUB><<<nb, BS, 0, st>>>(M->rows, M->rp, M->ci, val, x, y, a, z); break;
+    }
+}
+
+template <typename T>
+void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, int kclass) {
+    hipEvent_t t0 = nullptr;
+    timing_begin(c, kclass, &t0);
+    switch (M->group) {
+        case 64: launch_spmv_g<T, 64>(c->stream, M, x, y, epi, a, z); break;
+        case 32: launch_spmv_g<T, 32>(c->stream, M, x, y, epi, a, z); break;
+        case 16: launch_spmv_g<T, 16>(c->stream, M, x, y, epi, a, z); break;
+        case 8: launch_spmv_g<T, 8>(c->stream, M, x, y, epi, a, z); break;
+        default: launch_spmv_g<T, 4>(c->stream, M, x, y, epi, a, z); break;
+    }
+    HGM_HIP(hipGetLastError());
+    // algorithmic bytes: nnz*(s+4) + 8(rows+1) + s*cols + s*rows (+ s*rows epilogue operand)
+    const double s = sizeof(T);
+    double bytes = (double)M->nnz * (s + 4) + 8.0 * (M->rows + 1) + s * M->cols + s * M->rows;
+    if (epi != EPI_NONE) bytes += s * M->rows;
+    timing_end(c, kclass, t0, bytes);
+}
+
+template <typename T, int EPI>
+__global__ __launch_bounds__(BS) void k_epi(int64_t n, T* __restrict__ y, T a, const T* __restrict__ z) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS)
+        y[i] = apply_epi<T, EPI>(y[i], a, z, i);
+}
+
+static int grid_for(int64_t n) {
+    int64_t nb = (n + BS - 1) / BS;
+    if (nb > 4096) nb = 4096;
+    if (nb < 1) nb = 1;
+    return (int)nb;
+}
+
+template <typename T>
+void epilogue(hgm_ctx* c, int64_t n, T* y, int epi, T a, const T* z) {
+    const int g = grid_for(n);
+    switch (epi) {
+        case EPI_ADD: k_epi<T, EPI_ADD><<<g, BS, 0, c->stream>>>(n, y, a, z); break;
+        case EPI_SUB: k_epi<T, EPI_SUB><<<g, BS, 0, c->stream>>>(n, y, a, z); break;
+        case EPI_RSUB: k_epi<T, EPI_RSUB><<<g, BS, 0, c->stream>>>(n, y, a, z); break;
+        default: return;
+    }
+    HGM_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------
+// Reductions
+// ------------------------------------------------------------------------------
+template <typename T, int OP>   // 0: a.b   1: a.a   2: (a-b).(a-b)
+__global__ __launch_bounds__(BS) void k_reduce_partial(int64_t n, const T* __restrict__ a,
+                                                       const T* __restrict__ b,
+                                                       T* __restrict__ parts) {
+    __shared__ T sh[4];
+    T acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+        if (OP == 0) acc += a[i] * b[i];
+        else if (OP == 1) acc += a[i] * a[i];
+        else { T d = a[i] - b[i]; acc += d * d; }
+    }
+    T tot = block_sum_all(acc, sh);
+    if (threadIdx.x == 0) parts[blockIdx.x] = tot;
+}
+
+template <typename T>
+__global__ __launch_bounds__(BS) void k_finalize(const T* __restrict__ parts, int np, T* out) {
+    __shared__ T sh[4];
+    const T r = reduce_parts(parts + (int64_t)blockIdx.x * np, np, sh);
+    if (threadIdx.x == 0) out[blockIdx.x] = r;
+}
+
+template <typename T, int OP>
+static void reduce_to(hgm_ctx* c, int64_t n, const T* a, const T* b, T* out) {
+    const int np = parts_for(n);
+    T* parts = c->buf<T>("red_parts", MAX_PARTS);
+    k_reduce_partial<T, OP><<<np, BS, 0, c->stream>>>(n, a, b, parts);
+    k_finalize<T><<<1, BS, 0, c->stream>>>(parts, np, out);
+    HGM_HIP(hipGetLastError());
+}
+
+template <typename T> void dot(hgm_ctx* c, int64_t n, const T* a, const T* b, T* out) { reduce_to<T, 0>(c, n, a, b, out); }
+template <typename T> void sumsq(hgm_ctx* c, int64_t n, const T* a, T* out) { reduce_to<T, 1>(c, n, a, a, out); }
+template <typename T> void sumsq_diff(hgm_ctx* c, int64_t n, const T* a, const T* b, T* out) { reduce_to<T, 2>(c, n, a, b, out); }
+
+// partial dots of every column j (blockIdx.y) with w
+template <typename T>
+__global__ __launch_bounds__(BS) void k_multidot(int64_t n, const T* __restrict__ Q, int64_t ldq,
+                                                 const T* __restrict__ w, T* __restrict__ parts) {
+    __shared__ T sh[4];
+    const T* q = Q + (int64_t)blockIdx.y * ldq;
+    T acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS)
+        acc += q[i] * w[i];
+    T tot = block_sum_all(acc, sh);
+    if (threadIdx.x == 0) parts[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = tot;
+}
+
+template <typename T>
+void multidot(hgm_ctx* c, int64_t n, int ncols, const T* Q, int64_t ldq, const T* w, T* out) {
+    if (ncols <= 0) return;
+    const int np = parts_for(n);
+    T* parts = c->buf<T>("mdot_parts", (size_t)np * ncols);
+    k_multidot<T><<<dim3(np, ncols), BS, 0, c->stream>>>(n, Q, ldq, w, parts);
+    k_finalize<T><<<ncols, BS, 0, c->stream>>>(parts, np, out);
+    HGM_HIP(hipGetLastError());
+}
+
+template <typename T>
+__global__ __launch_bounds__(BS) void k_fro2(int64_t nnz, const T* __restrict__ v, double* parts) {
+    __shared__ double sh[4];
+    double acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * BS) {
+        const double d = (double)v[i];
+        acc += d * d;
+    }
+    double tot = block_sum_all(acc, sh);
+    if (threadIdx.x == 0) parts[blockIdx.x] = tot;
+}
+
+template <typename T>
+void fro2(hgm_ctx* c, const hgm_mat* M, double* out) {
+    const int np = parts_for(M->nnz);
+    double* parts = c->buf<double>("fro_parts", MAX_PARTS);
+    k_fro2<T><<<np, BS, 0, c->stream>>>(M->nnz, reinterpret_cast<const T*>(M->val), parts);
+    k_finalize<double><<<1, BS, 0, c->stream>>>(parts, np, out);
+    HGM_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------
+// Modified Gram-Schmidt, one fused pass per j (hybrid_*_rtp.m:20-24)
+// MODE 0: acc = q_d . v                       (first inner product, :21 with j = 1)
+// MODE 1: h = H(j-1); v -= h q_a; acc = q_d . v   (:22 for j-1 fused with :21 for j)
+// MODE 2: h = H(k);   v -= h q_a; acc = v . v      (:22 for j = k fused with norm, :24)
+// h comes from the previous pass's block partials (np_in > 0, single GPU) or from a
+// device scalar already all-reduced across ranks (np_in == 0).
+// ------------------------------------------------------------------------------
+template <typename T, int MODE>
+__global__ __launch_bounds__(BS) void k_mgs_pass(int64_t n, const T* __restrict__ qa,
+                                                 const T* __restrict__ qd, T* __restrict__ v,
+                                                 const T* __restrict__ pin, int np_in,
+                                                 const T* hsrc, T* hdst, T* __restrict__ pout) {
+    using T2 = typename V2<T>::t;
+    __shared__ T sh[4];
+    T h = 0;
+    if (MODE != 0) {
+        h = (np_in > 0) ? reduce_parts(pin, np_in, sh) : *hsrc;
+        if (hdst != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *hdst = h;
+    }
+    T acc0 = 0, acc1 = 0;
+    const int64_t n2 = n >> 1;
+    const int64_t stride = (int64_t)gridDim.x * BS;
+    T2* v2 = reinterpret_cast<T2*>(v);
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n2; i += stride) {
+        T2 vv = v2[i];
+        if (MODE != 0) {
+            const T2 qq = reinterpret_cast<const T2*>(qa)[i];
+            const T p0 = h * qq.x, p1 = h * qq.y;
+            vv.x = vv.x - p0;
+            vv.y = vv.y - p1;
+            v2[i] = vv;
+        }
+        if (MODE == 2) {
+            acc0 += vv.x * vv.x;
+            acc1 += vv.y * vv.y;
+        } else {
+            const T2 dd = reinterpret_cast<const T2*>(qd)[i];
+            acc0 += dd.x * vv.x;
+            acc1 += dd.y * vv.y;
+        }
+    }
+    if ((n & 1) && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        const int64_t i = n - 1;
+        T vv = v[i];
+        if (MODE != 0) {
+            const T p0 = h * qa[i];
+            vv = vv - p0;
+            v[i] = vv;
+        }
+        acc0 += (MODE == 2) ? vv * vv : qd[i] * vv;
+    }
+    const T tot = block_sum_all(acc0 + acc1, sh);
+    if (threadIdx.x == 0) pout[blockIdx.x] = tot;
+}
+
+// H(k+1,k) = sqrt(sum v^2);  if nonzero: q_{k+1} = v / H(k+1,k)   (hybrid_*_rtp.m:24-26)
+template <typename T>
+__global__ __launch_bounds__(BS) void k_mgs_normalize(int64_t n, T* __restrict__ v,
+                                                      const T* __restrict__ pin, int np_in,
+                                                      const T* ssrc, T* hdst) {
+    using T2 = typename V2<T>::t;
+    __shared__ T sh[4];
+    const T ss = (np_in > 0) ? reduce_parts(pin, np_in, sh) : *ssrc;
+    const T nrm = sqrt(ss);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *hdst = nrm;
+    if (nrm == 0) return;
+    const int64_t n2 = n >> 1;
+    T2* v2 = reinterpret_cast<T2*>(v);
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n2; i += (int64_t)gridDim.x * BS) {
+        T2 vv = v2[i];
+        vv.x = vv.x / nrm;
+        vv.y = vv.y / nrm;
+        v2[i] = vv;
+    }
+    if ((n & 1) && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) v[n - 1] = v[n - 1] / nrm;
+}
+
+template <typename T>
+void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist) {
+    hipEvent_t t0 = nullptr;
+    timing_begin(c, KC_MGS, &t0);
+    const int np = parts_for(n);
+    T* P = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
+    T* Pb[2] = {P, P + MAX_PARTS};
+    T* v = Q + (int64_t)(kk + 1) * ldq;
+    T* ss = c->buf<T>("mgs_ss", 4);
+    hipStream_t st = c->stream;
+    // pass 0: h_0 partials
+    k_mgs_pass<T, 0><<<np, BS, 0, st>>>(n, nullptr, Q, v, nullptr, 0, nullptr, nullptr, Pb[0]);
+    if (dist) {
+        k_finalize<T><<<1, BS, 0, st>>>(Pb[0], np, Hcol + 0);
+        allreduce(c, Hcol, 1);
+    }
+    for (int j = 1; j <= kk + 1; ++j) {
+        const T* qa = Q + (int64_t)(j - 1) * ldq;
+        T* pin = Pb[(j - 1) & 1];
+        T* pout = Pb[j & 1];
+        const int np_in = dist ? 0 : np;
+        T* hdst = dist ? nullptr : Hcol + (j - 1);
+        if (j <= kk) {
+            const T* qd = Q + (int64_t)j * ldq;
+            k_mgs_pass<T, 1><<<np, BS, 0, st>>>(n, qa, qd, v, pin, np_in, Hcol + (j - 1), hdst, pout);
+            if (dist) {
+                k_finalize<T><<<1, BS, 0, st>>>(pout, np, Hcol + j);
+                allreduce(c, Hcol + j, 1);
+            }
+        } else {
+            k_mgs_pass<T, 2><<<np, BS, 0, st>>>(n, qa, nullptr, v, pin, np_in, Hcol + (j - 1), hdst, pout);
+            if (dist) {
+                k_finalize<T><<<1, BS, 0, st>>>(pout, np, ss);
+                allreduce(c, ss, 1);
+            }
+        }
+    }
+    {
+        T* pin = Pb[(kk + 1) & 1];
+        k_mgs_normalize<T><<<np, BS, 0, st>>>(n, v, pin, dist ? 0 : np, ss, Hcol + kk + 1);
+    }
+    HGM_HIP(hipGetLastError());
+    // algorithmic bytes: (32k+24)n-style count for k+1 = kk+1 columns
+    const double s = sizeof(T);
+    const double bytes = s * n * (2.0 + 4.0 * kk + 3.0 + 2.0);
+    timing_end(c, KC_MGS, t0, bytes);
+}
+
+// ------------------------------------------------------------------------------
+// GEMV over the Krylov basis: x = Q(:,0:k) y  or  x -= Q y
+// ------------------------------------------------------------------------------
+template <typename T, int MODE>
+__global__ __launch_bounds__(BS) void k_gemv(int64_t n, int k, const T* __restrict__ Q, int64_t ldq,
+                                             const T* __restrict__ y, T* __restrict__ x) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+        T s = 0;
+        for (int j = 0; j < k; ++j) s += Q[(int64_t)j * ldq + i] * y[j];
+        if (MODE == 0) x[i] = s;
+        else x[i] = x[i] - s;
+    }
+}
+
+template <typename T>
+void gemv(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T* x, int mode) {
+    int64_t nb = (n + BS - 1) / BS;
+    if (nb > 8192) nb = 8192;
+    if (nb < 1) nb = 1;
+    if (mode == 0) k_gemv<T, 0><<<nb, BS, 0, c->stream>>>(n, k, Q, ldq, y, x);
+    else k_gemv<T, 1><<<nb, BS, 0, c->stream>>>(n, k, Q, ldq, y, x);
+    HGM_HIP(hipGetLastError());
+}
+
+// Classical Gram-Schmidt applied twice (option; C3's MGS vs CGS2 comparison).
+template <typename T>
+__global__ __launch_bounds__(BS) void k_add_store(int k, const T* a, const T* b, T* out) {
+    const int i = threadIdx.x;
+    if (i < k) out[i] = a[i] + b[i];
+}
+
+template <typename T>
+void cgs2(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist) {
+    hipEvent_t t0 = nullptr;
+    timing_begin(c, KC_MGS, &t0);
+    const int k = kk + 1;
+    T* v = Q + (int64_t)k * ldq;
+    T* h1 = c->buf<T>("cgs_h1", k + 8);
+    T* h2 = c->buf<T>("cgs_h2", k + 8);
+    multidot<T>(c, n, k, Q, ldq, v, h1);
+    if (dist) allreduce(c, h1, k);
+    gemv<T>(c, n, k, Q, ldq, h1, v, 1);
+    multidot<T>(c, n, k, Q, ldq, v, h2);
+    if (dist) allreduce(c, h2, k);
+    gemv<T>(c, n, k, Q, ldq, h2, v, 1);
+    k_add_store<T><<<1, BS, 0, c->stream>>>(k, h1, h2, Hcol);
+    T* ss = c->buf<T>("mgs_ss", 4);
+    sumsq<T>(c, n, v, ss);
+    if (dist) allreduce(c, ss, 1);
+    k_mgs_normalize<T><<<parts_for(n), BS, 0, c->stream>>>(n, v, nullptr, 0, ss, Hcol + k);
+    HGM_HIP(hipGetLastError());
+    const double s = sizeof(T);
+    timing_end(c, KC_MGS, t0, s * n * (4.0 * k + 8.0));
+}
+
+// ------------------------------------------------------------------------------
+// Elementwise
+// ------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(BS) void k_div(int64_t n, const T* __restrict__ in, T* __restrict__ out, T s) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS)
+        out[i] = in[i] / s;
+}
+template <typename T> void div_scalar(hgm_ctx* c, int64_t n, const T* in, T* out, T s) {
+    k_div<T><<<grid_for(n), BS, 0, c->stream>>>(n, in, out, s);
+    HGM_HIP(hipGetLastError());
+}
+
+// lsqr_solver.m:40-41:  x = x + (phi/rho) w ;  w = v - (theta/rho) w
+template <typename T>
+__global__ __launch_bounds__(BS) void k_lsqr_update(int64_t n, T* __restrict__ x, T* __restrict__ w,
+                                                    const T* __restrict__ v, T a, T b) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+        const T wi = w[i];
+        const T p = a * wi;
+        x[i] = x[i] + p;
+        const T q = b * wi;
+        w[i] = v[i] - q;
+    }
+}
+template <typename T> void lsqr_update(hgm_ctx* c, int64_t n, T* x, T* w, const T* v, T a, T b) {
+    k_lsqr_update<T><<<grid_for(n), BS, 0, c->stream>>>(n, x, w, v, a, b);
+    HGM_HIP(hipGetLastError());
+}
+
+// lsmr_solver.m:61-67
+template <typename T, bool FIRST>
+__global__ __launch_bounds__(BS) void k_lsmr_update(int64_t n, T* __restrict__ x, T* __restrict__ h,
+                                                    T* __restrict__ hbar, const T* __restrict__ v,
+                                                    T c_hbar, T c_x, T c_h) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+        const T hi = h[i];
+        T hb;
+        if (FIRST) hb = hi;                              // :62  hbar = h
+        else { const T p = c_hbar * hbar[i]; hb = hi - p; }   // :64
+        hbar[i] = hb;
+        const T q = c_x * hb;
+        x[i] = x[i] + q;                                 // :66
+        const T r = c_h * hi;
+        h[i] = v[i] - r;                                 // :67
+    }
+}
+template <typename T>
+void lsmr_update(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, const T* v, T c_hbar, T c_x, T c_h, bool first) {
+    if (first) k_lsmr_update<T, true><<<grid_for(n), BS, 0, c->stream>>>(n, x, h, hbar, v, c_hbar, c_x, c_h);
+    else k_lsmr_update<T, false><<<grid_for(n), BS, 0, c->stream>>>(n, x, h, hbar, v, c_hbar, c_x, c_h);
+    HGM_HIP(hipGetLastError());
+}
+
+template <typename T>
+__global__ __launch_bounds__(BS) void k_fill(int64_t n, T* x, T v) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) x[i] = v;
+}
+template <typename T> void fill(hgm_ctx* c, int64_t n, T* x, T v) {
+    k_fill<T><<<grid_for(n), BS, 0, c->stream>>>(n, x, v);
+    HGM_HIP(hipGetLastError());
+}
+
+template <typename T>
+__global__ __launch_bounds__(BS) void k_convert(int64_t n, const double* in, T* out) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = (T)in[i];
+}
+template <typename T>
+__global__ __launch_bounds__(BS) void k_convert_back(int64_t n, const T* in, double* out) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = (double)in[i];
+}
+template <typename T> void convert(hgm_ctx* c, int64_t n, const double* in, T* out) {
+    k_convert<T><<<grid_for(n), BS, 0, c->stream>>>(n, in, out);
+    HGM_HIP(hipGetLastError());
+}
+template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, double* out) {
+    k_convert_back<T><<<grid_for(n), BS, 0, c->stream>>>(n, in, out);
+    HGM_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------
+// explicit instantiations
+// ------------------------------------------------------------------------------
+#define HGM_INST(T)                                                                            \
+    template void spmv<T>(hgm_ctx*, const hgm_mat*, const T*, T*, int, T, const T*, int);      \
+    template void epilogue<T>(hgm_ctx*, int64_t, T*, int, T, const T*);                        \
+    template void dot<T>(hgm_ctx*, int64_t, const T*, const T*, T*);                           \
+    template void sumsq<T>(hgm_ctx*, int64_t, const T*, T*);                                   \
+    template void sumsq_diff<T>(hgm_ctx*, int64_t, const T*, const T*, T*);                    \
+    template void multidot<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*);        \
+    template void mgs<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool);                       \
+    template void cgs2<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool);                      \
+    template void gemv<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, int);       \
+    template void div_scalar<T>(hgm_ctx*, int64_t, const T*, T*, T);                           \
+    template void lsqr_update<T>(hgm_ctx*, int64_t, T*, T*, const T*, T, T);                   \
+    template void lsmr_update<T>(hgm_ctx*, int64_t, T*, T*, T*, const T*, T, T, T, bool);      \
+    template void fill<T>(hgm_ctx*, int64_t, T*, T);                                           \
+    template void convert<T>(hgm_ctx*, int64_t, const double*, T*);                            \
+    template void convert_back<T>(hgm_ctx*, int64_t, const T*, double*);                       \
+    template void fro2<T>(hgm_ctx*, const hgm_mat*, double*);
+
+HGM_INST(double)
+HGM_INST(float)
+
+}  // namespace hgm

@@ -1,0 +1,293 @@
+// Sparse operator construction on the device (gfx950):
+//  * deterministic CSR transpose (ray-major A <-> pixel-major A^T / MATLAB CSC hand-over),
+//  * parallel-beam Siddon projector generated ray-per-thread directly into CSR
+//    (same geometry and floating-point operation order as
+//    hgmres/problems.py so the two generators agree bit for bit).
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+
+#include "internal.h"
+
+namespace hgm {
+
+hgm_mat* mat_alloc(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, int dtype) {
+    hgm_mat* M = new hgm_mat();
+    M->ctx = c;
+    M->rows = rows;
+    M->cols = cols;
+    M->nnz = nnz;
+    M->dtype = dtype;
+    const size_t vs = dtype == HGM_F32 ? 4 : 8;
+    if (hipMalloc(&M->rp, sizeof(int64_t) * (rows + 1)) != hipSuccess ||
+        hipMalloc(&M->ci, sizeof(int32_t) * (nnz > 0 ? nnz : 1)) != hipSuccess ||
+        hipMalloc(&M->val, vs * (nnz > 0 ? nnz : 1)) != hipSuccess) {
+        mat_free(M);
+        throw Error{HGM_E_NOMEM, "hipMalloc failed for sparse matrix"};
+    }
+    M->group = pick_group(rows, nnz);
+    return M;
+}
+
+void mat_free(hgm_mat* M) {
+    if (!M) return;
+    if (M->rp) (void)hipFree(M->rp);
+    if (M->ci) (void)hipFree(M->ci);
+    if (M->val) (void)hipFree(M->val);
+    delete M;
+}
+
+// --------------------------------------------------------------------------
+// transpose
+// --------------------------------------------------------------------------
+__global__ void k_expand_rows(int64_t rows, const int64_t* __restrict__ rp, int32_t* __restrict__ ridx) {
+    // one wave per row
+    const int64_t row = (int64_t)blockIdx.x * (BS / 64) + threadIdx.x / 64;
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    for (int64_t i = rp[row] + lane; i < rp[row + 1]; i += 64) ridx[i] = (int32_t)row;
+}
+
+__global__ void k_iota(int64_t n, int32_t* out) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = (int32_t)i;
+}
+
+// row pointer of the transpose from the sorted column keys: rp[c] = first index with key >= c
+__global__ void k_bounds(int64_t nnz, int64_t cols, const int32_t* __restrict__ keys, int64_t* __restrict__ rp) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i <= nnz; i += (int64_t)gridDim.x * BS) {
+        const int64_t kprev = (i == 0) ? -1 : (int64_t)keys[i - 1];
+        const int64_t kcur = (i == nnz) ? cols : (int64_t)keys[i];
+        for (int64_t cc = kprev + 1; cc <= kcur; ++cc) rp[cc] = i;
+    }
+}
+
+template <typename T>
+__global__ void k_gather_t(int64_t nnz, const int32_t* __restrict__ perm, const int32_t* __restrict__ ridx,
+                           const T* __restrict__ vin, int32_t* __restrict__ ci_out, T* __restrict__ vout) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * BS) {
+        const int32_t p = perm[i];
+        ci_out[i] = ridx[p];
+        vout[i] = vin[p];
+    }
+}
+
+static int grid_cap(int64_t n) {
+    int64_t g = (n + BS - 1) / BS;
+    if (g > 65536) g = 65536;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+hgm_mat* transpose(hgm_ctx* c, const hgm_mat* M) {
+    HGM_REQUIRE(M->nnz < (int64_t)INT32_MAX, "transpose: nnz must be < 2^31");
+    HGM_REQUIRE(M->cols < (int64_t)INT32_MAX && M->rows < (int64_t)INT32_MAX, "transpose: dims must be < 2^31");
+    hipStream_t st = c->stream;
+    const int64_t nnz = M->nnz;
+    hgm_mat* T = mat_alloc(c, M->cols, M->rows, nnz, M->dtype);
+    if (nnz == 0) {
+        HGM_HIP(hipMemsetAsync(T->rp, 0, sizeof(int64_t) * (T->rows + 1), st));
+        HGM_HIP(hipStreamSynchronize(st));
+        return T;
+    }
+    int32_t *ridx = nullptr, *keys_out = nullptr, *perm_in = nullptr, *perm_out = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    int bits = 1;
+    while ((int64_t(1) << bits) < M->cols) ++bits;
+    try {
+        HGM_HIP(hipMalloc(&ridx, sizeof(int32_t) * nnz));
+        HGM_HIP(hipMalloc(&keys_out, sizeof(int32_t) * nnz));
+        HGM_HIP(hipMalloc(&perm_in, sizeof(int32_t) * nnz));
+        HGM_HIP(hipMalloc(&perm_out, sizeof(int32_t) * nnz));
+        k_expand_rows<<<(M->rows + 3) / 4, BS, 0, st>>>(M->rows, M->rp, ridx);
+        k_iota<<<grid_cap(nnz), BS, 0, st>>>(nnz, perm_in);
+        HGM_HIP(hipGetLastError());
+        // stable LSD radix sort by column keeps row order inside every output row
+        HGM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, M->ci, keys_out, perm_in, perm_out,
+                                                  (int)nnz, 0, bits, st));
+        HGM_HIP(hipMalloc(&tmp, tmp_bytes));
+        HGM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, M->ci, keys_out, perm_in, perm_out,
+                                                  (int)nnz, 0, bits, st));
+        k_bounds<<<grid_cap(nnz + 1), BS, 0, st>>>(nnz, M->cols, keys_out, T->rp);
+        if (M->dtype == HGM_F32)
+            k_gather_t<float><<<grid_cap(nnz), BS, 0, st>>>(nnz, perm_out, ridx, (const float*)M->val, T->ci, (float*)T->val);
+        else
+            k_gather_t<double><<<grid_cap(nnz), BS, 0, st>>>(nnz, perm_out, ridx, (const double*)M->val, T->ci, (double*)T->val);
+        HGM_HIP(hipGetLastError());
+        HGM_HIP(hipStreamSynchronize(st));
+    } catch (...) {
+        (void)hipFree(ridx); (void)hipFree(keys_out); (void)hipFree(perm_in); (void)hipFree(perm_out); (void)hipFree(tmp);
+        mat_free(T);
+        throw;
+    }
+    (void)hipFree(ridx); (void)hipFree(keys_out); (void)hipFree(perm_in); (void)hipFree(perm_out); (void)hipFree(tmp);
+    return T;
+}
+
+// --------------------------------------------------------------------------
+// Siddon parallel-beam projector (mirrors hgmres/problems.py::_siddon_chunk)
+// --------------------------------------------------------------------------
+struct RayGeom {
+    double x0, y0, c, s, tmin, tmax;
+    bool cx, cy, hit;
+};
+
+__device__ __forceinline__ RayGeom ray_geom(int N, double c, double s_, double sd) {
+    RayGeom g;
+    const double half = N / 2.0;
+    g.c = c;
+    g.s = s_;
+    g.x0 = -sd * s_;
+    g.y0 = sd * c;
+    g.cx = fabs(c) > 1e-12;
+    g.cy = fabs(s_) > 1e-12;
+    const double inf = INFINITY;
+    double txmin, txmax, tymin, tymax;
+    if (g.cx) {
+        const double a = ((0.0 - half) - g.x0) / c, b = (((double)N - half) - g.x0) / c;
+        txmin = fmin(a, b); txmax = fmax(a, b);
+    } else {
+        const bool in = fabs(g.x0) < half;
+        txmin = in ? -inf : inf; txmax = in ? inf : -inf;
+    }
+    if (g.cy) {
+        const double a = ((0.0 - half) - g.y0) / s_, b = (((double)N - half) - g.y0) / s_;
+        tymin = fmin(a, b); tymax = fmax(a, b);
+    } else {
+        const bool in = fabs(g.y0) < half;
+        tymin = in ? -inf : inf; tymax = in ? inf : -inf;
+    }
+    g.tmin = fmax(txmin, tymin);
+    g.tmax = fmin(txmax, tymax);
+    g.hit = g.tmin < g.tmax;
+    return g;
+}
+
+// Walk the merged, sorted crossing sequence [tmin, x/y-plane crossings in range, tmax]
+// and emit segments with length > 1e-10 (problems.py: valid = isfinite & L > 1e-10).
+template <bool FILL, typename T>
+__device__ int64_t siddon_walk(int N, const RayGeom& g, int64_t out0, int32_t* ci, T* val) {
+    if (!g.hit) return 0;
+    const double half = N / 2.0;
+    // next in-range crossing of each family in increasing t
+    int kx = 0, dkx = 1, ky = 0, dky = 1;
+    if (g.cx) { if (g.c > 0) { kx = 0; dkx = 1; } else { kx = N; dkx = -1; } }
+    if (g.cy) { if (g.s > 0) { ky = 0; dky = 1; } else { ky = N; dky = -1; } }
+    auto tx_at = [&](int k) { return (((double)k - half) - g.x0) / g.c; };
+    auto ty_at = [&](int k) { return (((double)k - half) - g.y0) / g.s; };
+    // skip crossings below tmin
+    double tx = INFINITY, ty = INFINITY;
+    bool hx = g.cx, hy = g.cy;
+    if (hx) { while (kx >= 0 && kx <= N && !(tx_at(kx) >= g.tmin)) kx += dkx; hx = (kx >= 0 && kx <= N); if (hx) tx = tx_at(kx); }
+    if (hy) { while (ky >= 0 && ky <= N && !(ty_at(ky) >= g.tmin)) ky += dky; hy = (ky >= 0 && ky <= N); if (hy) ty = ty_at(ky); }
+    if (hx && !(tx <= g.tmax)) { hx = false; tx = INFINITY; }
+    if (hy && !(ty <= g.tmax)) { hy = false; ty = INFINITY; }
+    double t0 = g.tmin;
+    int64_t cnt = 0;
+    bool done = false;
+    while (!done) {
+        double t1;
+        if (hx && (!hy || tx <= ty)) {
+            t1 = tx;
+            kx += dkx;
+            hx = (kx >= 0 && kx <= N);
+            if (hx) { tx = tx_at(kx); if (!(tx <= g.tmax)) { hx = false; tx = INFINITY; } }
+        } else if (hy) {
+            t1 = ty;
+            ky += dky;
+            hy = (ky >= 0 && ky <= N);
+            if (hy) { ty = ty_at(ky); if (!(ty <= g.tmax)) { hy = false; ty = INFINITY; } }
+        } else {
+            t1 = g.tmax;
+            done = true;
+        }
+        const double L = t1 - t0;
+        if (L > 1e-10) {
+            if (FILL) {
+                const double mid = 0.5 * (t0 + t1);
+                const double xm = g.x0 + mid * g.c;
+                const double ym = g.y0 + mid * g.s;
+                double fx = floor(xm + half), fy = floor(ym + half);
+                fx = fmin(fmax(fx, 0.0), (double)(N - 1));
+                fy = fmin(fmax(fy, 0.0), (double)(N - 1));
+                const int64_t ix = (int64_t)fx, iy = (int64_t)fy;
+                ci[out0 + cnt] = (int32_t)(ix * N + (N - 1 - iy));
+                val[out0 + cnt] = (T)L;
+            }
+            ++cnt;
+        }
+        t0 = t1;
+    }
+    return cnt;
+}
+
+template <bool FILL, typename T>
+__global__ __launch_bounds__(BS) void k_siddon(int N, int p, int64_t m, const double* __restrict__ cth,
+                                               const double* __restrict__ sth, const double* __restrict__ sdet,
+                                               int64_t* __restrict__ counts, const int64_t* __restrict__ rp,
+                                               int32_t* __restrict__ ci, T* __restrict__ val) {
+    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < m; r += (int64_t)gridDim.x * BS) {
+        const int a = (int)(r / p), d = (int)(r % p);
+        const RayGeom g = ray_geom(N, cth[a], sth[a], sdet[d]);
+        if (FILL) siddon_walk<true, T>(N, g, rp[r], ci, val);
+        else counts[r] = siddon_walk<false, T>(N, g, 0, nullptr, nullptr);
+    }
+}
+
+hgm_mat* siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype) {
+    HGM_REQUIRE(N > 0 && n_angles > 0, "siddon: N and n_angles must be positive");
+    hipStream_t st = c->stream;
+    const int p = (int)std::ceil(std::sqrt(2.0) * N);
+    const int64_t m = (int64_t)p * n_angles;
+    // geometry on the host with C libm (problems.py uses math.cos / math.sin, same libm)
+    std::vector<double> cth(n_angles), sth(n_angles), sdet(p);
+    const double dth = M_PI / n_angles;
+    for (int a = 0; a < n_angles; ++a) {
+        const double th = (double)a * dth;
+        cth[a] = std::cos(th);
+        sth[a] = std::sin(th);
+    }
+    for (int d = 0; d < p; ++d) sdet[d] = ((double)d - (p - 1) / 2.0) + det_offset;
+    double *dc = nullptr, *ds = nullptr, *dd = nullptr;
+    int64_t *counts = nullptr, *rp = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    hgm_mat* M = nullptr;
+    try {
+        HGM_HIP(hipMalloc(&dc, 8 * n_angles));
+        HGM_HIP(hipMalloc(&ds, 8 * n_angles));
+        HGM_HIP(hipMalloc(&dd, 8 * p));
+        HGM_HIP(hipMalloc(&counts, 8 * (m + 1)));
+        HGM_HIP(hipMalloc(&rp, 8 * (m + 1)));
+        HGM_HIP(hipMemcpyAsync(dc, cth.data(), 8 * n_angles, hipMemcpyHostToDevice, st));
+        HGM_HIP(hipMemcpyAsync(ds, sth.data(), 8 * n_angles, hipMemcpyHostToDevice, st));
+        HGM_HIP(hipMemcpyAsync(dd, sdet.data(), 8 * p, hipMemcpyHostToDevice, st));
+        HGM_HIP(hipMemsetAsync(counts, 0, 8 * (m + 1), st));
+        const int g = grid_cap(m);
+        k_siddon<false, double><<<g, BS, 0, st>>>(N, p, m, dc, ds, dd, counts, nullptr, nullptr, nullptr);
+        HGM_HIP(hipGetLastError());
+        HGM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, rp, (int)(m + 1), st));
+        HGM_HIP(hipMalloc(&tmp, tmp_bytes));
+        HGM_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, counts, rp, (int)(m + 1), st));
+        int64_t nnz = 0;
+        HGM_HIP(hipMemcpyAsync(&nnz, rp + m, 8, hipMemcpyDeviceToHost, st));
+        HGM_HIP(hipStreamSynchronize(st));
+        HGM_REQUIRE(nnz < (int64_t)INT32_MAX * 2, "siddon: nnz overflow");
+        M = mat_alloc(c, m, (int64_t)N * N, nnz, dtype);
+        HGM_HIP(hipMemcpyAsync(M->rp, rp, 8 * (m + 1), hipMemcpyDeviceToDevice, st));
+        if (dtype == HGM_F32)
+            k_siddon<true, float><<<g, BS, 0, st>>>(N, p, m, dc, ds, dd, nullptr, M->rp, M->ci, (float*)M->val);
+        else
+            k_siddon<true, double><<<g, BS, 0, st>>>(N, p, m, dc, ds, dd, nullptr, M->rp, M->ci, (double*)M->val);
+        HGM_HIP(hipGetLastError());
+        HGM_HIP(hipStreamSynchronize(st));
+    } catch (...) {
+        (void)hipFree(dc); (void)hipFree(ds); (void)hipFree(dd); (void)hipFree(counts); (void)hipFree(rp); (void)hipFree(tmp);
+        mat_free(M);
+        throw;
+    }
+    (void)hipFree(dc); (void)hipFree(ds); (void)hipFree(dd); (void)hipFree(counts); (void)hipFree(rp); (void)hipFree(tmp);
+    return M;
+}
+
+}  // namespace hgm

@@ -1,0 +1,698 @@
+// Solver loops of the reference, driven from the host over the HIP kernels.
+//
+// Each function follows one reference .m file; the per-line correspondence is
+// cited inline.  Vectors live in HBM for the whole solve; per iteration the host
+// only receives the new Hessenberg column (k+2 doubles) and a few scalars, and
+// sends back the k-vector y of the projected solve.
+//
+// Multi-GPU (ctx->world > 1): the pixel dimension n is sharded
+// (A_g = A(:,P_g), B_g = B(P_g,:)); every `A*v` is followed by an all-reduce of the
+// m-vector, every inner product of n-vectors by a scalar all-reduce; m-vectors
+// (b, u, the AB-side Krylov basis, A*Q columns) are replicated.
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <type_traits>
+#include <vector>
+
+#include "internal.h"
+
+namespace hgm {
+
+namespace {
+
+constexpr double EPSD = std::numeric_limits<double>::epsilon();
+
+inline int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+// Scalar slots in ctx->dscal.
+enum Slot { S_NB = 0, S_NXT = 1, S_BETA = 2, S_RES = 3, S_ERR = 4, S_ALPHA = 5, S_AR = 6, S_FRO = 7,
+            S_AUX = 8, S_AUX2 = 9 };
+
+template <typename T>
+T* dslot(hgm_ctx* c, int i) {
+    return reinterpret_cast<T*>(c->dscal) + i;
+}
+
+inline bool dist_n(hgm_ctx* c) { return c->world > 1; }
+
+// y = A x (+epilogue) where the output is an m-vector assembled across ranks.
+template <typename T>
+void apply_A(hgm_ctx* c, const hgm_mat* A, const T* x, T* y, int epi, T a, const T* z) {
+    if (!dist_n(c)) {
+        spmv<T>(c, A, x, y, epi, a, z, KC_SPMV_A);
+    } else if (epi == EPI_NONE) {
+        spmv<T>(c, A, x, y, EPI_NONE, T(0), nullptr, KC_SPMV_A);
+        allreduce(c, y, A->rows);
+    } else {
+        // z may alias y (u = A*v - alpha*u): assemble in scratch, then apply the epilogue
+        T* tmp = c->buf<T>("ar_tmp", A->rows + 1);
+        spmv<T>(c, A, x, tmp, EPI_NONE, T(0), nullptr, KC_SPMV_A);
+        allreduce(c, tmp, A->rows);
+        epilogue<T>(c, A->rows, tmp, epi, a, z);
+        HGM_HIP(hipMemcpyAsync(y, tmp, sizeof(T) * A->rows, hipMemcpyDeviceToDevice, c->stream));
+    }
+}
+
+// y = B u (+epilogue): B's rows are this rank's pixels, no exchange.
+template <typename T>
+void apply_B(hgm_ctx* c, const hgm_mat* B, const T* u, T* y, int epi, T a, const T* z) {
+    spmv<T>(c, B, u, y, epi, a, z, KC_SPMV_B);
+}
+
+// local sum of squares of an n-vector (+ all-reduce) into slot
+template <typename T>
+void nsumsq(hgm_ctx* c, int64_t n, const T* v, T* slot) {
+    sumsq<T>(c, n, v, slot);
+    if (dist_n(c)) allreduce(c, slot, 1);
+}
+template <typename T>
+void nsumsq_diff(hgm_ctx* c, int64_t n, const T* a, const T* b, T* slot) {
+    sumsq_diff<T>(c, n, a, b, slot);
+    if (dist_n(c)) allreduce(c, slot, 1);
+}
+
+template <typename T>
+T read1(hgm_ctx* c, const T* dev) {
+    T v;
+    Reader r(c);
+    r.add(&v, dev, sizeof(T));
+    r.go();
+    return v;
+}
+
+// Input vector hand-over: device pointer (HGM_DEVICE_PTRS) or host buffer.
+template <typename T>
+const T* stage_in(hgm_ctx* c, const char* name, const double* p, int64_t n, bool dev) {
+    if (p == nullptr) return nullptr;
+    if (dev && std::is_same<T, double>::value) return reinterpret_cast<const T*>(p);
+    T* d = c->buf<T>(name, n > 0 ? n : 1);
+    if (std::is_same<T, double>::value) {
+        h2d(c, d, p, sizeof(double) * n);
+    } else {
+        const double* src = p;
+        if (!dev) {
+            double* tmp = c->buf<double>(std::string(name) + "_f64", n > 0 ? n : 1);
+            h2d(c, tmp, p, sizeof(double) * n);
+            src = tmp;
+        }
+        convert<T>(c, n, src, d);
+    }
+    return d;
+}
+
+template <typename T>
+void stage_out(hgm_ctx* c, double* out, const T* d, int64_t n, bool dev) {
+    if (out == nullptr || n == 0) return;
+    if (std::is_same<T, double>::value) {
+        if (dev) {
+            HGM_HIP(hipMemcpyAsync(out, d, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
+            HGM_HIP(hipStreamSynchronize(c->stream));
+        } else {
+            HGM_HIP(hipMemcpyAsync(out, d, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+            HGM_HIP(hipStreamSynchronize(c->stream));
+        }
+    } else {
+        double* tmp = dev ? out : c->buf<double>("out_f64", n);
+        convert_back<T>(c, n, d, tmp);
+        if (!dev) HGM_HIP(hipMemcpyAsync(out, tmp, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+        HGM_HIP(hipStreamSynchronize(c->stream));
+    }
+}
+
+void check_dims(const hgm_mat* A, const hgm_mat* B) {
+    HGM_REQUIRE(A != nullptr, "A is NULL");
+    if (B) {
+        HGM_REQUIRE(B->rows == A->cols && B->cols == A->rows,
+                    "dimension mismatch: B must be size(A') (n x m)");
+        HGM_REQUIRE(B->dtype == A->dtype, "A and B must have the same dtype");
+    }
+}
+
+}  // namespace
+
+// ============================================================================
+// GMRES family (Arnoldi + projected solve)
+// ============================================================================
+enum Proj { PROJ_LS = 0, PROJ_PTR = 1, PROJ_ABRTP = 2 };
+
+struct GmresSpec {
+    int side;             // HGM_SIDE_BA: n-space Krylov of B*A (+λI) ; HGM_SIDE_AB: m-space of A*B
+    int proj;             // Proj
+    bool lambda_in_op;    // RTP: operator B*(A*v) + lambda*v
+    bool x_preassigned;   // hybrid_ba_gmres_rtp.m:4 initialises x = zeros
+};
+
+int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_mat* A, const hgm_mat* B,
+                 const double* b_in, const double* xt_in, double tol, int maxit, double lambda, double* x_out,
+                 double* err_out, double* res_out, int* niters) {
+    check_dims(A, B);
+    HGM_REQUIRE(B != nullptr, "B is NULL");
+    HGM_REQUIRE(b_in != nullptr && xt_in != nullptr, "b and x_true are required");
+    HGM_REQUIRE(A->dtype == HGM_F64, "GMRES family is fp64 (the reference's precision)");
+    HGM_REQUIRE(maxit >= 1, "maxit must be >= 1");
+    using T = double;
+    const bool dev = o && (o->flags & HGM_DEVICE_PTRS);
+    const int orth = o ? o->orth : HGM_MGS;
+    const int64_t m = A->rows, n = A->cols;
+    const bool nspace = sp.side == HGM_SIDE_BA;
+    const int64_t dim = nspace ? n : m;
+    const int64_t ldq = round_up(dim > 0 ? dim : 1, 64);
+    const bool dist = nspace && dist_n(c);
+    hipStream_t st = c->stream;
+
+    const T* b = stage_in<T>(c, "in_b", b_in, m, dev);
+    const T* xt = stage_in<T>(c, "in_xt", xt_in, n, dev);
+    T* Q = c->buf<T>("Q", (size_t)ldq * (maxit + 1));
+    T* Hd = c->buf<T>("H", (size_t)(maxit + 1) * maxit);
+    T* x = c->buf<T>("x", n > 0 ? n : 1);
+    T* t = c->buf<T>("t_m", m > 0 ? m : 1);        // m-vector scratch (A*q, residual)
+    T* tn = c->buf<T>("t_n", n > 0 ? n : 1);       // n-vector scratch (AB side: B*q)
+    T* z = c->buf<T>("z_m", m > 0 ? m : 1);        // AB side: z = Q*y
+    T* yd = c->buf<T>("y", maxit + 8);
+    const int64_t ldaq = round_up(m > 0 ? m : 1, 64);
+    T* AQ = sp.proj == PROJ_ABRTP ? c->buf<T>("AQ", (size_t)ldaq * maxit) : nullptr;
+    T* gcol = c->buf<T>("gcol", maxit + 8);
+    HGM_HIP(hipMemsetAsync(Hd, 0, sizeof(T) * (maxit + 1) * maxit, st));
+    fill<T>(c, n, x, T(0));
+
+    std::vector<double> H((size_t)(maxit + 1) * maxit, 0.0);
+    std::vector<double> err(maxit, 0.0), res(maxit, 0.0);
+    auto Hh = [&](int i, int j) -> double& { return H[(size_t)j * (maxit + 1) + i]; };
+
+    // ||b|| (m, replicated) and ||x_true|| (n, sharded) — MATLAB recomputes them every
+    // iteration (hybrid_*_rtp.m:32-33); the values are loop-invariant.
+    sumsq<T>(c, m, b, dslot<T>(c, S_NB));
+    nsumsq_diff<T>(c, n, xt, x, dslot<T>(c, S_NXT));   // ||x_true - 0||^2
+    // r0
+    T* q0 = Q;
+    if (nspace) {
+        apply_B<T>(c, B, b, q0, EPI_NONE, T(0), nullptr);   // d = B*b   (hybrid_*_rtp.m:7,9; *_bounds r0 = B*(b - A*0))
+    } else {
+        HGM_HIP(hipMemcpyAsync(q0, b, sizeof(T) * m, hipMemcpyDeviceToDevice, st));   // r0 = b - A*(B*0) = b
+    }
+    if (nspace) nsumsq<T>(c, dim, q0, dslot<T>(c, S_BETA));
+    else sumsq<T>(c, dim, q0, dslot<T>(c, S_BETA));
+    read_scalars(c, 0, 3);
+    const double nb = std::sqrt(c->hscal[S_NB]);
+    const double nxt = std::sqrt(c->hscal[S_NXT]);
+    const double beta = std::sqrt(c->hscal[S_BETA]);      // :10  beta = norm(r0)
+    div_scalar<T>(c, dim, q0, q0, beta);                  // :13  Q(:,1) = r0 / beta
+
+    bool x_assigned = sp.x_preassigned;
+    int k = 0;
+    std::vector<double> y, rhs, M;
+    std::vector<double> G((size_t)maxit * maxit, 0.0), cvec(maxit, 0.0);
+    for (k = 0; k < maxit; ++k) {
+        T* qk = Q + (int64_t)k * ldq;
+        T* v = Q + (int64_t)(k + 1) * ldq;
+        // ---- operator (hybrid_*_rtp.m:19 ; *_bounds.m:25) ----
+        if (nspace) {
+            T* Aq = AQ ? AQ + (int64_t)k * ldaq : t;
+            apply_A<T>(c, A, qk, Aq, EPI_NONE, T(0), nullptr);
+            if (sp.lambda_in_op) apply_B<T>(c, B, Aq, v, EPI_ADD, T(lambda), qk);   // B*(A*v) + lambda*v
+            else apply_B<T>(c, B, Aq, v, EPI_NONE, T(0), nullptr);                  // B*(A*v)
+        } else {
+            apply_B<T>(c, B, qk, tn, EPI_NONE, T(0), nullptr);                      // B*Q(:,k)
+            apply_A<T>(c, A, tn, v, EPI_NONE, T(0), nullptr);                       // A*(B*Q(:,k))
+        }
+        // ---- orthogonalisation (hybrid_*_rtp.m:20-26) ----
+        T* Hcol = Hd + (int64_t)k * (maxit + 1);
+        if (orth == HGM_CGS2) cgs2<T>(c, dim, Q, ldq, k, Hcol, dist);
+        else mgs<T>(c, dim, Q, ldq, k, Hcol, dist);
+        Reader rd(c);
+        rd.add(&Hh(0, k), Hcol, sizeof(T) * (k + 2));
+        if (sp.proj == PROJ_ABRTP) {
+            // column k of AQk'*AQk and AQk'*b (hybrid_ab_gmres_rtp.m:31-32); A*Q(:,j) was
+            // computed inside M_reg_op(Q(:,j)) at :19 — the same deterministic SpMV.
+            multidot<T>(c, m, k + 1, AQ, ldaq, AQ + (int64_t)k * ldaq, gcol);
+            dot<T>(c, m, AQ + (int64_t)k * ldaq, b, gcol + k + 1);
+            rd.add(&G[(size_t)k * maxit], gcol, sizeof(T) * (k + 1));
+            rd.add(&cvec[k], gcol + k + 1, sizeof(T));
+        }
+        rd.go();
+        if (Hh(k + 1, k) == 0) break;                    // :25  if H(k+1,k) == 0, break
+        const int kk = k + 1;                            // MATLAB k
+        y.assign(kk, 0.0);
+        if (sp.proj == PROJ_LS) {
+            // yk = H(1:k+1,1:k) \ [beta; zeros(k,1)]   (hybrid_ba_gmres_rtp.m:28-29)
+            M.assign((size_t)(kk + 1) * kk, 0.0);
+            for (int j = 0; j < kk; ++j)
+                for (int i = 0; i <= kk; ++i) M[(size_t)j * (kk + 1) + i] = Hh(i, j);
+            rhs.assign(kk + 1, 0.0);
+            rhs[0] = beta;
+            dense::qr_ls(kk + 1, kk, M.data(), rhs.data(), y.data());
+        } else if (sp.proj == PROJ_PTR) {
+            // yk = (Hk'*Hk + lambda*eye(k)) \ (Hk'*tk)   (*_hybrid_bounds.m:34-36)
+            M.assign((size_t)kk * kk, 0.0);
+            for (int i = 0; i < kk; ++i)
+                for (int j = 0; j < kk; ++j) {
+                    double s = 0;
+                    for (int r = 0; r <= kk; ++r) s += Hh(r, i) * Hh(r, j);
+                    M[(size_t)j * kk + i] = s + (i == j ? lambda : 0.0);
+                }
+            rhs.assign(kk, 0.0);
+            for (int i = 0; i < kk; ++i) rhs[i] = Hh(0, i) * beta;
+            dense::mldivide_square(kk, M.data(), rhs.data(), y.data());
+        } else {
+            // yk = (AQk'*AQk + lambda*eye(k)) \ (AQk'*b)   (hybrid_ab_gmres_rtp.m:32)
+            M.assign((size_t)kk * kk, 0.0);
+            for (int j = 0; j < kk; ++j)
+                for (int i = 0; i <= j; ++i) {
+                    const double g = G[(size_t)j * maxit + i];
+                    M[(size_t)j * kk + i] = g;
+                    M[(size_t)i * kk + j] = g;
+                }
+            for (int i = 0; i < kk; ++i) M[(size_t)i * kk + i] += lambda;
+            dense::mldivide_square(kk, M.data(), cvec.data(), y.data());
+        }
+        h2d(c, yd, y.data(), sizeof(double) * kk);
+        // ---- reconstruction (hybrid_*_rtp.m:30/33 ; *_bounds.m:37-38) ----
+        if (nspace) {
+            gemv<T>(c, n, kk, Q, ldq, yd, x, 0);                 // x = Q(:,1:k)*yk
+        } else {
+            gemv<T>(c, m, kk, Q, ldq, yd, z, 0);                 // zk = Q(:,1:k)*yk
+            apply_B<T>(c, B, z, x, EPI_NONE, T(0), nullptr);     // xk = B*zk
+        }
+        x_assigned = true;
+        // ---- monitors (hybrid_*_rtp.m:32-33 / :35-36) ----
+        apply_A<T>(c, A, x, t, EPI_RSUB, T(0), b);              // b - A*x
+        sumsq<T>(c, m, t, dslot<T>(c, S_RES));
+        nsumsq_diff<T>(c, n, x, xt, dslot<T>(c, S_ERR));
+        read_scalars(c, S_RES, 2);
+        res[k] = std::sqrt(c->hscal[S_RES]) / nb;
+        err[k] = std::sqrt(c->hscal[S_ERR]) / nxt;
+        if (res[k] <= tol) break;                        // :35 / :38 / *_bounds :79-83
+    }
+    if (k == maxit) k = maxit - 1;
+    const int nit = k + 1;                               // niters = k
+    if (!x_assigned) throw Error{HGM_E_NOT_ASSIGNED, "Output argument \"x\" not assigned during call (breakdown at k = 1)"};
+    stage_out<T>(c, x_out, x, n, dev);
+    if (err_out) std::memcpy(err_out, err.data(), sizeof(double) * nit);
+    if (res_out) std::memcpy(res_out, res.data(), sizeof(double) * nit);
+    if (niters) *niters = nit;
+    if (o && o->H_out) std::memcpy(o->H_out, H.data(), sizeof(double) * H.size());
+    return HGM_OK;
+}
+
+// ============================================================================
+// LSQR (lsqr_solver.m) and hybrid LSQR on [A; sqrt(lambda) I] (hybrid_lsqr_solver.m)
+// ============================================================================
+template <typename T>
+int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, const double* b_in,
+           const double* xt_in, double tol, int maxit, bool hybrid, double lambda, double* x_out,
+           double* err_out, double* res_out, int* niters) {
+    check_dims(A, At);
+    HGM_REQUIRE(At != nullptr, "At is NULL");
+    HGM_REQUIRE(b_in != nullptr && xt_in != nullptr, "b and x_true are required");
+    HGM_REQUIRE(maxit >= 1, "maxit must be >= 1");
+    const bool dev = o && (o->flags & HGM_DEVICE_PTRS);
+    const int64_t m = A->rows, n = A->cols;
+    const T* b = stage_in<T>(c, "in_b", b_in, m, dev);
+    const T* xt = stage_in<T>(c, "in_xt", xt_in, n, dev);
+    T* x = c->buf<T>("x", n + 1);
+    T* w = c->buf<T>("w", n + 1);
+    T* v = c->buf<T>("v", n + 1);
+    T* u = c->buf<T>("u", m + 1);
+    T* un = hybrid ? c->buf<T>("u_n", n + 1) : nullptr;    // lower block of u_aug
+    T* t = c->buf<T>("t_m", m + 1);
+    T* sl = reinterpret_cast<T*>(c->dscal);
+    const T sq = (T)std::sqrt(lambda);
+    fill<T>(c, n, x, T(0));
+    std::vector<double> err(maxit, 0.0), res(maxit, 0.0);
+
+    sumsq<T>(c, m, b, sl + S_NB);
+    nsumsq_diff<T>(c, n, xt, x, sl + S_NXT);
+    std::vector<T> hs(4);
+    Reader r0(c);
+    r0.add(&hs[0], sl + S_NB, sizeof(T));
+    r0.add(&hs[1], sl + S_NXT, sizeof(T));
+    r0.go();
+    const double nb = std::sqrt((double)hs[0]);
+    const double nxt = std::sqrt((double)hs[1]);
+    // beta = norm(b) (lsqr_solver.m:7; hybrid: norm([b;0]) = norm(b), hybrid_lsqr_solver.m:9)
+    double beta = nb;
+    div_scalar<T>(c, m, b, u, (T)beta);                                        // :8  u = b / beta
+    if (hybrid) fill<T>(c, n, un, T(0));                                       // u_aug = [b;0]/beta
+    if (hybrid) apply_B<T>(c, At, u, v, EPI_ADD, sq, un);                      // A_aug'*u_aug
+    else apply_B<T>(c, At, u, v, EPI_NONE, T(0), nullptr);                     // :10 v_hat = A'*u
+    nsumsq<T>(c, n, v, sl + S_ALPHA);
+    double alpha = std::sqrt((double)read1<T>(c, sl + S_ALPHA));               // :11
+    div_scalar<T>(c, n, v, v, (T)alpha);                                       // :12
+    HGM_HIP(hipMemcpyAsync(w, v, sizeof(T) * n, hipMemcpyDeviceToDevice, c->stream));   // :14 w = v
+    double phi_bar = beta, rho_bar = alpha;                                    // :15-16
+    int k = 0;
+    for (k = 0; k < maxit; ++k) {
+        // :22-24  u_hat = A*v - alpha*u ; beta = norm(u_hat) ; u = u_hat / beta
+        apply_A<T>(c, A, v, t, EPI_SUB, (T)alpha, u);
+        sumsq<T>(c, m, t, sl + S_BETA);
+        if (hybrid) {
+            // lower block of u_hat: (sqrt(lambda)*v) - (alpha*u_n), same norm as the upper block
+            T* tl = c->buf<T>("t_n", n + 1);
+            fill<T>(c, n, tl, T(0));
+            epilogue<T>(c, n, tl, EPI_ADD, sq, v);                     // tl = 0 + sq*v (exact: sq*v)
+            epilogue<T>(c, n, tl, EPI_SUB, (T)alpha, un);              // tl = tl - alpha*u_n
+            nsumsq<T>(c, n, tl, sl + S_AUX);
+            Reader rr(c);
+            rr.add(&hs[0], sl + S_BETA, sizeof(T));
+            rr.add(&hs[1], sl + S_AUX, sizeof(T));
+            rr.go();
+            beta = std::sqrt((double)(hs[0] + hs[1]));
+            div_scalar<T>(c, m, t, u, (T)beta);
+            div_scalar<T>(c, n, tl, un, (T)beta);
+            // :26 v_hat = A_aug'*u_aug - beta*v = (A'*u + sq*un) - beta*v
+            T* vh = c->buf<T>("t_n2", n + 1);   // A_aug'*u_aug reads v in the epilogue: not in place
+            apply_B<T>(c, At, u, vh, EPI_ADD, sq, un);
+            epilogue<T>(c, n, vh, EPI_SUB, (T)beta, v);
+            HGM_HIP(hipMemcpyAsync(v, vh, sizeof(T) * n, hipMemcpyDeviceToDevice, c->stream));
+        } else {
+            beta = std::sqrt((double)read1<T>(c, sl + S_BETA));
+            div_scalar<T>(c, m, t, u, (T)beta);
+            // :26 v_hat = A'*u - beta*v   (in place is safe: row i reads v(i) only in its epilogue)
+            apply_B<T>(c, At, u, v, EPI_SUB, (T)beta, v);
+        }
+        nsumsq<T>(c, n, v, sl + S_ALPHA);
+        alpha = std::sqrt((double)read1<T>(c, sl + S_ALPHA));                 // :27
+        div_scalar<T>(c, n, v, v, (T)alpha);                                   // :28
+        // :31-38 Givens rotation (host scalars)
+        const double rho = std::sqrt(rho_bar * rho_bar + beta * beta);
+        const double cs = rho_bar / rho;
+        const double sn = beta / rho;
+        const double theta = sn * alpha;
+        rho_bar = -cs * alpha;
+        const double phi = cs * phi_bar;
+        phi_bar = sn * phi_bar;
+        lsqr_update<T>(c, n, x, w, v, (T)(phi / rho), (T)(theta / rho));     // :40-41
+        nsumsq_diff<T>(c, n, x, xt, sl + S_ERR);
+        if (hybrid) {
+            apply_A<T>(c, A, x, t, EPI_RSUB, T(0), b);                        // hybrid :43  b - A*x
+            sumsq<T>(c, m, t, sl + S_RES);
+            Reader rr(c);
+            rr.add(&hs[0], sl + S_ERR, sizeof(T));
+            rr.add(&hs[1], sl + S_RES, sizeof(T));
+            rr.go();
+            err[k] = std::sqrt((double)hs[0]) / nxt;
+            res[k] = std::sqrt((double)hs[1]) / nb;
+            if (res[k] < tol) break;                                           // hybrid :45 (<)
+        } else {
+            err[k] = std::sqrt((double)read1<T>(c, sl + S_ERR)) / nxt;         // :43
+            res[k] = std::fabs(phi_bar) / nb;                                  // :44
+            if (res[k] <= tol) break;                                          // :46 (<=)
+        }
+    }
+    if (k == maxit) k = maxit - 1;
+    const int nit = k + 1;
+    if (!hybrid) {
+        apply_A<T>(c, A, x, t, EPI_RSUB, T(0), b);                            // :52 exact final residual
+        sumsq<T>(c, m, t, sl + S_RES);
+        res[nit - 1] = std::sqrt((double)read1<T>(c, sl + S_RES)) / nb;
+    }
+    stage_out<T>(c, x_out, x, n, dev);
+    if (err_out) std::memcpy(err_out, err.data(), sizeof(double) * nit);
+    if (res_out) std::memcpy(res_out, res.data(), sizeof(double) * nit);
+    if (niters) *niters = nit;
+    return HGM_OK;
+}
+
+// ============================================================================
+// LSMR (lsmr_solver.m)
+// ============================================================================
+template <typename T>
+int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, const double* b_in,
+           const double* xt_in, double tol, int maxit, double* x_out, double* err_out, double* res_out,
+           double* ar_out, int* iters) {
+    check_dims(A, At);
+    HGM_REQUIRE(At != nullptr, "At is NULL");
+    HGM_REQUIRE(b_in != nullptr, "b is required");
+    const bool dev = o && (o->flags & HGM_DEVICE_PTRS);
+    const int64_t m = A->rows, n = A->cols;
+    if (maxit <= 0) maxit = (int)std::min<int64_t>(m, n);                    // :5 default min(m,n)
+    HGM_REQUIRE(maxit >= 1, "maxit must be >= 1");
+    const T* b = stage_in<T>(c, "in_b", b_in, m, dev);
+    const T* xt = stage_in<T>(c, "in_xt", xt_in, n, dev);
+    T* x = c->buf<T>("x", n + 1);
+    T* v = c->buf<T>("v", n + 1);
+    T* h = c->buf<T>("h", n + 1);
+    T* hbar = c->buf<T>("hbar", n + 1);
+    T* u = c->buf<T>("u", m + 1);
+    T* r = c->buf<T>("t_m", m + 1);
+    T* atr = c->buf<T>("t_n", n + 1);
+    T* sl = reinterpret_cast<T*>(c->dscal);
+    fill<T>(c, n, x, T(0));                                                    // :7
+    fill<T>(c, n, hbar, T(0));                                                 // :26
+    std::vector<double> err(maxit, std::numeric_limits<double>::quiet_NaN());  // :28
+    std::vector<double> res(maxit, 0.0), ar(maxit, 0.0);
+    std::vector<T> hs(4);
+
+    sumsq<T>(c, m, b, sl + S_NB);
+    if (xt) nsumsq_diff<T>(c, n, xt, x, sl + S_NXT);
+    // ||A||_F (lsmr_solver.m:71, loop-invariant): cached per matrix
+    if (A->fro < 0) {
+        double* f = reinterpret_cast<double*>(c->dscal) + 64;
+        if (A->dtype == HGM_F32) fro2<float>(c, A, f); else fro2<double>(c, A, f);
+        if (dist_n(c)) allreduce(c, f, 1);
+        double fv;
+        Reader rf(c);
+        rf.add(&fv, f, sizeof(double));
+        rf.go();
+        const_cast<hgm_mat*>(A)->fro = std::sqrt(fv);
+    }
+    const double normA = A->fro;
+    Reader r0(c);
+    r0.add(&hs[0], sl + S_NB, sizeof(T));
+    if (xt) r0.add(&hs[1], sl + S_NXT, sizeof(T));
+    r0.go();
+    const double nb = std::sqrt((double)hs[0]);
+    const double nxt = xt ? std::sqrt((double)hs[1]) : 0.0;
+    HGM_HIP(hipMemcpyAsync(u, b, sizeof(T) * m, hipMemcpyDeviceToDevice, c->stream));   // :10
+    double beta = nb;                                                          // :11
+    if (beta > 0) div_scalar<T>(c, m, u, u, (T)beta);                          // :12
+    apply_B<T>(c, At, u, v, EPI_NONE, T(0), nullptr);                          // :14
+    nsumsq<T>(c, n, v, sl + S_ALPHA);
+    double alpha = std::sqrt((double)read1<T>(c, sl + S_ALPHA));              // :15
+    if (alpha > 0) div_scalar<T>(c, n, v, v, (T)alpha);                        // :16
+    double zetabar = alpha * beta, alphabar = alpha, rho = 1, rhobar = 1, cbar = 1, sbar = 0;   // :19-23
+    HGM_HIP(hipMemcpyAsync(h, v, sizeof(T) * n, hipMemcpyDeviceToDevice, c->stream));   // :25
+    int k = 0;
+    for (k = 0; k < maxit; ++k) {
+        apply_A<T>(c, A, v, u, EPI_SUB, (T)alpha, u);                          // :34 u = A*v - alpha*u
+        sumsq<T>(c, m, u, sl + S_BETA);
+        beta = std::sqrt((double)read1<T>(c, sl + S_BETA));                   // :35
+        if (beta > 0) div_scalar<T>(c, m, u, u, (T)beta);                      // :36
+        apply_B<T>(c, At, u, v, EPI_SUB, (T)beta, v);                          // :38 v = A.'*u - beta*v
+        nsumsq<T>(c, n, v, sl + S_ALPHA);
+        alpha = std::sqrt((double)read1<T>(c, sl + S_ALPHA));                 // :39
+        if (alpha > 0) div_scalar<T>(c, n, v, v, (T)alpha);                    // :40
+        const double alphahat = alphabar;                                      // :42
+        const double rhoold = rho;                                             // :43
+        rho = std::hypot(alphahat, beta);                                      // :44
+        const double cc = alphahat / rho, ss = beta / rho;                     // :45-46
+        const double thetanew = ss * alpha;                                    // :48
+        alphabar = cc * alpha;                                                 // :49
+        const double rhobarold = rhobar;                                       // :51
+        const double thetabar = sbar * rho;                                    // :52
+        rhobar = std::hypot(cbar * rho, thetanew);                             // :53
+        cbar = (cbar * rho) / rhobar;                                          // :54
+        sbar = thetanew / rhobar;                                              // :55
+        const double zeta = cbar * zetabar;                                    // :58
+        zetabar = -sbar * zetabar;                                             // :59
+        const double c_hbar = (thetabar * rho) / (rhoold * rhobarold);         // :64
+        const double c_x = zeta / (rho * rhobar);                              // :66
+        const double c_h = thetanew / rho;                                     // :67
+        lsmr_update<T>(c, n, x, h, hbar, v, (T)c_hbar, (T)c_x, (T)c_h, k == 0);
+        apply_A<T>(c, A, x, r, EPI_RSUB, T(0), b);                             // :69 r = b - A*x
+        sumsq<T>(c, m, r, sl + S_RES);
+        apply_B<T>(c, At, r, atr, EPI_NONE, T(0), nullptr);                    // :71 A.'*r
+        nsumsq<T>(c, n, atr, sl + S_AR);
+        if (xt) nsumsq_diff<T>(c, n, x, xt, sl + S_ERR);
+        Reader rr(c);
+        rr.add(&hs[0], sl + S_RES, sizeof(T));
+        rr.add(&hs[1], sl + S_AR, sizeof(T));
+        if (xt) rr.add(&hs[2], sl + S_ERR, sizeof(T));
+        rr.go();
+        const double nr = std::sqrt((double)hs[0]);
+        res[k] = nr / (nb + EPSD);                                             // :70
+        ar[k] = std::sqrt((double)hs[1]) / (normA * std::max(nr, EPSD));       // :71
+        if (xt) err[k] = std::sqrt((double)hs[2]) / nxt;                       // :72-73
+        if (res[k] < tol) break;                                               // :76 (<)
+    }
+    if (k == maxit) k = maxit - 1;
+    const int nit = k + 1;
+    stage_out<T>(c, x_out, x, n, dev);
+    if (err_out) std::memcpy(err_out, err.data(), sizeof(double) * nit);
+    if (res_out) std::memcpy(res_out, res.data(), sizeof(double) * nit);
+    if (ar_out) std::memcpy(ar_out, ar.data(), sizeof(double) * nit);
+    if (iters) *iters = nit;
+    return HGM_OK;
+}
+
+// ============================================================================
+// hybrid LSMR (hybrid_lsmr_solver.m)
+// ============================================================================
+int hybrid_lsmr(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, const double* b_in,
+                const double* xt_in, double tol, int maxit, double lambda, double* x_out, double* err_out,
+                double* res_out, int* niters) {
+    check_dims(A, At);
+    HGM_REQUIRE(At != nullptr, "At is NULL");
+    HGM_REQUIRE(A->dtype == HGM_F64, "hybrid LSMR is fp64");
+    HGM_REQUIRE(b_in != nullptr && xt_in != nullptr, "b and x_true are required");
+    HGM_REQUIRE(maxit >= 1, "maxit must be >= 1");
+    using T = double;
+    const bool dev = o && (o->flags & HGM_DEVICE_PTRS);
+    const int64_t m = A->rows, n = A->cols;
+    const int64_t ldv = round_up(n > 0 ? n : 1, 64);
+    const T* b = stage_in<T>(c, "in_b", b_in, m, dev);
+    const T* xt = stage_in<T>(c, "in_xt", xt_in, n, dev);
+    T* V = c->buf<T>("Q", (size_t)ldv * maxit);
+    T* x = c->buf<T>("x", n + 1);
+    T* u = c->buf<T>("u", m + 1);
+    T* t = c->buf<T>("t_m", m + 1);
+    T* yd = c->buf<T>("y", maxit + 8);
+    T* sl = reinterpret_cast<T*>(c->dscal);
+    fill<T>(c, n, x, T(0));
+    std::vector<double> err(maxit, 0.0), res(maxit, 0.0);
+    std::vector<double> Bk((size_t)(maxit + 1) * maxit, 0.0);                  // :11
+    auto BK = [&](int i, int j) -> double& { return Bk[(size_t)j * (maxit + 1) + i]; };
+
+    sumsq<T>(c, m, b, sl + S_NB);
+    nsumsq_diff<T>(c, n, xt, x, sl + S_NXT);
+    read_scalars(c, 0, 2);
+    const double nb = std::sqrt(c->hscal[S_NB]);
+    const double nxt = std::sqrt(c->hscal[S_NXT]);
+    const double beta1 = nb;                                                   // :7
+    div_scalar<T>(c, m, b, u, beta1);                                          // :8
+    T* v0 = V;
+    apply_B<T>(c, At, u, v0, EPI_NONE, 0.0, nullptr);                          // :13
+    nsumsq<T>(c, n, v0, sl + S_ALPHA);
+    double alpha1 = std::sqrt(read1<T>(c, sl + S_ALPHA));                      // :14
+    div_scalar<T>(c, n, v0, v0, alpha1);                                       // :15-16
+    int k = 0;
+    std::vector<double> Gm, G2, LHS, RHS, y;
+    for (k = 0; k < maxit; ++k) {
+        T* vk = V + (int64_t)k * ldv;
+        BK(k, k) = alpha1;                                                     // :23
+        apply_A<T>(c, A, vk, t, EPI_SUB, alpha1, u);                           // :24
+        sumsq<T>(c, m, t, sl + S_BETA);
+        const double beta_k = std::sqrt(read1<T>(c, sl + S_BETA));            // :25
+        div_scalar<T>(c, m, t, u, beta_k);                                     // :26
+        BK(k + 1, k) = beta_k;                                                 // :27
+        if (k < maxit - 1) {                                                   // :29
+            T* vn = V + (int64_t)(k + 1) * ldv;
+            apply_B<T>(c, At, u, vn, EPI_SUB, beta_k, vk);                     // :30
+            nsumsq<T>(c, n, vn, sl + S_ALPHA);
+            const double a1 = std::sqrt(read1<T>(c, sl + S_ALPHA));            // :31
+            div_scalar<T>(c, n, vn, vn, a1);                                   // :32-33
+            alpha1 = a1;                                                       // :34
+        }
+        const int kk = k + 1;
+        // :37-44  LHS = (Bk'*Bk)^2 + (alpha_k1*beta_k1)^2 e1 e1' + lambda I ; RHS = B_k(1,1) beta1 (Bk'*Bk) e1
+        Gm.assign((size_t)kk * kk, 0.0);
+        for (int i = 0; i < kk; ++i)
+            for (int j = 0; j < kk; ++j) {
+                double s = 0;
+                for (int r = 0; r <= kk; ++r) s += BK(r, i) * BK(r, j);
+                Gm[(size_t)j * kk + i] = s;
+            }
+        G2.assign((size_t)kk * kk, 0.0);
+        for (int i = 0; i < kk; ++i)
+            for (int j = 0; j < kk; ++j) {
+                double s = 0;
+                for (int l = 0; l < kk; ++l) s += Gm[(size_t)l * kk + i] * Gm[(size_t)j * kk + l];
+                G2[(size_t)j * kk + i] = s;
+            }
+        const double ab = alpha1 * beta_k;
+        LHS = G2;
+        LHS[0] += ab * ab;
+        for (int i = 0; i < kk; ++i) LHS[(size_t)i * kk + i] += lambda;
+        RHS.assign(kk, 0.0);
+        const double sc = BK(0, 0) * beta1;
+        for (int i = 0; i < kk; ++i) RHS[i] = sc * Gm[i];
+        y.assign(kk, 0.0);
+        dense::mldivide_square(kk, LHS.data(), RHS.data(), y.data());          // :44
+        h2d(c, yd, y.data(), sizeof(double) * kk);
+        gemv<T>(c, n, kk, V, ldv, yd, x, 0);                                   // :45
+        nsumsq_diff<T>(c, n, x, xt, sl + S_ERR);                               // :47
+        apply_A<T>(c, A, x, t, EPI_RSUB, 0.0, b);                              // :48
+        sumsq<T>(c, m, t, sl + S_RES);
+        read_scalars(c, S_RES, 2);
+        res[k] = std::sqrt(c->hscal[S_RES]) / nb;
+        err[k] = std::sqrt(c->hscal[S_ERR]) / nxt;
+        if (res[k] <= tol) break;                                              // :50
+    }
+    if (k == maxit) k = maxit - 1;
+    const int nit = k + 1;
+    stage_out<T>(c, x_out, x, n, dev);
+    if (err_out) std::memcpy(err_out, err.data(), sizeof(double) * nit);
+    if (res_out) std::memcpy(res_out, res.data(), sizeof(double) * nit);
+    if (niters) *niters = nit;
+    return HGM_OK;
+}
+
+// ============================================================================
+// Arnoldi for GCV (gcv_function.m:3-33)
+// ============================================================================
+int arnoldi(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b_in, int kg, int side,
+            double btol, int orth, double* H_out, double* beta_out, int* kdone) {
+    check_dims(A, B);
+    HGM_REQUIRE(B != nullptr, "B is NULL");
+    HGM_REQUIRE(A->dtype == HGM_F64, "Arnoldi is fp64");
+    HGM_REQUIRE(kg >= 1, "k must be >= 1");
+    using T = double;
+    const int64_t m = A->rows, n = A->cols;
+    const bool nspace = side == HGM_SIDE_BA;
+    const int64_t dim = nspace ? n : m;
+    const int64_t ldq = round_up(dim > 0 ? dim : 1, 64);
+    const bool dist = nspace && dist_n(c);
+    const T* b = stage_in<T>(c, "in_b", b_in, m, false);
+    T* Q = c->buf<T>("Q", (size_t)ldq * (kg + 1));
+    T* Hd = c->buf<T>("H", (size_t)(kg + 1) * kg);
+    T* t = c->buf<T>("t_m", m + 1);
+    T* tn = c->buf<T>("t_n", n + 1);
+    HGM_HIP(hipMemsetAsync(Hd, 0, sizeof(T) * (kg + 1) * kg, c->stream));
+    if (nspace) apply_B<T>(c, B, b, Q, EPI_NONE, 0.0, nullptr);                // :8  r0 = B*b
+    else HGM_HIP(hipMemcpyAsync(Q, b, sizeof(T) * m, hipMemcpyDeviceToDevice, c->stream));   // :5
+    if (nspace) nsumsq<T>(c, dim, Q, dslot<T>(c, S_BETA));
+    else sumsq<T>(c, dim, Q, dslot<T>(c, S_BETA));
+    const double beta = std::sqrt(read1<T>(c, dslot<T>(c, S_BETA)));           // :12
+    div_scalar<T>(c, dim, Q, Q, beta);                                         // :15
+    std::vector<double> H((size_t)(kg + 1) * kg, 0.0);
+    int done = 0;
+    for (int k = 0; k < kg; ++k) {
+        T* qk = Q + (int64_t)k * ldq;
+        T* v = Q + (int64_t)(k + 1) * ldq;
+        if (nspace) {
+            apply_A<T>(c, A, qk, t, EPI_NONE, 0.0, nullptr);
+            apply_B<T>(c, B, t, v, EPI_NONE, 0.0, nullptr);                    // :22 B*(A*Q(:,k))
+        } else {
+            apply_B<T>(c, B, qk, tn, EPI_NONE, 0.0, nullptr);
+            apply_A<T>(c, A, tn, v, EPI_NONE, 0.0, nullptr);                   // :20 A*(B*Q(:,k))
+        }
+        T* Hcol = Hd + (int64_t)k * (kg + 1);
+        if (orth == HGM_CGS2) cgs2<T>(c, dim, Q, ldq, k, Hcol, dist);
+        else mgs<T>(c, dim, Q, ldq, k, Hcol, dist);                            // :25-31
+        Reader rd(c);
+        rd.add(&H[(size_t)k * (kg + 1)], Hcol, sizeof(T) * (k + 2));
+        rd.go();
+        done = k + 1;
+        if (H[(size_t)k * (kg + 1) + k + 1] < btol) {                          // :30  H(k+1,k) < 1e-12 -> break
+            // the reference breaks before Q(:,k+1) = v/H(k+1,k); H(k+1,k) keeps its value
+            break;
+        }
+    }
+    if (H_out) std::memcpy(H_out, H.data(), sizeof(double) * H.size());
+    if (beta_out) *beta_out = beta;
+    if (kdone) *kdone = done;
+    return HGM_OK;
+}
+
+// explicit instantiations used by capi.cpp
+template int lsqr_t<double>(hgm_ctx*, const hgm_opts*, const hgm_mat*, const hgm_mat*, const double*, const double*,
+                            double, int, bool, double, double*, double*, double*, int*);
+template int lsqr_t<float>(hgm_ctx*, const hgm_opts*, const hgm_mat*, const hgm_mat*, const double*, const double*,
+                           double, int, bool, double, double*, double*, double*, int*);
+template int lsmr_t<double>(hgm_ctx*, const hgm_opts*, const hgm_mat*, const hgm_mat*, const double*, const double*,
+                            double, int, double*, double*, double*, double*, int*);
+template int lsmr_t<float>(hgm_ctx*, const hgm_opts*, const hgm_mat*, const hgm_mat*, const double*, const double*,
+                           double, int, double*, double*, double*, double*, int*);
+
+}  // namespace hgm

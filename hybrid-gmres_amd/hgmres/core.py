@@ -1,0 +1,465 @@
+"""Host-side mirror of the reference's MATLAB solver interface over libhgmres.
+
+Every public solver keeps the reference's name, positional arguments and
+output tuple (the MATLAB ``[x, error_norm, residual_norm, niters] = f(...)``
+becomes a Python tuple), with histories truncated to ``1:niters`` exactly as
+the ``.m`` files do.  Operators may be scipy sparse matrices, dense arrays, or
+:class:`SparseOperator` handles already resident in HBM.
+
+Reference signatures mirrored (file:line):
+  hybrid_ab_gmres_rtp.m:1, hybrid_ba_gmres_rtp.m:1, lsqr_solver.m:1,
+  lsmr_solver.m:1 (defaults :3,5), hybrid_lsqr_solver.m:1,
+  hybrid_lsmr_solver.m:1, gcv_function.m:1, ABgmres_hybrid_bounds.m:1-2,
+  ABgmres_nonhybrid_bounds.m:1-2, BAgmres_hybrid_bounds.m:1-2,
+  BAgmres_nonhybrid_bounds.m:1-2.
+Error behaviour: MATLAB errors (dimension mismatch, unassigned output) raise
+ValueError / :class:`OutputNotAssigned`; Krylov breakdown is not an error.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+import scipy.sparse as sp
+
+from . import _lib as L
+
+
+class HgmError(RuntimeError):
+    pass
+
+
+class OutputNotAssigned(HgmError):
+    """MATLAB: 'Output argument "x" not assigned during call'."""
+
+
+def _check(rc, ctx=None):
+    if rc == L.HGM_OK:
+        return
+    msg = ""
+    if ctx is not None and ctx._h:
+        msg = L.load().hgm_last_error(ctx._h).decode(errors="replace")
+    if rc == L.HGM_E_ARG:
+        raise ValueError(msg or "invalid argument")
+    if rc == L.HGM_E_NOT_ASSIGNED:
+        raise OutputNotAssigned(msg)
+    raise HgmError(f"libhgmres status {rc}: {msg}")
+
+
+def _dp(a):
+    return a.ctypes.data_as(L.dp) if a is not None else None
+
+
+def _f64(v, n=None, name="vector"):
+    a = np.ascontiguousarray(np.asarray(v, dtype=np.float64).reshape(-1))
+    if n is not None and a.shape[0] != n:
+        raise ValueError(f"{name} has length {a.shape[0]}, expected {n}")
+    return a
+
+
+class Context:
+    """One HIP device + stream (``hgm_ctx``).  ``world > 1`` contexts are made
+    by :func:`hgmres.dist.init_context`."""
+
+    def __init__(self, device: int = 0, _handle=None):
+        lib = L.load()
+        self.device = device
+        if _handle is None:
+            h = C.c_void_p()
+            rc = lib.hgm_ctx_create(device, C.byref(h))
+            if rc != L.HGM_OK:
+                raise HgmError(f"hgm_ctx_create(device={device}) failed with status {rc} (is a GPU visible?)")
+            _handle = h
+        self._h = _handle
+        self._keep = []          # callbacks kept alive
+
+    @property
+    def handle(self):
+        return self._h
+
+    def rank_world(self):
+        r, w = C.c_int(), C.c_int()
+        _check(L.load().hgm_ctx_rank(self._h, C.byref(r), C.byref(w)), self)
+        return r.value, w.value
+
+    def synchronize(self):
+        _check(L.load().hgm_ctx_synchronize(self._h), self)
+
+    def stream(self):
+        return L.load().hgm_ctx_stream(self._h)
+
+    def set_host_allreduce(self, rank, world, fn):
+        """Route cross-rank sums through ``fn(np.ndarray) -> None`` (in place).
+        Used for shard emulation (several processes on one device, gloo)."""
+        def _cb(buf, count, _user):
+            try:
+                arr = np.ctypeslib.as_array(buf, shape=(count,))
+                fn(arr)
+                return 0
+            except Exception:   # noqa: BLE001 - reported as a comm error by the library
+                return -1
+        cb = L.ALLREDUCE_FN(_cb)
+        self._keep.append(cb)
+        _check(L.load().hgm_ctx_set_host_allreduce(self._h, rank, world, cb, None), self)
+
+    def kernel_timing(self, enable=True):
+        _check(L.load().hgm_kernel_timing(self._h, int(enable)), self)
+
+    def kernel_timing_read(self, cls):
+        ms, calls, by = C.c_double(), C.c_int64(), C.c_double()
+        _check(L.load().hgm_kernel_timing_read(self._h, cls, C.byref(ms), C.byref(calls), C.byref(by)), self)
+        return ms.value, calls.value, by.value
+
+    def close(self):
+        if self._h:
+            L.load().hgm_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:   # noqa: BLE001
+            pass
+
+
+_default_ctx = None
+_ctx_lock = threading.Lock()
+
+
+def default_context() -> Context:
+    global _default_ctx
+    with _ctx_lock:
+        if _default_ctx is None:
+            dev = int(os.environ.get("HGM_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+            _default_ctx = Context(dev)
+        return _default_ctx
+
+
+class SparseOperator:
+    """A CSR operator resident in HBM (``hgm_mat``)."""
+
+    def __init__(self, ctx: Context, handle, shape, nnz, dtype):
+        self.ctx = ctx
+        self._h = handle
+        self.shape = shape
+        self.nnz = nnz
+        self.dtype = dtype
+        self._T = None
+
+    @classmethod
+    def from_scipy(cls, M, ctx: Context | None = None, dtype=L.HGM_F64):
+        ctx = ctx or default_context()
+        if not sp.issparse(M):
+            M = sp.csr_matrix(np.asarray(M, dtype=np.float64))
+        M = M.tocsr()
+        rp = np.ascontiguousarray(M.indptr, dtype=np.int64)
+        ci = np.ascontiguousarray(M.indices, dtype=np.int32)
+        va = np.ascontiguousarray(M.data, dtype=np.float64)
+        h = C.c_void_p()
+        _check(L.load().hgm_mat_create_csr(ctx.handle, M.shape[0], M.shape[1], M.nnz,
+                                           rp.ctypes.data_as(L.ip64), ci.ctypes.data_as(L.ip32),
+                                           _dp(va), dtype, C.byref(h)), ctx)
+        return cls(ctx, h, M.shape, int(M.nnz), dtype)
+
+    @classmethod
+    def from_csc(cls, M, ctx: Context | None = None, dtype=L.HGM_F64):
+        """MATLAB sparse hand-over (CSC, 64-bit indices), transposed on device."""
+        ctx = ctx or default_context()
+        M = sp.csc_matrix(M)
+        M.sort_indices()
+        jc = np.ascontiguousarray(M.indptr, dtype=np.int64)
+        ir = np.ascontiguousarray(M.indices, dtype=np.int64)
+        pr = np.ascontiguousarray(M.data, dtype=np.float64)
+        h = C.c_void_p()
+        _check(L.load().hgm_mat_create_csc(ctx.handle, M.shape[0], M.shape[1], M.nnz,
+                                           jc.ctypes.data_as(L.ip64), ir.ctypes.data_as(L.ip64),
+                                           _dp(pr), dtype, C.byref(h)), ctx)
+        return cls(ctx, h, M.shape, int(M.nnz), dtype)
+
+    @classmethod
+    def siddon(cls, N, n_angles, ctx: Context | None = None, dtype=L.HGM_F64, det_offset=None):
+        """Parallel-beam projector generated on the device."""
+        from .problems import DETECTOR_OFFSET
+        ctx = ctx or default_context()
+        off = DETECTOR_OFFSET if det_offset is None else det_offset
+        h = C.c_void_p()
+        _check(L.load().hgm_mat_create_siddon(ctx.handle, N, n_angles, off, dtype, C.byref(h)), ctx)
+        return cls._wrap(ctx, h)
+
+    @classmethod
+    def _wrap(cls, ctx, h):
+        r, c_, nz, dt = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int()
+        _check(L.load().hgm_mat_info(h, C.byref(r), C.byref(c_), C.byref(nz), C.byref(dt)), ctx)
+        return cls(ctx, h, (r.value, c_.value), nz.value, dt.value)
+
+    @property
+    def T(self) -> "SparseOperator":
+        """Device transpose (cached)."""
+        if self._T is None:
+            h = C.c_void_p()
+            _check(L.load().hgm_mat_transpose(self.ctx.handle, self._h, C.byref(h)), self.ctx)
+            self._T = SparseOperator._wrap(self.ctx, h)
+            self._T._T = self
+        return self._T
+
+    def to_scipy(self) -> sp.csr_matrix:
+        rows, cols = self.shape
+        rp = np.empty(rows + 1, dtype=np.int64)
+        ci = np.empty(max(self.nnz, 1), dtype=np.int32)
+        va = np.empty(max(self.nnz, 1), dtype=np.float64)
+        _check(L.load().hgm_mat_download(self.ctx.handle, self._h, rp.ctypes.data_as(L.ip64),
+                                         ci.ctypes.data_as(L.ip32), _dp(va)), self.ctx)
+        M = sp.csr_matrix((va[: self.nnz], ci[: self.nnz], rp), shape=self.shape)
+        M.has_sorted_indices = False
+        return M
+
+    def matvec_device(self, x_ptr: int, y_ptr: int):
+        _check(L.load().hgm_spmv(self.ctx.handle, self._h, C.c_void_p(x_ptr), C.c_void_p(y_ptr)), self.ctx)
+
+    def __matmul__(self, x):
+        """Host convenience y = M @ x (copies through HBM)."""
+        x = _f64(x, self.shape[1], "x")
+        ctx = self.ctx
+        lib = L.load()
+        es = 8 if self.dtype == L.HGM_F64 else 4
+        xd, yd = C.c_void_p(), C.c_void_p()
+        _check(lib.hgm_dev_alloc(ctx.handle, es * max(1, self.shape[1]), C.byref(xd)), ctx)
+        _check(lib.hgm_dev_alloc(ctx.handle, es * max(1, self.shape[0]), C.byref(yd)), ctx)
+        try:
+            xs = x if es == 8 else x.astype(np.float32)
+            _check(lib.hgm_memcpy_h2d(ctx.handle, xd, xs.ctypes.data_as(C.c_void_p), es * self.shape[1]), ctx)
+            _check(lib.hgm_spmv(ctx.handle, self._h, xd, yd), ctx)
+            y = np.empty(self.shape[0], dtype=np.float64 if es == 8 else np.float32)
+            _check(lib.hgm_memcpy_d2h(ctx.handle, y.ctypes.data_as(C.c_void_p), yd, es * self.shape[0]), ctx)
+        finally:
+            lib.hgm_dev_free(ctx.handle, xd)
+            lib.hgm_dev_free(ctx.handle, yd)
+        return y.astype(np.float64)
+
+    def close(self):
+        if self._h:
+            L.load().hgm_mat_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:   # noqa: BLE001
+            pass
+
+
+def as_operator(M, ctx=None, dtype=L.HGM_F64) -> SparseOperator:
+    if isinstance(M, SparseOperator):
+        return M
+    return SparseOperator.from_scipy(M, ctx=ctx, dtype=dtype)
+
+
+def _ops(A, B, ctx):
+    ctx = ctx or (A.ctx if isinstance(A, SparseOperator) else default_context())
+    Ao = as_operator(A, ctx)
+    if B is None:
+        Bo = Ao.T
+    else:
+        Bo = as_operator(B, ctx, Ao.dtype)
+    if Bo.shape != (Ao.shape[1], Ao.shape[0]):
+        raise ValueError(f"dimension mismatch: A is {Ao.shape}, B is {Bo.shape} (expected size(A'))")
+    return ctx, Ao, Bo
+
+
+def _opts(orth="mgs", H_out=None, device_ptrs=False):
+    o = L.hgm_opts()
+    o.flags = L.HGM_DEVICE_PTRS if device_ptrs else 0
+    o.orth = L.HGM_CGS2 if str(orth).lower() == "cgs2" else L.HGM_MGS
+    o.H_out = _dp(H_out) if H_out is not None else None
+    return o
+
+
+def _gmres_call(fn_name, A, B, b, x_true, tol, maxit, lam, ctx, orth, return_H, extra=()):
+    ctx, Ao, Bo = _ops(A, B, ctx)
+    m, n = Ao.shape
+    maxit = int(maxit)
+    b = _f64(b, m, "b")
+    xt = _f64(x_true, n, "x_true")
+    x = np.zeros(n)
+    err = np.zeros(maxit)
+    res = np.zeros(maxit)
+    it = C.c_int(0)
+    H = np.zeros((maxit + 1) * maxit) if return_H else None
+    o = _opts(orth, H)
+    fn = getattr(L.load(), fn_name)
+    if fn_name == "hgm_gmres_bounds_ex":
+        lam_, side, hyb = extra
+        rc = fn(ctx.handle, C.byref(o), Ao._h, Bo._h, _dp(b), _dp(xt), float(tol), maxit, float(lam_), side, hyb,
+                _dp(x), _dp(err), _dp(res), C.byref(it))
+    else:
+        rc = fn(ctx.handle, C.byref(o), Ao._h, Bo._h, _dp(b), _dp(xt), float(tol), maxit, float(lam),
+                _dp(x), _dp(err), _dp(res), C.byref(it))
+    _check(rc, ctx)
+    k = it.value
+    out = (x, err[:k].copy(), res[:k].copy(), k)
+    if return_H:
+        out = out + (H.reshape(maxit, maxit + 1).T.copy(),)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Reference solver signatures
+# ---------------------------------------------------------------------------
+def hybrid_ab_gmres_rtp(A, B, b, x_true, tol, maxit, lambda_, *, ctx=None, orth="mgs", return_H=False):
+    """``[x, error_norm, residual_norm, niters] = hybrid_ab_gmres_rtp(A,B,b,x_true,tol,maxit,lambda)``
+    (hybrid_ab_gmres_rtp.m:1-45): n-space Arnoldi on ``B*A + lambda*I``, projected
+    Tikhonov ``(AQk'AQk + lambda I) y = AQk' b``."""
+    return _gmres_call("hgm_hybrid_ab_gmres_rtp_ex", A, B, b, x_true, tol, maxit, lambda_, ctx, orth, return_H)
+
+
+def hybrid_ba_gmres_rtp(A, B, b, x_true, tol, maxit, lambda_, *, ctx=None, orth="mgs", return_H=False):
+    """``hybrid_ba_gmres_rtp.m:1-42``: Arnoldi on ``B*A + lambda*I``, ``yk = Hk \\ beta e1``."""
+    return _gmres_call("hgm_hybrid_ba_gmres_rtp_ex", A, B, b, x_true, tol, maxit, lambda_, ctx, orth, return_H)
+
+
+def _bounds(A, B, b, x_true, tol, maxit, lam, side, hybrid, ctx, orth, return_H):
+    out = _gmres_call("hgm_gmres_bounds_ex", A, B, b, x_true, tol, maxit, lam, ctx, orth, return_H,
+                      extra=(lam, side, hybrid))
+    # outputs 5-8 (phi_final, dphi_final, phi_iter, dphi_iter): dense spectral bounds, out of scope
+    return out[:4] + (None, None, None, None) + out[4:]
+
+
+def ABgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lambda_, DeltaM=None, *, ctx=None, orth="mgs", return_H=False):
+    """``ABgmres_hybrid_bounds.m`` outputs 1-4: m-space Arnoldi on ``A*B``, PTR Tikhonov, ``x = B*z``."""
+    return _bounds(A, B, b, x_true, tol, maxit, lambda_, L.HGM_SIDE_AB, 1, ctx, orth, return_H)
+
+
+def ABgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, *, ctx=None, orth="mgs", return_H=False):
+    """``ABgmres_nonhybrid_bounds.m`` outputs 1-4."""
+    return _bounds(A, B, b, x_true, tol, maxit, 0.0, L.HGM_SIDE_AB, 0, ctx, orth, return_H)
+
+
+def BAgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lambda_, DeltaM=None, *, ctx=None, orth="mgs", return_H=False):
+    """``BAgmres_hybrid_bounds.m`` outputs 1-4: n-space Arnoldi on ``B*A``, PTR Tikhonov."""
+    return _bounds(A, B, b, x_true, tol, maxit, lambda_, L.HGM_SIDE_BA, 1, ctx, orth, return_H)
+
+
+def BAgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, *, ctx=None, orth="mgs", return_H=False):
+    """``BAgmres_nonhybrid_bounds.m`` outputs 1-4.  The reference forms ``M = B*A``
+    explicitly (``:4``); here the operator is applied as ``B*(A*q)``."""
+    return _bounds(A, B, b, x_true, tol, maxit, 0.0, L.HGM_SIDE_BA, 0, ctx, orth, return_H)
+
+
+def _gkb_ops(A, ctx, At=None, dtype=L.HGM_F64):
+    ctx = ctx or (A.ctx if isinstance(A, SparseOperator) else default_context())
+    Ao = as_operator(A, ctx, dtype)
+    Ato = as_operator(At, ctx, Ao.dtype) if At is not None else Ao.T
+    return ctx, Ao, Ato
+
+
+def lsqr_solver(A, b, x_true, tol, maxit, *, ctx=None, At=None):
+    """``[x, error_norm, residual_norm, niters] = lsqr_solver(A,b,x_true,tol,maxit)`` (lsqr_solver.m:1-54)."""
+    ctx, Ao, Ato = _gkb_ops(A, ctx, At)
+    m, n = Ao.shape
+    maxit = int(maxit)
+    b = _f64(b, m, "b")
+    xt = _f64(x_true, n, "x_true")
+    x, err, res, it = np.zeros(n), np.zeros(maxit), np.zeros(maxit), C.c_int(0)
+    o = _opts()
+    _check(L.load().hgm_lsqr_solver_ex(ctx.handle, C.byref(o), Ao._h, Ato._h, _dp(b), _dp(xt), float(tol), maxit,
+                                       _dp(x), _dp(err), _dp(res), C.byref(it)), ctx)
+    k = it.value
+    return x, err[:k].copy(), res[:k].copy(), k
+
+
+def lsmr_solver(A, b, x_true=None, tol=None, maxit=None, *, ctx=None, At=None):
+    """``[x, err_hist, res_hist, ar_hist, iters] = lsmr_solver(A,b,x_true,tol,maxit)``
+    (lsmr_solver.m:1-83; ``tol`` defaults to 1e-6, ``maxit`` to ``min(m,n)``)."""
+    ctx, Ao, Ato = _gkb_ops(A, ctx, At)
+    m, n = Ao.shape
+    tol = 1e-6 if tol is None else float(tol)
+    maxit = min(m, n) if maxit is None else int(maxit)
+    b = _f64(b, m, "b")
+    xt = None if x_true is None or np.size(x_true) == 0 else _f64(x_true, n, "x_true")
+    x = np.zeros(n)
+    eh, rh, ah, it = np.zeros(maxit), np.zeros(maxit), np.zeros(maxit), C.c_int(0)
+    o = _opts()
+    _check(L.load().hgm_lsmr_solver_ex(ctx.handle, C.byref(o), Ao._h, Ato._h, _dp(b), _dp(xt), tol, maxit,
+                                       _dp(x), _dp(eh), _dp(rh), _dp(ah), C.byref(it)), ctx)
+    k = it.value
+    return x, eh[:k].copy(), rh[:k].copy(), ah[:k].copy(), k
+
+
+def hybrid_lsqr_solver(A, b, x_true, tol, maxit, lambda_, *, ctx=None, At=None):
+    """``hybrid_lsqr_solver.m:1-52`` (LSQR on ``[A; sqrt(lambda) I]``, augmentation implicit)."""
+    ctx, Ao, Ato = _gkb_ops(A, ctx, At)
+    m, n = Ao.shape
+    maxit = int(maxit)
+    b = _f64(b, m, "b")
+    xt = _f64(x_true, n, "x_true")
+    x, err, res, it = np.zeros(n), np.zeros(maxit), np.zeros(maxit), C.c_int(0)
+    _check(L.load().hgm_hybrid_lsqr_solver(ctx.handle, Ao._h, Ato._h, _dp(b), _dp(xt), float(tol), maxit,
+                                           float(lambda_), _dp(x), _dp(err), _dp(res), C.byref(it)), ctx)
+    k = it.value
+    return x, err[:k].copy(), res[:k].copy(), k
+
+
+def hybrid_lsmr_solver(A, b, x_true, tol, maxit, lambda_, *, ctx=None, At=None):
+    """``hybrid_lsmr_solver.m:1-57``."""
+    ctx, Ao, Ato = _gkb_ops(A, ctx, At)
+    m, n = Ao.shape
+    maxit = int(maxit)
+    b = _f64(b, m, "b")
+    xt = _f64(x_true, n, "x_true")
+    x, err, res, it = np.zeros(n), np.zeros(maxit), np.zeros(maxit), C.c_int(0)
+    _check(L.load().hgm_hybrid_lsmr_solver(ctx.handle, Ao._h, Ato._h, _dp(b), _dp(xt), float(tol), maxit,
+                                           float(lambda_), _dp(x), _dp(err), _dp(res), C.byref(it)), ctx)
+    k = it.value
+    return x, err[:k].copy(), res[:k].copy(), k
+
+
+def arnoldi(A, B, b, k, gcv_type="ba", *, ctx=None, breakdown_tol=1e-12, orth="mgs"):
+    """Arnoldi part of ``gcv_function.m:3-33``: returns (H, beta, kdone)."""
+    ctx, Ao, Bo = _ops(A, B, ctx)
+    side = L.HGM_SIDE_AB if gcv_type == "ab" else L.HGM_SIDE_BA
+    b = _f64(b, Ao.shape[0], "b")
+    H = np.zeros((k + 1) * k)
+    beta, kd = C.c_double(), C.c_int()
+    o = L.HGM_CGS2 if orth == "cgs2" else L.HGM_MGS
+    _check(L.load().hgm_arnoldi(ctx.handle, Ao._h, Bo._h, _dp(b), int(k), side, float(breakdown_tol), o,
+                                _dp(H), C.byref(beta), C.byref(kd)), ctx)
+    return H.reshape(k, k + 1).T.copy(), beta.value, kd.value
+
+
+def gcv_from_H(H, beta, lambda_, trace_m):
+    """λ-dependent part of ``gcv_function.m:35-58`` on a cached H ((k+1) x k)."""
+    H = np.asarray(H, dtype=np.float64)
+    k = H.shape[1]
+    Hf = np.ascontiguousarray(H.T).reshape(-1)
+    g = C.c_double()
+    rc = L.load().hgm_gcv_from_H(_dp(Hf), k, float(beta), float(lambda_), float(trace_m), C.byref(g))
+    if rc != L.HGM_OK:
+        raise ValueError("hgm_gcv_from_H: invalid arguments")
+    return g.value
+
+
+def gcv_function(lambda_, A, B, b, m, k_gcv, gcv_type, *, ctx=None):
+    """``gcv_val = gcv_function(lambda,A,B,b,m,k_gcv,gcv_type)`` (gcv_function.m:1-59)."""
+    ctx, Ao, Bo = _ops(A, B, ctx)
+    side = L.HGM_SIDE_AB if gcv_type == "ab" else L.HGM_SIDE_BA
+    b = _f64(b, Ao.shape[0], "b")
+    g = C.c_double()
+    _check(L.load().hgm_gcv_function(ctx.handle, float(lambda_), Ao._h, Bo._h, _dp(b), int(m), int(k_gcv), side,
+                                     C.byref(g)), ctx)
+    return g.value
+
+
+def gcv_fminbnd(H, beta, trace_m, lo=1e-9, hi=1e-1, tolx=1e-8):
+    """``fminbnd(@(l) gcv_function(l,...), lo, hi, optimset('TolX',tolx))`` on ONE cached
+    Arnoldi (analyze_regularization.m:37-46): returns (lambda_opt, gcv_opt)."""
+    H = np.asarray(H, dtype=np.float64)
+    k = H.shape[1]
+    Hf = np.ascontiguousarray(H.T).reshape(-1)
+    lo_, g = C.c_double(), C.c_double()
+    rc = L.load().hgm_gcv_fminbnd(_dp(Hf), k, float(beta), float(trace_m), float(lo), float(hi), float(tolx),
+                                  C.byref(lo_), C.byref(g))
+    if rc != L.HGM_OK:
+        raise ValueError("hgm_gcv_fminbnd: invalid arguments")
+    return lo_.value, g.value

@@ -1,0 +1,210 @@
+/*
+ * hgmres.h — C ABI of the MI355X-native Arnoldi/GMRES + Golub–Kahan inner loop.
+ *
+ * This is the drop-in boundary for the reference's solver functions
+ * (luisayang-malaxiangguo/Hybrid-GMRES, pure MATLAB).  The reference has no
+ * FFI of its own; each entry point below replaces one MATLAB function with the
+ * same positional arguments and output meaning, and is what a MATLAB mex
+ * gateway or a ctypes binding calls:
+ *
+ *   hgm_hybrid_ab_gmres_rtp  <- hybrid_ab_gmres_rtp.m:1   [x,error_norm,residual_norm,niters]
+ *   hgm_hybrid_ba_gmres_rtp  <- hybrid_ba_gmres_rtp.m:1   [x,error_norm,residual_norm,niters]
+ *   hgm_gmres_bounds         <- ABgmres_hybrid_bounds.m:1-2, ABgmres_nonhybrid_bounds.m:1-2,
+ *                               BAgmres_hybrid_bounds.m:1-2, BAgmres_nonhybrid_bounds.m:1-2
+ *                               (outputs 1-4; the dense spectral-bound outputs 5-8 are out of scope)
+ *   hgm_lsqr_solver          <- lsqr_solver.m:1           [x,error_norm,residual_norm,niters]
+ *   hgm_lsmr_solver          <- lsmr_solver.m:1           [x,err_hist,res_hist,ar_hist,iters]
+ *   hgm_hybrid_lsqr_solver   <- hybrid_lsqr_solver.m:1
+ *   hgm_hybrid_lsmr_solver   <- hybrid_lsmr_solver.m:1
+ *   hgm_gcv_function         <- gcv_function.m:1          gcv_val
+ *   hgm_arnoldi / hgm_gcv_from_H  <- gcv_function.m:18-33 / :35-58 split (Arnoldi once, lambda on H;
+ *                               pattern of plot_gcv_surface.m:58-122)
+ *   hgm_mat_create_csc       <- MATLAB sparse (CSC, jc/ir/pr) operand hand-over
+ *   hgm_spmv                 <- the `A*v` / `B*u` / `A'*u` mtimes inside every solver
+ *
+ * Conventions:
+ *   - int status: 0 ok, < 0 error (hgm_last_error(ctx) has the message).  A Krylov
+ *     breakdown (H(k+1,k) == 0) is NOT an error: the solver stops with niters = k,
+ *     exactly like the reference's `break`.  HGM_E_NOT_ASSIGNED mirrors MATLAB's
+ *     'Output argument "x" not assigned' (breakdown at k = 1 where the reference never
+ *     assigns x: hybrid_ab_gmres_rtp.m:4,33 and *_bounds.m:37-38,86).
+ *   - Caller-owned host buffers: x has size n, histories have size maxit; the
+ *     library writes *niters entries (the MATLAB wrapper truncates to 1:niters).
+ *   - Matrices are library-owned device objects behind opaque handles.
+ *   - One context = one HIP device + one HIP stream; not thread-safe per context.
+ *   - Multi-GPU: one process per GPU (hgm_ctx_create_dist over RCCL).  Operators are
+ *     pixel-sharded: rank g holds A_g = A(:,P_g) (ray-major CSR, local columns) and
+ *     B_g = B(P_g,:); n-vectors (x, x_true) are passed as the rank's shard, m-vectors
+ *     (b) replicated on every rank.
+ */
+#ifndef HGMRES_H
+#define HGMRES_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HGM_API __attribute__((visibility("default")))
+
+#define HGM_VERSION 100
+#define HGM_UNIQUE_ID_BYTES 128
+
+typedef struct hgm_ctx hgm_ctx;
+typedef struct hgm_mat hgm_mat;
+
+enum hgm_status {
+    HGM_OK = 0,
+    HGM_E_ARG = -1,          /* bad argument / dimension mismatch (MATLAB: error()) */
+    HGM_E_HIP = -2,          /* HIP runtime error */
+    HGM_E_NOMEM = -3,        /* device allocation failed */
+    HGM_E_COMM = -4,         /* RCCL / host all-reduce failure */
+    HGM_E_NOT_ASSIGNED = -5, /* MATLAB 'Output argument "x" not assigned during call' */
+    HGM_E_UNSUPPORTED = -6
+};
+
+enum hgm_dtype { HGM_F64 = 0, HGM_F32 = 1 };
+enum hgm_orth { HGM_MGS = 0, HGM_CGS2 = 1 };
+enum hgm_side { HGM_SIDE_AB = 0, HGM_SIDE_BA = 1 };
+
+/* Flags for the *_ex entry points. */
+enum hgm_flags {
+    HGM_DEVICE_PTRS = 1  /* b, x_true, x are device pointers (inputs resident in HBM) */
+};
+
+typedef struct hgm_opts {
+    int flags;        /* hgm_flags */
+    int orth;         /* hgm_orth: Arnoldi orthogonalisation (reference: MGS) */
+    double* H_out;    /* optional host buffer, (maxit+1) x maxit column-major Hessenberg */
+} hgm_opts;
+
+/* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for
+ * shard emulation / testing on one device. */
+typedef int (*hgm_allreduce_fn)(double* buf, int64_t count, void* user);
+
+/* ---- context ---------------------------------------------------------- */
+HGM_API int hgm_version(void);
+HGM_API int hgm_device_count(int* count);
+HGM_API int hgm_ctx_create(int device, hgm_ctx** ctx);
+HGM_API int hgm_comm_unique_id(void* id_out /* HGM_UNIQUE_ID_BYTES */);
+HGM_API int hgm_ctx_create_dist(int device, int rank, int world, const void* unique_id, hgm_ctx** ctx);
+HGM_API int hgm_ctx_set_host_allreduce(hgm_ctx* ctx, int rank, int world, hgm_allreduce_fn fn, void* user);
+HGM_API void hgm_ctx_destroy(hgm_ctx* ctx);
+HGM_API const char* hgm_last_error(const hgm_ctx* ctx);
+HGM_API int hgm_ctx_synchronize(hgm_ctx* ctx);
+HGM_API void* hgm_ctx_stream(hgm_ctx* ctx);
+HGM_API int hgm_ctx_rank(const hgm_ctx* ctx, int* rank, int* world);
+
+/* ---- sparse operators --------------------------------------------------- */
+/* CSR from host arrays (row_ptr: rows+1 int64, col_idx: nnz int32, val: nnz
+ * doubles; dtype selects the device storage precision). */
+HGM_API int hgm_mat_create_csr(hgm_ctx* ctx, int64_t rows, int64_t cols, int64_t nnz,
+                               const int64_t* row_ptr, const int32_t* col_idx,
+                               const double* val, int dtype, hgm_mat** out);
+/* MATLAB sparse hand-over: CSC of an rows x cols matrix (jc: cols+1, ir: nnz,
+ * pr: nnz, 64-bit mwIndex).  The device CSR (row-major) is built by a
+ * deterministic device transpose. */
+HGM_API int hgm_mat_create_csc(hgm_ctx* ctx, int64_t rows, int64_t cols, int64_t nnz,
+                               const int64_t* jc, const int64_t* ir, const double* pr,
+                               int dtype, hgm_mat** out);
+/* Deterministic device transpose (stable: entries of each output row keep
+ * increasing column order). */
+HGM_API int hgm_mat_transpose(hgm_ctx* ctx, const hgm_mat* in, hgm_mat** out);
+/* Parallel-beam Siddon projector generated on the device (ray-major CSR,
+ * bit-compatible geometry with hgmres.problems.siddon_projector). */
+HGM_API int hgm_mat_create_siddon(hgm_ctx* ctx, int N, int n_angles, double det_offset,
+                                  int dtype, hgm_mat** out);
+HGM_API int hgm_mat_info(const hgm_mat* mat, int64_t* rows, int64_t* cols, int64_t* nnz, int* dtype);
+HGM_API int hgm_mat_download(hgm_ctx* ctx, const hgm_mat* mat, int64_t* row_ptr, int32_t* col_idx, double* val);
+HGM_API void hgm_mat_destroy(hgm_mat* mat);
+
+/* y = A*x on device pointers (elements of the matrix dtype), on the context stream. */
+HGM_API int hgm_spmv(hgm_ctx* ctx, const hgm_mat* A, const void* x_dev, void* y_dev);
+
+/* ---- device memory helpers (for callers without their own allocator) ---- */
+HGM_API int hgm_dev_alloc(hgm_ctx* ctx, int64_t bytes, void** ptr);
+HGM_API int hgm_dev_free(hgm_ctx* ctx, void* ptr);
+HGM_API int hgm_memcpy_h2d(hgm_ctx* ctx, void* dst, const void* src, int64_t bytes);
+HGM_API int hgm_memcpy_d2h(hgm_ctx* ctx, void* dst, const void* src, int64_t bytes);
+
+/* ---- solvers (MATLAB signatures; host buffers) --------------------------- */
+HGM_API int hgm_hybrid_ab_gmres_rtp(hgm_ctx* ctx, const hgm_mat* A, const hgm_mat* B,
+                                    const double* b, const double* x_true, double tol, int maxit,
+                                    double lambda, double* x, double* error_norm,
+                                    double* residual_norm, int* niters);
+HGM_API int hgm_hybrid_ba_gmres_rtp(hgm_ctx* ctx, const hgm_mat* A, const hgm_mat* B,
+                                    const double* b, const double* x_true, double tol, int maxit,
+                                    double lambda, double* x, double* error_norm,
+                                    double* residual_norm, int* niters);
+/* side = HGM_SIDE_AB (m-space Arnoldi on A*B) or HGM_SIDE_BA (n-space on B*A);
+ * hybrid = 1: PTR Tikhonov (HkᵀHk+λI)\(Hkᵀ t), 0: GMRES Hk\βe1. */
+HGM_API int hgm_gmres_bounds(hgm_ctx* ctx, const hgm_mat* A, const hgm_mat* B, const double* b,
+                             const double* x_true, double tol, int maxit, double lambda, int side,
+                             int hybrid, double* x, double* error_norm, double* residual_norm,
+                             int* niters);
+HGM_API int hgm_lsqr_solver(hgm_ctx* ctx, const hgm_mat* A, const hgm_mat* At, const double* b,
+                            const double* x_true, double tol, int maxit, double* x,
+                            double* error_norm, double* residual_norm, int* niters);
+/* x_true may be NULL (err_hist stays NaN, lsmr_solver.m:28,72). */
+HGM_API int hgm_lsmr_solver(hgm_ctx* ctx, const hgm_mat* A, const hgm_mat* At, const double* b,
+                            const double* x_true, double tol, int maxit, double* x,
+                            double* err_hist, double* res_hist, double* ar_hist, int* iters);
+HGM_API int hgm_hybrid_lsqr_solver(hgm_ctx* ctx, const hgm_mat* A, const hgm_mat* At,
+                                   const double* b, const double* x_true, double tol, int maxit,
+                                   double lambda, double* x, double* error_norm,
+                                   double* residual_norm, int* niters);
+HGM_API int hgm_hybrid_lsmr_solver(hgm_ctx* ctx, const hgm_mat* A, const hgm_mat* At,
+                                   const double* b, const double* x_true, double tol, int maxit,
+                                   double lambda, double* x, double* error_norm,
+                                   double* residual_norm, int* niters);
+
+/* Extended forms: options (device pointers, orthogonalisation, Hessenberg out). */
+HGM_API int hgm_hybrid_ab_gmres_rtp_ex(hgm_ctx* ctx, const hgm_opts* opts, const hgm_mat* A,
+                                       const hgm_mat* B, const double* b, const double* x_true,
+                                       double tol, int maxit, double lambda, double* x,
+                                       double* error_norm, double* residual_norm, int* niters);
+HGM_API int hgm_hybrid_ba_gmres_rtp_ex(hgm_ctx* ctx, const hgm_opts* opts, const hgm_mat* A,
+                                       const hgm_mat* B, const double* b, const double* x_true,
+                                       double tol, int maxit, double lambda, double* x,
+                                       double* error_norm, double* residual_norm, int* niters);
+HGM_API int hgm_gmres_bounds_ex(hgm_ctx* ctx, const hgm_opts* opts, const hgm_mat* A,
+                                const hgm_mat* B, const double* b, const double* x_true, double tol,
+                                int maxit, double lambda, int side, int hybrid, double* x,
+                                double* error_norm, double* residual_norm, int* niters);
+HGM_API int hgm_lsqr_solver_ex(hgm_ctx* ctx, const hgm_opts* opts, const hgm_mat* A,
+                               const hgm_mat* At, const double* b, const double* x_true, double tol,
+                               int maxit, double* x, double* error_norm, double* residual_norm,
+                               int* niters);
+HGM_API int hgm_lsmr_solver_ex(hgm_ctx* ctx, const hgm_opts* opts, const hgm_mat* A,
+                               const hgm_mat* At, const double* b, const double* x_true, double tol,
+                               int maxit, double* x, double* err_hist, double* res_hist,
+                               double* ar_hist, int* iters);
+
+/* ---- GCV (gcv_function.m) ------------------------------------------------ */
+/* Arnoldi only: H is (k+1) x k column-major (zero columns kept after a break,
+ * gcv_function.m:33); *kdone = steps completed before the < breakdown_tol break. */
+HGM_API int hgm_arnoldi(hgm_ctx* ctx, const hgm_mat* A, const hgm_mat* B, const double* b,
+                        int k, int side, double breakdown_tol, int orth, double* H,
+                        double* beta, int* kdone);
+/* λ-dependent part of gcv_function.m:35-58 on a cached H (host only). */
+HGM_API int hgm_gcv_from_H(const double* H, int k, double beta, double lambda, double trace_m,
+                           double* gcv_val);
+HGM_API int hgm_gcv_function(hgm_ctx* ctx, double lambda, const hgm_mat* A, const hgm_mat* B,
+                             const double* b, int64_t m, int k_gcv, int side, double* gcv_val);
+/* fminbnd (Brent) over λ ∈ [lo, hi] of GCV on one cached Arnoldi (analyze_regularization.m:37-46). */
+HGM_API int hgm_gcv_fminbnd(const double* H, int k, double beta, double trace_m, double lo,
+                            double hi, double tolx, double* lambda_opt, double* gcv_opt);
+
+/* ---- timing hooks used by bench.py ---------------------------------------- */
+/* Average device time (ms) of the named kernel class over the calls since the
+ * last reset, measured with HIP events on the context stream.  classes:
+ * 0 = SpMV on A (ray-major), 1 = SpMV on B/Aᵀ (pixel-major), 2 = MGS pass. */
+HGM_API int hgm_kernel_timing(hgm_ctx* ctx, int enable);
+HGM_API int hgm_kernel_timing_read(hgm_ctx* ctx, int cls, double* total_ms, int64_t* calls,
+                                   double* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HGMRES_H */

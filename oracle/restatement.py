@@ -1,0 +1,480 @@
+"""ORACLE — CPU restatement of the reference MATLAB solvers (test infrastructure only).
+
+This module is the checker, never the product: only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import it.
+
+Each function restates one reference ``.m`` file line by line, in numpy/scipy,
+with the reference file:line cited beside each step.  MATLAB semantics kept
+(SURVEY.md Appendix A):
+
+* operator order ``B*(A*v) + lambda*v`` (two roundings for the epilogue);
+* modified Gram–Schmidt with the *updated* ``v`` in each inner product;
+* normalisation by division (``v / H(k+1,k)``), breakdown on exact ``== 0``
+  (``< 1e-12`` in ``gcv_function.m:30``);
+* ``mldivide``: square symmetric with positive diagonal -> Cholesky, falling
+  back to LU; rectangular -> Householder QR least squares (:func:`mldivide`);
+* histories pre-allocated to ``maxit`` and truncated to ``1:niters``;
+  ``niters = k`` even after a breakdown ``break``;
+* MATLAB "output argument not assigned" errors raised as ``UnboundLocalError``-
+  like :class:`OutputNotAssigned`.
+
+PARITY STATUS: **parity unpinned** with respect to reference artefacts.  The
+reference is MATLAB (absent from this image and the GPU box), ships no tests,
+fixtures or golden vectors, and depends on un-vendored Regularization Tools /
+``PRtomo_mismatched``.  The restatement is instead
+cross-checked against independent implementations of the same published
+algorithms (``scipy.sparse.linalg.lsqr`` / ``lsmr``, a dense Krylov least-squares
+solve) and against the equivalences the reference itself asserts in
+``run_equivalence_plots.m:12-22`` and ``run_ptr_rtp_comparison.m:15-19``
+(see ``tests/test_oracle.py``).
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.linalg as sla
+import scipy.sparse as sp
+
+EPS = np.finfo(np.float64).eps
+
+
+class OutputNotAssigned(RuntimeError):
+    """MATLAB: 'Output argument "x" not assigned during call'."""
+
+
+def _norm(v):
+    return float(np.linalg.norm(v))
+
+
+def mldivide(M, rhs):
+    """MATLAB ``M \\ rhs`` for the small dense systems the solvers form.
+
+    Square + symmetric + positive diagonal -> Cholesky (falls back to LU when
+    not positive definite); square otherwise -> LU; rectangular -> QR least
+    squares with column pivoting (LAPACK xGEQP3, as MATLAB)."""
+    M = np.asarray(M, dtype=np.float64)
+    rhs = np.asarray(rhs, dtype=np.float64)
+    r, c = M.shape
+    if r == c:
+        if np.array_equal(M, M.T) and np.all(np.diag(M) > 0):
+            try:
+                cf = sla.cho_factor(M, lower=False, check_finite=False)
+                return sla.cho_solve(cf, rhs, check_finite=False)
+            except np.linalg.LinAlgError:
+                pass
+        return sla.solve(M, rhs, check_finite=False)
+    Qm, R, piv = sla.qr(M, mode="economic", pivoting=True, check_finite=False)
+    z = sla.solve_triangular(R, Qm.T @ rhs, check_finite=False)
+    y = np.empty_like(z)
+    y[piv] = z
+    return y
+
+
+def _mgs_arnoldi_step(Q, H, k, v, breakdown_tol=None):
+    """Arnoldi MGS inner loop, ``hybrid_ba_gmres_rtp.m:20-26`` (0-based k).
+    Returns True on breakdown."""
+    for j in range(k + 1):                       # :20  for j = 1:k
+        H[j, k] = Q[:, j] @ v                    # :21  H(j,k) = Q(:,j)'*v
+        v = v - H[j, k] * Q[:, j]                # :22  v = v - H(j,k)*Q(:,j)
+    H[k + 1, k] = _norm(v)                       # :24  H(k+1,k) = norm(v)
+    if breakdown_tol is None:
+        if H[k + 1, k] == 0:                     # :25  if H(k+1,k) == 0, break
+            return True
+    elif H[k + 1, k] < breakdown_tol:            # gcv_function.m:30
+        return True
+    Q[:, k + 1] = v / H[k + 1, k]                # :26  Q(:,k+1) = v / H(k+1,k)
+    return False
+
+
+def hybrid_ba_gmres_rtp(A, B, b, x_true, tol, maxit, lam, return_H=False):
+    """``hybrid_ba_gmres_rtp.m:1-42``."""
+    n = A.shape[1]                               # :3
+    x = np.zeros(n)                              # :4
+    M_reg = lambda v: B @ (A @ v) + lam * v      # :6
+    d = B @ b                                    # :7
+    r0 = d - M_reg(x)                            # :9
+    beta = _norm(r0)                             # :10
+    Q = np.zeros((n, maxit + 1))                 # :11
+    H = np.zeros((maxit + 1, maxit))             # :12
+    Q[:, 0] = r0 / beta                          # :13
+    error_norm = np.zeros(maxit)                 # :15
+    residual_norm = np.zeros(maxit)              # :16
+    nb, nxt = _norm(b), _norm(x_true)
+    k = 0
+    for k in range(maxit):                       # :18
+        v = M_reg(Q[:, k])                       # :19
+        if _mgs_arnoldi_step(Q, H, k, v):        # :20-26
+            break
+        Hk = H[: k + 2, : k + 1]                 # :28
+        rhs = np.zeros(k + 2)
+        rhs[0] = beta
+        yk = mldivide(Hk, rhs)                   # :29
+        x = Q[:, : k + 1] @ yk                   # :30
+        residual_norm[k] = _norm(b - A @ x) / nb     # :32
+        error_norm[k] = _norm(x - x_true) / nxt      # :33
+        if residual_norm[k] <= tol:              # :35
+            break
+    niters = k + 1                               # :38
+    out = (x, error_norm[:niters], residual_norm[:niters], niters)
+    return out + (H,) if return_H else out
+
+
+def hybrid_ab_gmres_rtp(A, B, b, x_true, tol, maxit, lam, return_H=False):
+    """``hybrid_ab_gmres_rtp.m:1-45`` (n-space Arnoldi on B*A + lambda*I)."""
+    n = A.shape[1]                               # :3
+    x0 = np.zeros(n)                             # :4
+    M_reg_op = lambda v: B @ (A @ v) + lam * v   # :6
+    d_krylov = B @ b                             # :7
+    r0 = d_krylov - M_reg_op(x0)                 # :9
+    beta = _norm(r0)                             # :10
+    Q = np.zeros((n, maxit + 1))                 # :11
+    H = np.zeros((maxit + 1, maxit))             # :12
+    Q[:, 0] = r0 / beta                          # :13
+    error_norm = np.zeros(maxit)
+    residual_norm = np.zeros(maxit)
+    nb, nxt = _norm(b), _norm(x_true)
+    x = None
+    k = 0
+    for k in range(maxit):                       # :18
+        v = M_reg_op(Q[:, k])                    # :19
+        if _mgs_arnoldi_step(Q, H, k, v):        # :20-26
+            break
+        Qk = Q[:, : k + 1]                       # :28
+        AQk = A @ Qk                             # :31
+        G = AQk.T @ AQk
+        yk = mldivide(G + lam * np.eye(k + 1), AQk.T @ b)   # :32
+        x = Qk @ yk                              # :33
+        residual_norm[k] = _norm(b - A @ x) / nb     # :35
+        error_norm[k] = _norm(x - x_true) / nxt      # :36
+        if residual_norm[k] <= tol:              # :38
+            break
+    if x is None:                                # breakdown at k=1: x never assigned
+        raise OutputNotAssigned('Output argument "x" not assigned (hybrid_ab_gmres_rtp)')
+    niters = k + 1                               # :41
+    out = (x, error_norm[:niters], residual_norm[:niters], niters)
+    return out + (H,) if return_H else out
+
+
+def lsqr_solver(A, b, x_true, tol, maxit):
+    """``lsqr_solver.m:1-54``."""
+    n = A.shape[1]
+    x = np.zeros(n)                              # :5
+    beta = _norm(b)                              # :7
+    u = b / beta                                 # :8
+    v_hat = A.T @ u                              # :10
+    alpha = _norm(v_hat)                         # :11
+    v = v_hat / alpha                            # :12
+    w = v.copy()                                 # :14
+    phi_bar = beta                               # :15
+    rho_bar = alpha                              # :16
+    error_norm = np.zeros(maxit)
+    residual_norm = np.zeros(maxit)
+    nb, nxt = _norm(b), _norm(x_true)
+    k = 0
+    for k in range(maxit):                       # :20
+        u_hat = A @ v - alpha * u                # :22
+        beta = _norm(u_hat)                      # :23
+        u = u_hat / beta                         # :24
+        v_hat = A.T @ u - beta * v               # :26
+        alpha = _norm(v_hat)                     # :27
+        v = v_hat / alpha                        # :28
+        rho = np.sqrt(rho_bar ** 2 + beta ** 2)  # :31
+        c = rho_bar / rho                        # :32
+        s = beta / rho                           # :33
+        theta = s * alpha                        # :35
+        rho_bar = -c * alpha                     # :36
+        phi = c * phi_bar                        # :37
+        phi_bar = s * phi_bar                    # :38
+        x = x + (phi / rho) * w                  # :40
+        w = v - (theta / rho) * w                # :41
+        error_norm[k] = _norm(x - x_true) / nxt  # :43
+        residual_norm[k] = abs(phi_bar) / nb     # :44
+        if residual_norm[k] <= tol:              # :46
+            break
+    niters = k + 1                               # :49
+    error_norm = error_norm[:niters]
+    residual_norm = residual_norm[:niters].copy()
+    residual_norm[-1] = _norm(b - A @ x) / nb    # :52
+    return x, error_norm, residual_norm, niters
+
+
+def lsmr_solver(A, b, x_true=None, tol=None, maxit=None):
+    """``lsmr_solver.m:1-83`` (defaults ``:3,5``)."""
+    if tol is None:
+        tol = 1e-6                               # :3
+    m, n = A.shape                               # :4
+    if maxit is None:
+        maxit = min(m, n)                        # :5
+    x = np.zeros(n)                              # :7
+    u = b.copy()                                 # :10
+    beta = _norm(u)                              # :11
+    if beta > 0:
+        u = u / beta                             # :12
+    v = A.T @ u                                  # :14
+    alpha = _norm(v)                             # :15
+    if alpha > 0:
+        v = v / alpha                            # :16
+    zetabar = alpha * beta                       # :19
+    alphabar = alpha                             # :20
+    rho = 1.0                                    # :21
+    rhobar = 1.0                                 # :22
+    cbar, sbar = 1.0, 0.0                        # :23
+    h = v.copy()                                 # :25
+    hbar = np.zeros(n)                           # :26
+    err_hist = np.full(maxit, np.nan)            # :28
+    res_hist = np.zeros(maxit)                   # :29
+    ar_hist = np.zeros(maxit)                    # :30
+    nb = _norm(b)
+    normA = float(sp.linalg.norm(A, "fro")) if sp.issparse(A) else float(np.linalg.norm(A, "fro"))
+    k = 0
+    for k in range(maxit):                       # :32
+        u = A @ v - alpha * u                    # :34
+        beta = _norm(u)                          # :35
+        if beta > 0:
+            u = u / beta                         # :36
+        v = A.T @ u - beta * v                   # :38
+        alpha = _norm(v)                         # :39
+        if alpha > 0:
+            v = v / alpha                        # :40
+        alphahat = alphabar                      # :42
+        rhoold = rho                             # :43
+        rho = np.hypot(alphahat, beta)           # :44
+        c = alphahat / rho                       # :45
+        s = beta / rho                           # :46
+        thetanew = s * alpha                     # :48
+        alphabar = c * alpha                     # :49
+        rhobarold = rhobar                       # :51
+        thetabar = sbar * rho                    # :52
+        rhobar = np.hypot(cbar * rho, thetanew)  # :53
+        cbar = (cbar * rho) / rhobar             # :54
+        sbar = thetanew / rhobar                 # :55
+        zeta = cbar * zetabar                    # :58
+        zetabar = -sbar * zetabar                # :59
+        if k == 0:
+            hbar = h.copy()                      # :62
+        else:
+            hbar = h - (thetabar * rho) / (rhoold * rhobarold) * hbar   # :64
+        x = x + (zeta / (rho * rhobar)) * hbar   # :66
+        h = v - (thetanew / rho) * h             # :67
+        r = b - A @ x                            # :69
+        res_hist[k] = _norm(r) / (nb + EPS)      # :70
+        ar_hist[k] = _norm(A.T @ r) / (normA * max(_norm(r), EPS))   # :71
+        if x_true is not None and np.size(x_true) > 0:
+            err_hist[k] = _norm(x - x_true) / _norm(x_true)           # :72-73
+        if res_hist[k] < tol:                    # :76
+            break
+    iters = k + 1                                # :79
+    return x, err_hist[:iters], res_hist[:iters], ar_hist[:iters], iters
+
+
+def hybrid_lsqr_solver(A, b, x_true, tol, maxit, lam):
+    """``hybrid_lsqr_solver.m:1-52`` (explicit augmentation ``:5-6``)."""
+    m, n = A.shape
+    A_aug = sp.vstack([sp.csr_matrix(A), np.sqrt(lam) * sp.identity(n, format="csr")]).tocsr()   # :5
+    b_aug = np.concatenate([b, np.zeros(n)])     # :6
+    x = np.zeros(n)                              # :8
+    beta_aug = _norm(b_aug)                      # :9
+    u_aug = b_aug / beta_aug                     # :10
+    v_hat = A_aug.T @ u_aug                      # :11
+    alpha_aug = _norm(v_hat)                     # :12
+    v = v_hat / alpha_aug                        # :13
+    w = v.copy()                                 # :14
+    phi_bar = beta_aug                           # :15
+    rho_bar = alpha_aug                          # :16
+    error_norm = np.zeros(maxit)
+    residual_norm = np.zeros(maxit)
+    nb, nxt = _norm(b), _norm(x_true)
+    k = 0
+    for k in range(maxit):                       # :21
+        u_hat = A_aug @ v - alpha_aug * u_aug    # :22
+        beta_aug = _norm(u_hat)                  # :23
+        u_aug = u_hat / beta_aug                 # :24
+        v_hat = A_aug.T @ u_aug - beta_aug * v   # :26
+        alpha_aug = _norm(v_hat)                 # :27
+        v = v_hat / alpha_aug                    # :28
+        rho = np.sqrt(rho_bar ** 2 + beta_aug ** 2)   # :30
+        c = rho_bar / rho                        # :31
+        s = beta_aug / rho                       # :32
+        theta = s * alpha_aug                    # :34
+        rho_bar = -c * alpha_aug                 # :35
+        phi = c * phi_bar                        # :36
+        phi_bar = s * phi_bar                    # :37
+        x = x + (phi / rho) * w                  # :39
+        w = v - (theta / rho) * w                # :40
+        error_norm[k] = _norm(x - x_true) / nxt  # :42
+        residual_norm[k] = _norm(b - A @ x) / nb # :43
+        if residual_norm[k] < tol:               # :45
+            break
+    niters = k + 1
+    return x, error_norm[:niters], residual_norm[:niters], niters
+
+
+def hybrid_lsmr_solver(A, b, x_true, tol, maxit, lam):
+    """``hybrid_lsmr_solver.m:1-57``."""
+    n = A.shape[1]
+    x = np.zeros(n)                              # :4
+    u = b.copy()                                 # :6
+    beta1 = _norm(u)                             # :7
+    u = u / beta1                                # :8
+    V = np.zeros((n, maxit))                     # :10
+    B_k = np.zeros((maxit + 1, maxit))           # :11
+    v_hat = A.T @ u                              # :13
+    alpha1 = _norm(v_hat)                        # :14
+    v = v_hat / alpha1                           # :15
+    V[:, 0] = v                                  # :16
+    error_norm = np.zeros(maxit)
+    residual_norm = np.zeros(maxit)
+    nb, nxt = _norm(b), _norm(x_true)
+    k = 0
+    for k in range(maxit):                       # :21
+        B_k[k, k] = alpha1                       # :23
+        u_hat = A @ v - alpha1 * u               # :24
+        beta_k = _norm(u_hat)                    # :25
+        u = u_hat / beta_k                       # :26
+        B_k[k + 1, k] = beta_k                   # :27
+        if k < maxit - 1:                        # :29
+            v_hat = A.T @ u - beta_k * v         # :30
+            alpha_k_plus_1 = _norm(v_hat)        # :31
+            v = v_hat / alpha_k_plus_1           # :32
+            V[:, k + 1] = v                      # :33
+            alpha1 = alpha_k_plus_1              # :34
+        Bk = B_k[: k + 2, : k + 1]               # :37
+        alpha_k1 = alpha1                        # :38
+        beta_k1 = beta_k                         # :39
+        G = Bk.T @ Bk
+        E11 = np.zeros((k + 1, k + 1))
+        E11[0, 0] = 1.0
+        LHS = G @ G + (alpha_k1 * beta_k1) ** 2 * E11 + lam * np.eye(k + 1)   # :41
+        e1 = np.zeros(k + 1)
+        e1[0] = 1.0
+        RHS = B_k[0, 0] * beta1 * (G @ e1)       # :42
+        yk = mldivide(LHS, RHS)                  # :44
+        x = V[:, : k + 1] @ yk                   # :45
+        error_norm[k] = _norm(x - x_true) / nxt  # :47
+        residual_norm[k] = _norm(b - A @ x) / nb # :48
+        if residual_norm[k] <= tol:              # :50
+            break
+    niters = k + 1
+    return x, error_norm[:niters], residual_norm[:niters], niters
+
+
+def _gmres_ptr(A, B, b, x_true, tol, maxit, lam, side, hybrid, explicit_BA=False, return_H=False):
+    """Arnoldi + projected-solve part of ``{AB,BA}gmres_{hybrid,nonhybrid}_bounds.m``
+    (lines cited per variant below).  The spectral-bound outputs
+    (``phi_*``/``dphi_*``) are out of scope."""
+    m, n = A.shape
+    if side == "ab":
+        r0 = b - A @ (B @ np.zeros(B.shape[1]))  # AB*_bounds.m:11-12
+        dim = m
+        op = lambda q: A @ (B @ q)               # AB*_bounds.m:25
+    else:
+        if hybrid:
+            r0 = B @ (b - A @ np.zeros(n))       # BAgmres_hybrid_bounds.m:12-13
+            op = lambda q: B @ (A @ q)           # BAgmres_hybrid_bounds.m:25
+        else:
+            r0 = B @ b                           # BAgmres_nonhybrid_bounds.m:12-13
+            if explicit_BA:
+                M = (B @ A)                      # BAgmres_nonhybrid_bounds.m:4
+                op = lambda q: M @ q             # :25
+            else:
+                op = lambda q: B @ (A @ q)
+        dim = n
+    beta = _norm(r0)
+    Q = np.zeros((dim, maxit + 1))
+    H = np.zeros((maxit + 1, maxit))
+    Q[:, 0] = r0 / beta
+    res = np.zeros(maxit)
+    err = np.zeros(maxit)
+    nb, nxt = _norm(b), _norm(x_true)
+    xk = None
+    k = 0
+    for k in range(maxit):                       # :24
+        v = op(Q[:, k])                          # :25
+        if _mgs_arnoldi_step(Q, H, k, v):        # :26-32
+            break
+        Hk = H[: k + 2, : k + 1]
+        tk = np.zeros(k + 2)
+        tk[0] = beta
+        if hybrid:
+            yk = mldivide(Hk.T @ Hk + lam * np.eye(k + 1), Hk.T @ tk)   # hybrid :34-36
+        else:
+            yk = mldivide(Hk, tk)                # nonhybrid :35
+        zk = Q[:, : k + 1] @ yk                  # :37 / :36
+        xk = B @ zk if side == "ab" else zk      # AB :38 ; BA :37
+        res[k] = _norm(b - A @ xk) / nb          # :40 / :39
+        err[k] = _norm(xk - x_true) / nxt        # :41 / :40
+        if res[k] <= tol:                        # :83 / :78 / :79
+            break
+    if xk is None:
+        raise OutputNotAssigned('Output argument "x" not assigned (*gmres_*_bounds)')
+    niters = k + 1
+    out = (xk, err[:niters], res[:niters], niters)
+    return out + (H,) if return_H else out
+
+
+def ABgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lam, DeltaM=None, return_H=False):
+    """``ABgmres_hybrid_bounds.m:11-41,83-88`` (first four outputs)."""
+    return _gmres_ptr(A, B, b, x_true, tol, maxit, lam, "ab", True, return_H=return_H)
+
+
+def ABgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, return_H=False):
+    """``ABgmres_nonhybrid_bounds.m:12-40,78-83``."""
+    return _gmres_ptr(A, B, b, x_true, tol, maxit, 0.0, "ab", False, return_H=return_H)
+
+
+def BAgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lam, DeltaM=None, return_H=False):
+    """``BAgmres_hybrid_bounds.m:11-40,79-84``."""
+    return _gmres_ptr(A, B, b, x_true, tol, maxit, lam, "ba", True, return_H=return_H)
+
+
+def BAgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, explicit_BA=True, return_H=False):
+    """``BAgmres_nonhybrid_bounds.m:4,12-40,79-84`` — uses the explicit product
+    ``M = B*A`` as the reference does (``:4,25``)."""
+    return _gmres_ptr(A, B, b, x_true, tol, maxit, 0.0, "ba", False,
+                      explicit_BA=explicit_BA, return_H=return_H)
+
+
+def arnoldi(A, B, b, k_gcv, gcv_type, breakdown_tol=1e-12):
+    """Arnoldi part of ``gcv_function.m:3-33``: returns (H, beta) with H of
+    size (k_gcv+1) x k_gcv (zero columns kept after a break, ``:33``)."""
+    if gcv_type == "ab":
+        r0 = b                                   # :5
+        dim = A.shape[0]
+        op = lambda q: A @ (B @ q)               # :20
+    else:
+        r0 = B @ b                               # :8
+        dim = A.shape[1]
+        op = lambda q: B @ (A @ q)               # :22
+    beta = _norm(r0)                             # :12
+    Q = np.zeros((dim, k_gcv + 1))               # :13
+    H = np.zeros((k_gcv + 1, k_gcv))             # :14
+    Q[:, 0] = r0 / beta                          # :15
+    for k in range(k_gcv):                       # :18
+        v = op(Q[:, k])
+        if _mgs_arnoldi_step(Q, H, k, v, breakdown_tol=breakdown_tol):   # :25-31
+            break
+    return H, beta
+
+
+def gcv_from_H(H, beta, lam, trace_m):
+    """λ-dependent part of ``gcv_function.m:33-58`` on a cached H."""
+    k = H.shape[1]                               # :33
+    Hk = H[: k + 1, :k]                          # :35
+    tk = np.zeros(k + 1)
+    tk[0] = beta                                 # :16,:36
+    yk = mldivide(Hk.T @ Hk + lam * np.eye(k), Hk.T @ tk)   # :38
+    residual_norm_sq = _norm(tk - Hk @ yk) ** 2  # :40
+    s_diag = np.linalg.svd(H[:k, :k], compute_uv=False)     # :42-43
+    trace_val = np.sum(s_diag ** 2 / (s_diag ** 2 + lam))   # :51
+    denominator = (trace_m - trace_val) ** 2     # :52
+    with np.errstate(divide="ignore", invalid="ignore"):
+        gcv_val = residual_norm_sq / denominator  # :54
+    if np.isnan(gcv_val) or np.isinf(gcv_val) or denominator < EPS:   # :56
+        gcv_val = 1e20                           # :57
+    return float(gcv_val)
+
+
+def gcv_function(lam, A, B, b, m, k_gcv, gcv_type):
+    """``gcv_function.m:1-59``."""
+    H, beta = arnoldi(A, B, b, k_gcv, gcv_type)
+    trace_m = m if gcv_type == "ab" else A.shape[1]   # :46-50
+    return gcv_from_H(H, beta, lam, trace_m)

@@ -1,0 +1,73 @@
+"""Generate the committed golden fixtures under tests/golden/.
+
+The reference (MATLAB) cannot run in this image or on the GPU box and ships no
+fixtures, so these vectors are produced by the CPU restatement in
+``oracle/restatement.py`` on small synthetic tomography problems.  Inputs are
+stored raw (CSR arrays, b, x_true); outputs are the reference-semantics
+solver results.  Regenerate with:  python tests/golden/make_golden.py
+"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "hybrid-gmres_amd"))
+sys.path.insert(0, ROOT)
+
+from hgmres.problems import tomo_problem  # noqa: E402
+from oracle import restatement as R       # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def csr_hash(M):
+    h = hashlib.sha256()
+    for a in (M.indptr.astype(np.int64), M.indices.astype(np.int32), M.data.astype(np.float64)):
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def dump(name, P, maxit, lam, tol=0.0, store_raw=True):
+    A, B, b, xt = P.A, P.B, P.b, P.x_true
+    d = {"maxit": maxit, "lam": lam, "tol": tol, "N": P.N, "n_angles": P.n_angles,
+         "A_sha256": csr_hash(A), "B_sha256": csr_hash(B), "b": b, "x_true": xt}
+    if store_raw:
+        d.update(A_indptr=A.indptr.astype(np.int64), A_indices=A.indices.astype(np.int32), A_data=A.data.copy(),
+                 B_indptr=B.indptr.astype(np.int64), B_indices=B.indices.astype(np.int32), B_data=B.data.copy(),
+                 shape=np.array(A.shape))
+    x, e, r, k, H = R.hybrid_ab_gmres_rtp(A, B, b, xt, tol, maxit, lam, return_H=True)
+    d.update(hab_x=x, hab_err=e, hab_res=r, hab_k=k, hab_H=H)
+    x, e, r, k, H = R.hybrid_ba_gmres_rtp(A, B, b, xt, tol, maxit, lam, return_H=True)
+    d.update(hba_x=x, hba_err=e, hba_res=r, hba_k=k, hba_H=H)
+    for tag, f, args in (("abp", R.ABgmres_hybrid_bounds, (lam,)), ("abn", R.ABgmres_nonhybrid_bounds, ()),
+                         ("bap", R.BAgmres_hybrid_bounds, (lam,)), ("ban", R.BAgmres_nonhybrid_bounds, ())):
+        x, e, r, k, H = f(A, B, b, xt, tol, maxit, *args, return_H=True)
+        d.update({f"{tag}_x": x, f"{tag}_err": e, f"{tag}_res": r, f"{tag}_k": k, f"{tag}_H": H})
+    x, e, r, k = R.lsqr_solver(A, b, xt, tol, maxit)
+    d.update(lsqr_x=x, lsqr_err=e, lsqr_res=r, lsqr_k=k)
+    x, e, r, a, k = R.lsmr_solver(A, b, xt, tol, maxit)
+    d.update(lsmr_x=x, lsmr_err=e, lsmr_res=r, lsmr_ar=a, lsmr_k=k)
+    x, e, r, k = R.hybrid_lsqr_solver(A, b, xt, tol, maxit, lam)
+    d.update(hlsqr_x=x, hlsqr_err=e, hlsqr_res=r, hlsqr_k=k)
+    x, e, r, k = R.hybrid_lsmr_solver(A, b, xt, tol, maxit, lam)
+    d.update(hlsmr_x=x, hlsmr_err=e, hlsmr_res=r, hlsmr_k=k)
+    m = A.shape[0]
+    for typ in ("ab", "ba"):
+        H, beta = R.arnoldi(A, B, b, maxit, typ)
+        d[f"gcv_{typ}_H"] = H
+        d[f"gcv_{typ}_beta"] = beta
+        d[f"gcv_{typ}_vals"] = np.array([R.gcv_function(l, A, B, b, m, maxit, typ) for l in (1e-6, 1e-4, 1e-2)])
+    np.savez_compressed(os.path.join(OUT, name), **d)
+    print("wrote", name, {k: (v.shape if hasattr(v, "shape") else v) for k, v in d.items() if "sha" in k or k == "shape"})
+
+
+if __name__ == "__main__":
+    # matched back-projector B = A^T (run_equivalence_plots.m:5 style), 24^2 phantom, 12 angles
+    dump("tomo24_matched.npz", tomo_problem(24, 12, noise=1e-2, seed=0, backprojector="matched"), maxit=12, lam=1e-2)
+    # unmatched pixel-driven back-projector (the reference's B != A^T setting)
+    dump("tomo24_pixel.npz", tomo_problem(24, 12, noise=1e-2, seed=1, backprojector="pixel"), maxit=12, lam=1e-2)
+    # C1 geometry (64^2, 90 angles): operator regenerated from the generator, pinned by hash
+    dump("tomo64_c1.npz", tomo_problem(64, 90, noise=1e-2, seed=0, backprojector="matched"), maxit=20, lam=1e-2,
+         store_raw=False)
