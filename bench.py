@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Benchmark: GMRES iterations/s + SpMV GB/s (% HBM roofline) on a synthetic 2-D phantom.
+
+Workload (BASELINE.json configs[1], the metric's single-GPU configuration):
+  hybrid_ab_gmres_rtp, fp64, 512x512 Shepp-Logan phantom, parallel-beam Siddon A
+  (30 angles, 725 detectors: m = 21,750 rays, n = 262,144 pixels, nnz = 1.0e7),
+  matched back-projector B = A', lambda = 1e-2, maxit = 20, tol = 0 (all 20
+  iterations run).  One "step" = one complete 20-iteration solve.  Inputs (A, B,
+  b, x_true) are resident in HBM before the timed region.
+
+Multi-GPU (torchrun, one process per GPU): weak scaling over independent
+slices — rank r reconstructs its own slice (same geometry, noise seed r); there
+is no data-path collective (the 512^2 operator is below the size where pixel
+sharding amortises its all-reduce, north_star; the RCCL-sharded operator path
+is `--workload c4 --shard`).  value = total GMRES iterations of all ranks / max
+rank time.
+
+Extra fields: "roofline" for the dominant SpMV kernel (algorithmic bytes per
+launch / average launch duration from HIP events recorded on the library's
+stream during the timed region), "kernels" (both SpMV classes and MGS),
+"cpu_baseline" (the oracle restatement timed on host cores, rank 0, N=1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "hybrid-gmres_amd"), ROOT]
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+WORKLOADS = {
+    "c2": dict(N=512, angles=30, solver="hybrid_ab_gmres_rtp", maxit=20, lam=1e-2),
+    "c3": dict(N=2048, angles=19, solver="hybrid_ba_gmres_rtp", maxit=20, lam=1e-2),
+    "c4": dict(N=4096, angles=47, solver="ABgmres_nonhybrid_bounds", maxit=20, lam=0.0),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--orth", default="mgs", choices=["mgs", "cgs2"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP-event timing")
+    ap.add_argument("--cpu-iters", type=int, default=0, help="oracle iterations for cpu_baseline (0 = maxit)")
+    return ap.parse_args()
+
+
+def build_problem(ctx, wl, seed):
+    """A generated on the device (bit-identical to hgmres.problems.siddon_projector),
+    B = A' by the device transpose, b = A x_true + noise."""
+    import hgmres
+    from hgmres.problems import shepp_logan
+    N, na = wl["N"], wl["angles"]
+    A = hgmres.SparseOperator.siddon(N, na, ctx=ctx)
+    B = A.T
+    x_true = shepp_logan(N).ravel(order="F")
+    b_exact = A @ x_true
+    rng = np.random.default_rng(seed)
+    e = rng.standard_normal(A.shape[0])
+    e = e / np.linalg.norm(e) * 1e-2 * np.linalg.norm(b_exact)
+    return A, B, b_exact + e, x_true
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    import ctypes as C
+    import hgmres
+    from hgmres import _lib as L
+    from hgmres.core import _check
+
+    wl = WORKLOADS[args.workload]
+    ctx = hgmres.Context(local)
+    A, B, b, x_true = build_problem(ctx, wl, seed=rank)
+    m, n = A.shape
+    dev = torch.device("cuda", local)
+    b_d = torch.from_numpy(b).to(dev)
+    xt_d = torch.from_numpy(x_true).to(dev)
+    x_d = torch.zeros(n, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    maxit, lam = wl["maxit"], wl["lam"]
+    err = np.zeros(maxit)
+    res = np.zeros(maxit)
+    it = C.c_int(0)
+    o = L.hgm_opts()
+    o.flags = L.HGM_DEVICE_PTRS
+    o.orth = L.HGM_CGS2 if args.orth == "cgs2" else L.HGM_MGS
+    o.H_out = None
+    lib = L.load()
+    dptr = lambda t: C.cast(C.c_void_p(t.data_ptr()), L.dp)   # noqa: E731
+    ep, rp = err.ctypes.data_as(L.dp), res.ctypes.data_as(L.dp)
+
+    def step():
+        if wl["solver"] == "hybrid_ab_gmres_rtp":
+            rc = lib.hgm_hybrid_ab_gmres_rtp_ex(ctx.handle, C.byref(o), A._h, B._h, dptr(b_d), dptr(xt_d), 0.0,
+                                                maxit, lam, dptr(x_d), ep, rp, C.byref(it))
+        elif wl["solver"] == "hybrid_ba_gmres_rtp":
+            rc = lib.hgm_hybrid_ba_gmres_rtp_ex(ctx.handle, C.byref(o), A._h, B._h, dptr(b_d), dptr(xt_d), 0.0,
+                                                maxit, lam, dptr(x_d), ep, rp, C.byref(it))
+        else:
+            rc = lib.hgm_gmres_bounds_ex(ctx.handle, C.byref(o), A._h, B._h, dptr(b_d), dptr(xt_d), 0.0, maxit,
+                                         lam, L.HGM_SIDE_AB, 0, dptr(x_d), ep, rp, C.byref(it))
+        _check(rc, ctx)
+        if it.value != maxit:
+            raise RuntimeError(f"solver stopped at {it.value} != {maxit}")
+
+    for _ in range(args.warmup):
+        step()
+    timing = not args.no_timing
+    ctx.kernel_timing(timing)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    dt = t1 - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    kern = {}
+    names = {0: "spmv_A_raymajor", 1: "spmv_B_pixelmajor", 2: "mgs_pass_sweep"}
+    if timing:
+        for cls, nm in names.items():
+            ms, calls, by = ctx.kernel_timing_read(cls)
+            if calls:
+                avg_s = ms / calls / 1e3
+                kern[nm] = {"calls": calls, "avg_us": avg_s * 1e6, "bytes_per_launch": by / calls,
+                            "GBps": by / calls / avg_s / 1e9, "total_ms": ms}
+        ctx.kernel_timing(False)
+    iters = args.steps * maxit * world
+    value = iters / dt
+    roof = None
+    spmv = {k: v for k, v in kern.items() if k.startswith("spmv")}
+    if spmv:
+        dom_name = max(spmv, key=lambda k: spmv[k]["total_ms"])
+        d = spmv[dom_name]
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
+        if os.path.exists(tf):
+            try:
+                traffic = json.load(open(tf)).get(dom_name)
+            except Exception:   # noqa: BLE001
+                traffic = None
+        roof = {"bound": "hbm", "kernel": dom_name, "achieved": round(d["GBps"], 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(d["GBps"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "bytes_per_launch": d["bytes_per_launch"], "avg_launch_us": round(d["avg_us"], 2)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(A, B, b, x_true, wl, args.cpu_iters)
+
+    if rank == 0:
+        line = {
+            "metric": "GMRES iters/sec + SpMV GB/s (% HBM roofline), 2-D phantom A, 1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "GMRES iters/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (Siddon parallel-beam A generated on device, Shepp-Logan phantom, 1% noise)",
+            "config": {
+                "workload": f"{args.workload}: {wl['solver']} {wl['N']}x{wl['N']} phantom, {wl['angles']} angles, "
+                            f"m={m}, n={n}, nnz(A)={A.nnz}, maxit={maxit}, tol=0, lambda={lam}, orth={args.orth}",
+                "global_batch": world,
+                "parallelism": "replicas: one independent slice per GPU" if world > 1 else "single GPU",
+                "step": f"one complete {maxit}-iteration solve",
+            },
+            "roofline": roof,
+            "kernels": kern,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(A, B, b, x_true, wl, iters):
+    """The oracle restatement (reference algorithm, scipy SpMV) on one host core."""
+    from oracle import restatement as R
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:   # pragma: no cover
+        threadpool_limits = None
+    As, Bs = A.to_scipy(), B.to_scipy()
+    maxit = iters or wl["maxit"]
+    fn = getattr(R, wl["solver"])
+    args = (As, Bs, b, x_true, 0.0, maxit) + ((wl["lam"],) if wl["solver"] != "ABgmres_nonhybrid_bounds" else ())
+    import contextlib
+    with (threadpool_limits(limits=1) if threadpool_limits else contextlib.nullcontext()):
+        t0 = time.perf_counter()
+        out = fn(*args)
+        dt = time.perf_counter() - t0
+    k = out[3]
+    return {"value": round(k / dt, 4), "unit": "GMRES iters/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/restatement.py {wl['solver']} on the same {wl['N']}^2 operator, {k} iterations "
+                      f"({dt:.1f} s, scipy CSR SpMV + numpy, 1 thread)"}
+
+
+if __name__ == "__main__":
+    main()

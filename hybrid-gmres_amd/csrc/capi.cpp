@@ -308,6 +308,7 @@ HGM_API int hgm_mat_create_csr(hgm_ctx* c, int64_t rows, int64_t cols, int64_t n
             }
         }
         HGM_HIP(hipStreamSynchronize(c->stream));
+        set_bands(c, M, auto_band_width(M));
     });
     *out = M;
     return HGM_OK;
@@ -336,14 +337,20 @@ HGM_API int hgm_mat_create_csc(hgm_ctx* c, int64_t rows, int64_t cols, int64_t n
 HGM_API int hgm_mat_transpose(hgm_ctx* c, const hgm_mat* in, hgm_mat** out) {
     if (!c || !in || !out) return HGM_E_ARG;
     *out = nullptr;
-    HGM_TRY(c, *out = transpose(c, in));
+    HGM_TRY(c, {
+        *out = transpose(c, in);
+        set_bands(c, *out, auto_band_width(*out));
+    });
     return HGM_OK;
 }
 
 HGM_API int hgm_mat_create_siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype, hgm_mat** out) {
     if (!c || !out) return HGM_E_ARG;
     *out = nullptr;
-    HGM_TRY(c, *out = siddon(c, N, n_angles, det_offset, dtype));
+    HGM_TRY(c, {
+        *out = siddon(c, N, n_angles, det_offset, dtype);
+        set_bands(c, *out, auto_band_width(*out));
+    });
     return HGM_OK;
 }
 
@@ -353,6 +360,25 @@ HGM_API int hgm_mat_info(const hgm_mat* M, int64_t* rows, int64_t* cols, int64_t
     if (cols) *cols = M->cols;
     if (nnz) *nnz = M->nnz;
     if (dtype) *dtype = M->dtype;
+    return HGM_OK;
+}
+
+HGM_API int hgm_mat_set_bands(hgm_ctx* c, hgm_mat* M, int64_t band_width, int group) {
+    if (!c || !M || band_width < -1) return HGM_E_ARG;
+    if (group != 0 && group != 4 && group != 8 && group != 16 && group != 32 && group != 64) return HGM_E_ARG;
+    HGM_TRY(c, {
+        HGM_HIP(hipSetDevice(c->device));
+        set_bands(c, M, band_width == -1 ? auto_band_width(M) : band_width);
+        if (group && M->nbands > 1) M->bgroup = group;
+    });
+    return HGM_OK;
+}
+
+HGM_API int hgm_mat_tune(hgm_mat* M, int variant, int group) {
+    if (!M || variant < 0 || variant > 7) return HGM_E_ARG;
+    if (group != 0 && group != 4 && group != 8 && group != 16 && group != 32 && group != 64) return HGM_E_ARG;
+    M->variant = variant;
+    if (group) M->group = group;
     return HGM_OK;
 }
 
@@ -377,7 +403,7 @@ HGM_API int hgm_mat_download(hgm_ctx* c, const hgm_mat* M, int64_t* row_ptr, int
 
 HGM_API void hgm_mat_destroy(hgm_mat* M) {
     if (!M) return;
-    if (M->ctx && M->ctx->stream) (void)hipStreamSynchronize(M->ctx->stream);
+    (void)hipDeviceSynchronize();   // hipFree below is device-synchronous anyway; never touch M->ctx here
     mat_free(M);
 }
 

@@ -89,8 +89,24 @@ struct hgm_mat {
     int32_t* ci = nullptr;   // nnz
     void* val = nullptr;     // nnz (double or float)
     int group = 64;          // lanes per row in the SpMV kernel
+    int variant = 0;         // SpmvVariant bits
     double fro = -1.0;       // cached ||M||_F (lsmr_solver.m:71 is loop-invariant)
+    // Column-banded copy (cache blocking of the x gather): the columns are
+    // cut into nbands contiguous bands of band_w pixels; segment (b, r) of row r that lies
+    // in band b is [brp[b*rows + r], brp[b*rows + r + 1]) of bci/bval (band-major order).
+    int64_t band_w = 0;
+    int nbands = 0;
+    int bgroup = 16;         // lanes per segment in the banded kernel
+    int64_t* brp = nullptr;
+    int32_t* bci = nullptr;
+    void* bval = nullptr;
 };
+
+namespace hgm {
+// SpMV kernel variants (bit flags): 16-byte paired loads, nontemporal val/col loads,
+// XCD-aware row-block order.
+enum SpmvVariant { SPMV_VEC = 1, SPMV_NT = 2, SPMV_XCD = 4 };
+}
 
 namespace hgm {
 
@@ -138,6 +154,9 @@ template <typename T> void fro2(hgm_ctx* c, const hgm_mat* M, double* out_dev);
 hgm_mat* mat_alloc(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, int dtype);
 void mat_free(hgm_mat* M);
 hgm_mat* transpose(hgm_ctx* c, const hgm_mat* M);
+// build / drop the column-banded copy (band_w <= 0 or >= cols drops it)
+void set_bands(hgm_ctx* c, hgm_mat* M, int64_t band_w);
+int64_t auto_band_width(const hgm_mat* M);
 hgm_mat* siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype);
 
 // ---------------- comm / scalars (capi.cpp) ----------------

@@ -51,7 +51,8 @@ __device__ __forceinline__ T reduce_parts(const T* __restrict__ p, int np, T* sh
 }
 
 int parts_for(int64_t n) {
-    int64_t nb = (n + 2 * BS * 8 - 1) / (2 * BS * 8);   // >= 8 element pairs per thread
+    // >= 2 element pairs per thread, up to MAX_PARTS blocks (256 CUs x 4)
+    int64_t nb = (n + 2 * BS * 2 - 1) / (2 * BS * 2);
     if (nb < 1) nb = 1;
     if (nb > MAX_PARTS) nb = MAX_PARTS;
     return (int)nb;
@@ -68,32 +69,134 @@ __device__ __forceinline__ T apply_epi(T t, T a, const T* __restrict__ z, int64_
     return t;
 }
 
-template <typename T, int G, int EPI>
+template <bool NT, typename V>
+__device__ __forceinline__ V ld(const V* p) {
+    if (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
+// native clang vectors (the nontemporal builtin does not take HIP_vector_type)
+typedef double nd2 __attribute__((ext_vector_type(2)));
+typedef float nf2 __attribute__((ext_vector_type(2)));
+typedef int ni2 __attribute__((ext_vector_type(2)));
+template <typename T> struct NV2;
+template <> struct NV2<double> { using t = nd2; };
+template <> struct NV2<float> { using t = nf2; };
+
+// XCD-aware block order (speed only, never correctness): consecutive logical row blocks
+// run on the same XCD so neighbouring rays share x lines in that XCD's L2
+// (cdna_hip_programming.md §5 "XCD swizzle must be bijective").
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+    const int64_t q = nb / 8, r = nb % 8, xcd = b % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
+
+// One G-lane group per CSR row.  VEC: each lane streams pairs of entries with 16-byte
+// value loads and 8-byte index loads (row heads/tails peeled to keep them aligned).
+// NT: nontemporal (streaming) loads for val/col so they do not evict x from L2/MALL.
+// Per-lane partial of the dot product of entries [s, e) with x, lane gl of a G-lane group.
+template <typename T, int G, bool VEC, bool NT>
+__device__ __forceinline__ T seg_partial(int64_t s, int64_t e, int gl, const int32_t* __restrict__ ci,
+                                         const T* __restrict__ val, const T* __restrict__ x) {
+    T a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    {
+        if (!VEC) {
+            int64_t i = s + gl;
+            for (; i + 3 * G < e; i += 4 * G) {
+                const int32_t c0 = ld<NT>(ci + i), c1 = ld<NT>(ci + i + G), c2 = ld<NT>(ci + i + 2 * G),
+                              c3 = ld<NT>(ci + i + 3 * G);
+                const T v0 = ld<NT>(val + i), v1 = ld<NT>(val + i + G), v2 = ld<NT>(val + i + 2 * G),
+                        v3 = ld<NT>(val + i + 3 * G);
+                a0 += v0 * x[c0];
+                a1 += v1 * x[c1];
+                a2 += v2 * x[c2];
+                a3 += v3 * x[c3];
+            }
+            for (; i < e; i += G) a0 += ld<NT>(val + i) * x[ld<NT>(ci + i)];
+        } else {
+            using T2 = typename NV2<T>::t;
+            using I2 = ni2;
+            const int64_t s2 = (s + 1) & ~int64_t(1);     // first even index >= s
+            const int64_t e2 = e & ~int64_t(1);           // last even bound <= e
+            if (gl == 0 && s < s2 && s < e) a0 += ld<NT>(val + s) * x[ld<NT>(ci + s)];
+            if (gl == G - 1 && e2 < e && e2 >= s2) a1 += ld<NT>(val + e2) * x[ld<NT>(ci + e2)];
+            int64_t i = s2 + 2 * gl;
+            for (; i + 2 * G < e2; i += 4 * G) {
+                const I2 c0 = ld<NT>(reinterpret_cast<const I2*>(ci + i));
+                const I2 c1 = ld<NT>(reinterpret_cast<const I2*>(ci + i + 2 * G));
+                const T2 v0 = ld<NT>(reinterpret_cast<const T2*>(val + i));
+                const T2 v1 = ld<NT>(reinterpret_cast<const T2*>(val + i + 2 * G));
+                a0 += v0.x * x[c0.x];
+                a1 += v0.y * x[c0.y];
+                a2 += v1.x * x[c1.x];
+                a3 += v1.y * x[c1.y];
+            }
+            for (; i < e2; i += 2 * G) {
+                const I2 c0 = ld<NT>(reinterpret_cast<const I2*>(ci + i));
+                const T2 v0 = ld<NT>(reinterpret_cast<const T2*>(val + i));
+                a0 += v0.x * x[c0.x];
+                a1 += v0.y * x[c0.y];
+            }
+        }
+    }
+    return (a0 + a1) + (a2 + a3);
+}
+
+template <typename T, int G>
+__device__ __forceinline__ T group_sum(T acc) {
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    return acc;
+}
+
+template <typename T, int G, int EPI, bool VEC, bool NT>
 __global__ __launch_bounds__(BS) void k_spmv(int64_t rows, const int64_t* __restrict__ rp,
                                              const int32_t* __restrict__ ci,
                                              const T* __restrict__ val, const T* __restrict__ x,
-                                             T* __restrict__ y, T a, const T* __restrict__ z) {
+                                             T* __restrict__ y, T a, const T* __restrict__ z, int xcd) {
     constexpr int RPB = BS / G;
-    const int64_t row = (int64_t)blockIdx.x * RPB + threadIdx.x / G;
+    const int64_t blk = xcd ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t row = blk * RPB + threadIdx.x / G;
     const int gl = threadIdx.x & (G - 1);
-    T a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    if (row < rows) {
-        const int64_t s = rp[row], e = rp[row + 1];
-        int64_t i = s + gl;
-        for (; i + 3 * G < e; i += 4 * G) {
-            const int32_t c0 = ci[i], c1 = ci[i + G], c2 = ci[i + 2 * G], c3 = ci[i + 3 * G];
-            const T v0 = val[i], v1 = val[i + G], v2 = val[i + 2 * G], v3 = val[i + 3 * G];
-            a0 += v0 * x[c0];
-            a1 += v1 * x[c1];
-            a2 += v2 * x[c2];
-            a3 += v3 * x[c3];
-        }
-        for (; i < e; i += G) a0 += val[i] * x[ci[i]];
-    }
-    T acc = (a0 + a1) + (a2 + a3);
-#pragma unroll
-    for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    T acc = 0;
+    if (row < rows) acc = seg_partial<T, G, VEC, NT>(rp[row], rp[row + 1], gl, ci, val, x);
+    acc = group_sum<T, G>(acc);
     if (gl == 0 && row < rows) y[row] = apply_epi<T, EPI>(acc, a, z, row);
+}
+
+// Column-banded SpMV: work items (band b, block of RPB rows) in band-major order, grid-
+// stride, so the blocks resident at any moment gather x from one band's slice (L2-
+// resident).  Writes the per-band partial ypart[b*rows + r]; k_band_reduce sums them.
+template <typename T, int G, bool VEC, bool NT>
+__global__ __launch_bounds__(BS) void k_spmv_band(int64_t rows, int nbands, const int64_t* __restrict__ brp,
+                                                  const int32_t* __restrict__ ci, const T* __restrict__ val,
+                                                  const T* __restrict__ x, T* __restrict__ ypart) {
+    constexpr int RPB = BS / G;
+    const int64_t rb_per_band = (rows + RPB - 1) / RPB;
+    const int64_t items = rb_per_band * nbands;
+    const int gl = threadIdx.x & (G - 1);
+    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const int64_t b = it / rb_per_band;
+        const int64_t row = (it - b * rb_per_band) * RPB + threadIdx.x / G;
+        T acc = 0;
+        if (row < rows) {
+            const int64_t* p = brp + b * rows + row;
+            acc = seg_partial<T, G, VEC, NT>(p[0], p[1], gl, ci, val, x);
+        }
+        acc = group_sum<T, G>(acc);
+        if (gl == 0 && row < rows) ypart[b * rows + row] = acc;
+    }
+}
+
+// y[r] = epi( sum_b ypart[b*rows + r] ), bands summed in increasing b (deterministic)
+template <typename T, int EPI>
+__global__ __launch_bounds__(BS) void k_band_reduce(int64_t rows, int nbands, const T* __restrict__ ypart,
+                                                    T* __restrict__ y, T a, const T* __restrict__ z) {
+    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BS) {
+        T s = 0;
+        for (int b = 0; b < nbands; ++b) s += ypart[(int64_t)b * rows + r];
+        y[r] = apply_epi<T, EPI>(s, a, z, r);
+    }
 }
 
 int pick_group(int64_t rows, int64_t nnz) {
@@ -105,17 +208,67 @@ int pick_group(int64_t rows, int64_t nnz) {
     return 4;
 }
 
-template <typename T, int G>
-static void launch_spmv_g(hipStream_t st, const hgm_mat* M, const T* x, T* y, int epi, T a,
-                          const T* z) {
+template <typename T, int G, bool VEC, bool NT>
+static void launch_spmv_v(hipStream_t st, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
     const int64_t nb = (M->rows + (BS / G) - 1) / (BS / G);
     if (nb == 0) return;
     const T* val = reinterpret_cast<const T*>(M->val);
+    const int xcd = (M->variant & SPMV_XCD) ? 1 : 0;
     switch (epi) {
-        case EPI_NONE: k_spmv<T, G, EPI_NONE><<<nb, BS, 0, st>>>(M->rows, M->rp, M->ci, val, x, y, a, z); break;
-        case EPI_ADD: k_spmv<T, G, EPI_ADD><<<nb, BS, 0, st>>>(M->rows, M->rp, M->ci, val, x, y, a, z); break;
-        case EPI_SUB: k_spmv<T, G, EPI_SUB><<<nb, BS, 0, st>>>(M->rows, M->rp, M->ci, val, x, y, a, z); break;
-        default: k_spmv<T, G, EPI_RSUB><<<nb, BS, 0, st>>>(M->rows, M->rp, M->ci, val, x, y, a, z); break;
+        case EPI_NONE: k_spmv<T, G, EPI_NONE, VEC, NT><<<nb, BS, 0, st>>>(M->rows, M->rp, M->ci, val, x, y, a, z, xcd); break;
+        case EPI_ADD: k_spmv<T, G, EPI_ADD, VEC, NT><<<nb, BS, 0, st>>>(M->rows, M->rp, M->ci, val, x, y, a, z, xcd); break;
+        case EPI_SUB: k_spmv<T, G, EPI_SUB, VEC, NT><<<nb, BS, 0, st>>>(M->rows, M->rp, M->ci, val, x, y, a, z, xcd); break;
+        default: k_spmv<T, G, EPI_RSUB, VEC, NT><<<nb, BS, 0, st>>>(M->rows, M->rp, M->ci, val, x, y, a, z, xcd); break;
+    }
+}
+
+template <typename T, int G>
+static void launch_spmv_g(hipStream_t st, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
+    const bool vec = M->variant & SPMV_VEC, nt = M->variant & SPMV_NT;
+    if (vec && nt) launch_spmv_v<T, G, true, true>(st, M, x, y, epi, a, z);
+    else if (vec) launch_spmv_v<T, G, true, false>(st, M, x, y, epi, a, z);
+    else if (nt) launch_spmv_v<T, G, false, true>(st, M, x, y, epi, a, z);
+    else launch_spmv_v<T, G, false, false>(st, M, x, y, epi, a, z);
+}
+
+template <typename T, int G, bool VEC, bool NT>
+static void launch_band_v(hipStream_t st, const hgm_mat* M, const T* x, T* yp) {
+    constexpr int RPB = BS / G;
+    const int64_t items = (M->rows + RPB - 1) / RPB * M->nbands;
+    int64_t grid = 256 * 8;                      // ~all resident blocks, grid-stride in band-major order
+    if (grid > items) grid = items;
+    if (grid < 1) return;
+    k_spmv_band<T, G, VEC, NT><<<grid, BS, 0, st>>>(M->rows, M->nbands, M->brp, M->bci,
+                                                    reinterpret_cast<const T*>(M->bval), x, yp);
+}
+
+template <typename T, int G>
+static void launch_band_g(hipStream_t st, const hgm_mat* M, const T* x, T* yp) {
+    const bool vec = M->variant & SPMV_VEC, nt = M->variant & SPMV_NT;
+    if (vec && nt) launch_band_v<T, G, true, true>(st, M, x, yp);
+    else if (vec) launch_band_v<T, G, true, false>(st, M, x, yp);
+    else if (nt) launch_band_v<T, G, false, true>(st, M, x, yp);
+    else launch_band_v<T, G, false, false>(st, M, x, yp);
+}
+
+template <typename T>
+static void spmv_banded(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
+    T* yp = c->buf<T>("band_part", (size_t)M->nbands * M->rows + 1);
+    switch (M->bgroup) {
+        case 64: launch_band_g<T, 64>(c->stream, M, x, yp); break;
+        case 32: launch_band_g<T, 32>(c->stream, M, x, yp); break;
+        case 16: launch_band_g<T, 16>(c->stream, M, x, yp); break;
+        case 8: launch_band_g<T, 8>(c->stream, M, x, yp); break;
+        default: launch_band_g<T, 4>(c->stream, M, x, yp); break;
+    }
+    int64_t g = (M->rows + BS - 1) / BS;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    switch (epi) {
+        case EPI_NONE: k_band_reduce<T, EPI_NONE><<<g, BS, 0, c->stream>>>(M->rows, M->nbands, yp, y, a, z); break;
+        case EPI_ADD: k_band_reduce<T, EPI_ADD><<<g, BS, 0, c->stream>>>(M->rows, M->nbands, yp, y, a, z); break;
+        case EPI_SUB: k_band_reduce<T, EPI_SUB><<<g, BS, 0, c->stream>>>(M->rows, M->nbands, yp, y, a, z); break;
+        default: k_band_reduce<T, EPI_RSUB><<<g, BS, 0, c->stream>>>(M->rows, M->nbands, yp, y, a, z); break;
     }
 }
 
@@ -123,6 +276,15 @@ template <typename T>
 void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, int kclass) {
     hipEvent_t t0 = nullptr;
     timing_begin(c, kclass, &t0);
+    if (M->nbands > 1) {
+        spmv_banded<T>(c, M, x, y, epi, a, z);
+        HGM_HIP(hipGetLastError());
+        const double s = sizeof(T);
+        double bytes = (double)M->nnz * (s + 4) + 8.0 * (M->rows + 1) + s * M->cols + s * M->rows;
+        if (epi != EPI_NONE) bytes += s * M->rows;
+        timing_end(c, kclass, t0, bytes);
+        return;
+    }
     switch (M->group) {
         case 64: launch_spmv_g<T, 64>(c->stream, M, x, y, epi, a, z); break;
         case 32: launch_spmv_g<T, 32>(c->stream, M, x, y, epi, a, z); break;

@@ -6,6 +6,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
+#include <cstdlib>
 
 #include "internal.h"
 
@@ -26,15 +27,113 @@ hgm_mat* mat_alloc(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, int dtyp
         throw Error{HGM_E_NOMEM, "hipMalloc failed for sparse matrix"};
     }
     M->group = pick_group(rows, nnz);
+    M->variant = SPMV_VEC;
+    // tuning overrides (benchmarks only): HGM_SPMV_VARIANT=<bits>, HGM_SPMV_GROUP=<lanes>
+    if (const char* v = std::getenv("HGM_SPMV_VARIANT")) M->variant = std::atoi(v);
+    if (const char* g = std::getenv("HGM_SPMV_GROUP")) {
+        const int gg = std::atoi(g);
+        if (gg == 4 || gg == 8 || gg == 16 || gg == 32 || gg == 64) M->group = gg;
+    }
     return M;
+}
+
+static int grid_cap(int64_t n);
+
+static void free_bands(hgm_mat* M) {
+    if (M->brp) (void)hipFree(M->brp);
+    if (M->bci) (void)hipFree(M->bci);
+    if (M->bval) (void)hipFree(M->bval);
+    M->brp = nullptr;
+    M->bci = nullptr;
+    M->bval = nullptr;
+    M->nbands = 0;
+    M->band_w = 0;
 }
 
 void mat_free(hgm_mat* M) {
     if (!M) return;
+    free_bands(M);
     if (M->rp) (void)hipFree(M->rp);
     if (M->ci) (void)hipFree(M->ci);
     if (M->val) (void)hipFree(M->val);
     delete M;
+}
+
+// --------------------------------------------------------------------------
+// column bands (cache blocking of the x gather for long-row operators)
+// --------------------------------------------------------------------------
+// one thread per row, sequential over the row (each row is owned by one thread: no races)
+__global__ void k_band_count(int64_t rows, int64_t W, const int64_t* __restrict__ rp,
+                             const int32_t* __restrict__ ci, int64_t* __restrict__ cnt) {
+    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BS)
+        for (int64_t i = rp[r]; i < rp[r + 1]; ++i) cnt[(int64_t)(ci[i] / W) * rows + r] += 1;
+}
+
+template <typename T>
+__global__ void k_band_fill(int64_t rows, int64_t W, const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                            const T* __restrict__ val, int64_t* __restrict__ cur, int32_t* __restrict__ bci,
+                            T* __restrict__ bval) {
+    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BS)
+        for (int64_t i = rp[r]; i < rp[r + 1]; ++i) {
+            const int64_t p = cur[(int64_t)(ci[i] / W) * rows + r]++;
+            bci[p] = ci[i];
+            bval[p] = val[i];
+        }
+}
+
+int64_t auto_band_width(const hgm_mat* M) {
+    const size_t vs = M->dtype == HGM_F32 ? 4 : 8;
+    if (const char* e = std::getenv("HGM_BAND_WIDTH")) return std::atoll(e);
+    // x fits comfortably in one XCD's 4 MiB L2: no banding
+    if ((double)M->cols * vs <= 4.0 * 1024 * 1024) return 0;
+    // only long-row operators benefit (the short pixel-major rows of B gather an L2-resident y)
+    if (M->rows > 0 && (double)M->nnz / (double)M->rows < 64) return 0;
+    return (int64_t)(1 << 18);   // 256 Ki pixels = 2 MiB fp64 x-slice per band
+}
+
+void set_bands(hgm_ctx* c, hgm_mat* M, int64_t W) {
+    free_bands(M);
+    if (W <= 0 || W >= M->cols || M->nnz == 0) return;
+    const int64_t nb = (M->cols + W - 1) / W;
+    HGM_REQUIRE(nb * M->rows + 1 < (int64_t)INT32_MAX, "set_bands: too many (band,row) segments");
+    hipStream_t st = c->stream;
+    const size_t vs = M->dtype == HGM_F32 ? 4 : 8;
+    const int64_t nseg = nb * M->rows;
+    int64_t* cnt = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    try {
+        HGM_HIP(hipMalloc(&M->brp, sizeof(int64_t) * (nseg + 1)));
+        HGM_HIP(hipMalloc(&M->bci, sizeof(int32_t) * M->nnz));
+        HGM_HIP(hipMalloc(&M->bval, vs * M->nnz));
+        HGM_HIP(hipMalloc(&cnt, sizeof(int64_t) * (nseg + 1)));
+        HGM_HIP(hipMemsetAsync(cnt, 0, sizeof(int64_t) * (nseg + 1), st));
+        const int g = grid_cap(M->rows);
+        k_band_count<<<g, BS, 0, st>>>(M->rows, W, M->rp, M->ci, cnt);
+        HGM_HIP(hipGetLastError());
+        HGM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, M->brp, (int)(nseg + 1), st));
+        HGM_HIP(hipMalloc(&tmp, tmp_bytes));
+        HGM_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, M->brp, (int)(nseg + 1), st));
+        HGM_HIP(hipMemcpyAsync(cnt, M->brp, sizeof(int64_t) * (nseg + 1), hipMemcpyDeviceToDevice, st));
+        if (M->dtype == HGM_F32)
+            k_band_fill<float><<<g, BS, 0, st>>>(M->rows, W, M->rp, M->ci, (const float*)M->val, cnt, M->bci, (float*)M->bval);
+        else
+            k_band_fill<double><<<g, BS, 0, st>>>(M->rows, W, M->rp, M->ci, (const double*)M->val, cnt, M->bci, (double*)M->bval);
+        HGM_HIP(hipGetLastError());
+        HGM_HIP(hipStreamSynchronize(st));
+    } catch (...) {
+        (void)hipFree(cnt);
+        (void)hipFree(tmp);
+        free_bands(M);
+        throw;
+    }
+    (void)hipFree(cnt);
+    (void)hipFree(tmp);
+    M->band_w = W;
+    M->nbands = (int)nb;
+    const double avg = (double)M->nnz / (double)nseg;
+    M->bgroup = avg >= 96 ? 32 : (avg >= 24 ? 16 : 8);
+    if (const char* g = std::getenv("HGM_BAND_GROUP")) M->bgroup = std::atoi(g);
 }
 
 // --------------------------------------------------------------------------

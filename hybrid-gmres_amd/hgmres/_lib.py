@@ -55,6 +55,8 @@ _SIGS = {
     "hgm_mat_transpose": (c_int, [c_void_p, c_void_p, P(c_void_p)]),
     "hgm_mat_create_siddon": (c_int, [c_void_p, c_int, c_int, c_double, c_int, P(c_void_p)]),
     "hgm_mat_info": (c_int, [c_void_p, ip64, ip64, ip64, P(c_int)]),
+    "hgm_mat_tune": (c_int, [c_void_p, c_int, c_int]),
+    "hgm_mat_set_bands": (c_int, [c_void_p, c_void_p, c_int64, c_int]),
     "hgm_mat_download": (c_int, [c_void_p, c_void_p, ip64, ip32, dp]),
     "hgm_mat_destroy": (None, [c_void_p]),
     "hgm_spmv": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),

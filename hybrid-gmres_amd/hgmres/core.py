@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 import threading
 
 import numpy as np
@@ -118,6 +119,8 @@ class Context:
             self._h = None
 
     def __del__(self):
+        if sys.is_finalizing():       # HIP runtime may already be torn down at exit
+            return
         try:
             self.close()
         except Exception:   # noqa: BLE001
@@ -215,6 +218,15 @@ class SparseOperator:
         M.has_sorted_indices = False
         return M
 
+    def tune(self, variant: int, group: int = 0):
+        """Select the SpMV kernel variant (bits: 1 paired 16-B loads, 2 nontemporal,
+        4 XCD-aware order) and lanes per row."""
+        _check(L.load().hgm_mat_tune(self._h, int(variant), int(group)), self.ctx)
+
+    def set_bands(self, band_width: int, group: int = 0):
+        """Column banding of the x gather (0 = off, -1 = automatic)."""
+        _check(L.load().hgm_mat_set_bands(self.ctx.handle, self._h, int(band_width), int(group)), self.ctx)
+
     def matvec_device(self, x_ptr: int, y_ptr: int):
         _check(L.load().hgm_spmv(self.ctx.handle, self._h, C.c_void_p(x_ptr), C.c_void_p(y_ptr)), self.ctx)
 
@@ -239,11 +251,16 @@ class SparseOperator:
         return y.astype(np.float64)
 
     def close(self):
+        if self._T is not None and self._T is not self:
+            T, self._T = self._T, None
+            T._T = None
         if self._h:
             L.load().hgm_mat_destroy(self._h)
             self._h = None
 
     def __del__(self):
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:   # noqa: BLE001

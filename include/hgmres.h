@@ -116,6 +116,15 @@ HGM_API int hgm_mat_transpose(hgm_ctx* ctx, const hgm_mat* in, hgm_mat** out);
 HGM_API int hgm_mat_create_siddon(hgm_ctx* ctx, int N, int n_angles, double det_offset,
                                   int dtype, hgm_mat** out);
 HGM_API int hgm_mat_info(const hgm_mat* mat, int64_t* rows, int64_t* cols, int64_t* nnz, int* dtype);
+/* SpMV kernel selection for this operator (tuning/benchmark hook): variant bits
+ * 1 = 16-byte paired loads, 2 = nontemporal val/col loads, 4 = XCD-aware row-block
+ * order; group = lanes per row (4, 8, 16, 32 or 64; 0 keeps the current choice). */
+HGM_API int hgm_mat_tune(hgm_mat* mat, int variant, int group);
+/* Column banding of the SpMV x-gather (cache blocking): band_width pixels per band
+ * (0 = off, -1 = automatic: on for long-row operators whose x exceeds one XCD's L2),
+ * group = lanes per (band,row) segment (0 = automatic).  Operators are created with
+ * the automatic choice. */
+HGM_API int hgm_mat_set_bands(hgm_ctx* ctx, hgm_mat* mat, int64_t band_width, int group);
 HGM_API int hgm_mat_download(hgm_ctx* ctx, const hgm_mat* mat, int64_t* row_ptr, int32_t* col_idx, double* val);
 HGM_API void hgm_mat_destroy(hgm_mat* mat);
 

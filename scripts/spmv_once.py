@@ -1,0 +1,55 @@
+"""Run a few SpMV launches per (operator, variant, group) — the target of rocprofv3
+PMC passes (FETCH_SIZE / WRITE_SIZE / TCC_HIT / TCC_MISS) in scripts/profile_spmv.sh.
+Prints the launch order so counter rows can be matched to cases.
+usage: python scripts/spmv_once.py CFG [A:v:g ...] [--reps 3]
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "hybrid-gmres_amd"), ROOT]
+
+import hgmres  # noqa: E402
+from hgmres import _lib as L  # noqa: E402
+from hgmres.problems import CONFIGS  # noqa: E402
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    reps = 3
+    if "--reps" in sys.argv:
+        reps = int(sys.argv[sys.argv.index("--reps") + 1])
+        args = [a for a in args if a != str(reps)]
+    cfg, cases = args[0], args[1:] or ["A:1:32", "B:1:8"]
+    lib = L.load()
+    ctx = hgmres.Context(0)
+    N, na = CONFIGS[cfg]
+    A = hgmres.SparseOperator.siddon(N, na, ctx=ctx)
+    B = A.T
+    ops = {"A": A, "B": B}
+    bufs = {}
+    for nm, M in ops.items():
+        rows, cols = M.shape
+        xd, yd = C.c_void_p(), C.c_void_p()
+        lib.hgm_dev_alloc(ctx.handle, 8 * cols, C.byref(xd))
+        lib.hgm_dev_alloc(ctx.handle, 8 * rows, C.byref(yd))
+        ones = np.ones(cols)
+        lib.hgm_memcpy_h2d(ctx.handle, xd, ones.ctypes.data_as(C.c_void_p), 8 * cols)
+        bufs[nm] = (xd, yd)
+    for case in cases:
+        nm, v, g = case.split(":")
+        M = ops[nm]
+        M.tune(int(v), int(g))
+        xd, yd = bufs[nm]
+        for _ in range(reps):
+            lib.hgm_spmv(ctx.handle, M._h, xd, yd)
+        ctx.synchronize()
+        print(f"case {cfg} {case} rows={M.shape[0]} cols={M.shape[1]} nnz={M.nnz} launches={reps}", flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

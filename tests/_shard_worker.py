@@ -1,0 +1,69 @@
+"""Worker for test_gpu_parity.py::test_shard_emulation_two_ranks.
+
+Runs the pixel-sharded solvers as ``world`` processes on ONE device with the
+cross-rank sums routed through the library's host all-reduce hook (a fixed-order
+two-party sum over a local socket), i.e. the same C++ code path as RCCL mode
+with a different transport.  usage: _shard_worker.py RANK WORLD PORT OUTDIR
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "hybrid-gmres_amd"), ROOT]
+
+import hgmres  # noqa: E402
+from hgmres.dist import plan_pixel_shards, shard_operators  # noqa: E402
+from hgmres.problems import tomo_problem  # noqa: E402
+
+
+def main():
+    rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    P = tomo_problem(64, 90, noise=1e-2, seed=0)
+    ctx = hgmres.Context(0)
+    conn = None
+    if world > 1:
+        from multiprocessing.connection import Client, Listener
+        if rank == 0:
+            lst = Listener(("127.0.0.1", port), authkey=b"hgm")
+            conn = lst.accept()
+        else:
+            for _ in range(600):
+                try:
+                    conn = Client(("127.0.0.1", port), authkey=b"hgm")
+                    break
+                except (ConnectionRefusedError, OSError):
+                    time.sleep(0.1)
+            assert conn is not None
+
+        def allreduce(arr):
+            if rank == 0:
+                other = conn.recv()
+                s = arr + other          # fixed order: rank 0 + rank 1
+                conn.send(s)
+                arr[:] = s
+            else:
+                conn.send(arr.copy())
+                arr[:] = conn.recv()
+
+        ctx.set_host_allreduce(rank, world, allreduce)
+    lo, hi = plan_pixel_shards(P.A, world, P.B)[rank]
+    A_g, B_g = shard_operators(P.A, P.B, lo, hi)
+    xt = P.x_true[lo:hi]
+    res = {}
+    x, e, r, k, H = hgmres.hybrid_ba_gmres_rtp(A_g, B_g, P.b, xt, 0.0, 15, 1e-2, ctx=ctx, return_H=True)
+    res.update(hba_x=x, hba_res=r, hba_err=e, hba_H=H)
+    x, e, r, k = hgmres.lsqr_solver(A_g, P.b, xt, 0.0, 10, ctx=ctx, At=B_g)
+    res.update(lsqr_x=x, lsqr_res=r, lsqr_err=e)
+    out_ = hgmres.ABgmres_hybrid_bounds(A_g, B_g, P.b, xt, 0.0, 12, 1e-2, ctx=ctx)
+    res.update(abp_x=out_[0], abp_res=out_[2], abp_err=out_[1])
+    np.savez(os.path.join(out, f"rank{rank}_of{world}.npz"), lo=lo, hi=hi, **res)
+    if conn is not None:
+        conn.close()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
