@@ -119,6 +119,19 @@ void h2d(hgm_ctx* c, void* dev, const void* host, size_t bytes) {
     HGM_HIP(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, c->stream));
 }
 
+void h2d_pinned(hgm_ctx* c, void* dev, const void* host, size_t bytes) {
+    if (bytes == 0) return;
+    if (bytes > c->hup_bytes) {
+        if (c->hup) (void)hipHostFree(c->hup);
+        c->hup = nullptr;
+        const size_t nb = bytes < 4096 ? 4096 : bytes;
+        HGM_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->hup), nb, hipHostMallocDefault));
+        c->hup_bytes = nb;
+    }
+    std::memcpy(c->hup, host, bytes);
+    HGM_HIP(hipMemcpyAsync(dev, c->hup, bytes, hipMemcpyHostToDevice, c->stream));
+}
+
 void read_scalars(hgm_ctx* c, int first, int count) {
     HGM_HIP(hipMemcpyAsync(c->hscal + first, c->dscal + first, sizeof(double) * count, hipMemcpyDeviceToHost,
                            c->stream));
@@ -260,6 +273,7 @@ HGM_API void hgm_ctx_destroy(hgm_ctx* c) {
     if (c->dscal) (void)hipFree(c->dscal);
     if (c->hscal) (void)hipHostFree(c->hscal);
     if (c->hstage) (void)hipHostFree(c->hstage);
+    if (c->hup) (void)hipHostFree(c->hup);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -308,7 +322,7 @@ HGM_API int hgm_mat_create_csr(hgm_ctx* c, int64_t rows, int64_t cols, int64_t n
             }
         }
         HGM_HIP(hipStreamSynchronize(c->stream));
-        set_bands(c, M, auto_band_width(M));
+        finalize_operator(c, M);
     });
     *out = M;
     return HGM_OK;
@@ -339,7 +353,7 @@ HGM_API int hgm_mat_transpose(hgm_ctx* c, const hgm_mat* in, hgm_mat** out) {
     *out = nullptr;
     HGM_TRY(c, {
         *out = transpose(c, in);
-        set_bands(c, *out, auto_band_width(*out));
+        finalize_operator(c, *out);
     });
     return HGM_OK;
 }
@@ -349,7 +363,7 @@ HGM_API int hgm_mat_create_siddon(hgm_ctx* c, int N, int n_angles, double det_of
     *out = nullptr;
     HGM_TRY(c, {
         *out = siddon(c, N, n_angles, det_offset, dtype);
-        set_bands(c, *out, auto_band_width(*out));
+        finalize_operator(c, *out);
     });
     return HGM_OK;
 }
@@ -375,10 +389,11 @@ HGM_API int hgm_mat_set_bands(hgm_ctx* c, hgm_mat* M, int64_t band_width, int gr
 }
 
 HGM_API int hgm_mat_tune(hgm_mat* M, int variant, int group) {
-    if (!M || variant < 0 || variant > 7) return HGM_E_ARG;
+    if (!M || variant < 0 || variant > 15) return HGM_E_ARG;
     if (group != 0 && group != 4 && group != 8 && group != 16 && group != 32 && group != 64) return HGM_E_ARG;
     M->variant = variant;
-    if (group) M->group = group;
+    if (group && (variant & SPMV_STREAM)) M->sgroup = M->bsgroup = group;   // lanes per segment reduction
+    else if (group) M->group = group;
     return HGM_OK;
 }
 

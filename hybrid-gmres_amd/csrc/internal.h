@@ -71,6 +71,8 @@ struct hgm_ctx {
     double* hscal = nullptr;                  // pinned host mirror
     double* hstage = nullptr;                 // pinned host staging (allreduce / small copies)
     size_t hstage_bytes = 0;
+    double* hup = nullptr;                    // pinned upload buffer (projected-solve y)
+    size_t hup_bytes = 0;
     hgm::Timing timing;
 
     template <typename T>
@@ -100,12 +102,24 @@ struct hgm_mat {
     int64_t* brp = nullptr;
     int32_t* bci = nullptr;
     void* bval = nullptr;
+    // chunk -> first segment starting in it, for the nnz-balanced streaming kernel
+    int32_t* cfo = nullptr;      // rows as segments (nchunks+1)
+    int32_t* bcfo = nullptr;     // (band,row) segments
+    int sgroup = 8, bsgroup = 16;  // lanes per segment in the streaming reduction
 };
 
 namespace hgm {
 // SpMV kernel variants (bit flags): 16-byte paired loads, nontemporal val/col loads,
-// XCD-aware row-block order.
-enum SpmvVariant { SPMV_VEC = 1, SPMV_NT = 2, SPMV_XCD = 4 };
+// XCD-aware row-block order, nnz-balanced streaming (chunked) kernel.
+enum SpmvVariant { SPMV_VEC = 1, SPMV_NT = 2, SPMV_XCD = 4, SPMV_STREAM = 8 };
+constexpr int SCH = 2048;   // entries per streaming chunk (256 threads x 8)
+
+struct SegIndex {
+    int64_t nnz, nseg, nchunks;
+    const int64_t* sp;       // nseg+1 segment pointers
+    const int32_t* fo;       // nchunks+1
+};
+inline int64_t stream_chunks(int64_t nnz) { return (nnz + SCH - 1) / SCH; }
 }
 
 namespace hgm {
@@ -127,7 +141,11 @@ template <typename T> void sumsq(hgm_ctx* c, int64_t n, const T* a, T* out_dev);
 template <typename T> void sumsq_diff(hgm_ctx* c, int64_t n, const T* a, const T* b, T* out_dev);
 // out[j] = Q(:,j)' * w, j < ncols (local)
 template <typename T>
-void multidot(hgm_ctx* c, int64_t n, int ncols, const T* Q, int64_t ldq, const T* w, T* out_dev);
+void multidot(hgm_ctx* c, int64_t n, int ncols, const T* Q, int64_t ldq, const T* w, T* out_dev,
+              const T* extra = nullptr);   // out[ncols] = extra' * w when extra != nullptr
+// x = Q(:,0:k) y fused with *err_out = ||x - xt||^2 (local)
+template <typename T>
+void gemv_err(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T* x, const T* xt, T* err_out);
 
 // MGS sweep of v = Q(:,kk+1) against Q(:,0..kk); writes Hcol[0..kk+1] (device) and
 // normalises Q(:,kk+1) unless H(kk+1,kk) == 0.  dist: n-vectors sharded (scalar all-reduce
@@ -156,6 +174,10 @@ void mat_free(hgm_mat* M);
 hgm_mat* transpose(hgm_ctx* c, const hgm_mat* M);
 // build / drop the column-banded copy (band_w <= 0 or >= cols drops it)
 void set_bands(hgm_ctx* c, hgm_mat* M, int64_t band_w);
+// chunk index of the nnz-balanced streaming kernel over the rows
+void build_stream_index(hgm_ctx* c, hgm_mat* M);
+// everything a freshly created operator gets: automatic bands + streaming index
+void finalize_operator(hgm_ctx* c, hgm_mat* M);
 int64_t auto_band_width(const hgm_mat* M);
 hgm_mat* siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype);
 
@@ -172,6 +194,9 @@ struct Reader {
     void go();
 };
 void h2d(hgm_ctx* c, void* dev, const void* host, size_t bytes);
+// small upload through a pinned buffer (truly asynchronous); the caller must not issue
+// another h2d_pinned before the stream has passed the previous one (one per iteration)
+void h2d_pinned(hgm_ctx* c, void* dev, const void* host, size_t bytes);
 void read_scalars(hgm_ctx* c, int first, int count);   // dscal -> hscal (sync)
 void sync(hgm_ctx* c);
 void timing_begin(hgm_ctx* c, int cls, hipEvent_t* start);

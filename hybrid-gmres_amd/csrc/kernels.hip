@@ -188,6 +188,140 @@ __global__ __launch_bounds__(BS) void k_spmv_band(int64_t rows, int nbands, cons
     }
 }
 
+// ------------------------------------------------------------------------------
+// nnz-balanced streaming SpMV over segments (rows, or (band,row) pairs).
+// Block k owns entries [k*CH, (k+1)*CH): it streams them with 16-byte loads, stages the
+// products in LDS, then G-lane groups reduce every segment that STARTS in the chunk
+// (fo[k] .. fo[k+1]) plus the head part of the segment that started earlier.  Complete
+// segments are written (with the epilogue); a segment running past the chunk leaves its
+// partial in tail[k] and every later chunk's share in head[j]; k_stream_fixup adds them
+// in chunk order.  Fixed chunking => fixed summation order => bitwise reproducible.
+// ------------------------------------------------------------------------------
+template <typename T, int G, int EPI, bool NT>
+__global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, const int64_t* __restrict__ sp,
+                                                    const int32_t* __restrict__ fo, const int32_t* __restrict__ ci,
+                                                    const T* __restrict__ val, const T* __restrict__ x,
+                                                    T* __restrict__ out, T a, const T* __restrict__ z,
+                                                    T* __restrict__ head, T* __restrict__ tail) {
+    using T2 = typename NV2<T>::t;
+    __shared__ T prod[SCH];
+    const int64_t k = blockIdx.x;
+    const int64_t c0 = k * SCH;
+    const int64_t c1 = (c0 + SCH < nnz) ? c0 + SCH : nnz;
+    const int n = (int)(c1 - c0);
+    if (n == SCH) {
+#pragma unroll
+        for (int u = 0; u < SCH / (2 * BS); ++u) {
+            const int j = 2 * threadIdx.x + u * 2 * BS;
+            const T2 v = ld<NT>(reinterpret_cast<const T2*>(val + c0 + j));
+            const ni2 cc = ld<NT>(reinterpret_cast<const ni2*>(ci + c0 + j));
+            prod[j] = v.x * x[cc.x];
+            prod[j + 1] = v.y * x[cc.y];
+        }
+    } else {
+        for (int j = threadIdx.x; j < n; j += BS) prod[j] = val[c0 + j] * x[ci[c0 + j]];
+    }
+    __syncthreads();
+    const int64_t s_begin = fo[k], s_end = fo[k + 1];
+    const int has_head = (s_begin > 0 && sp[s_begin] > c0) ? 1 : 0;
+    const int64_t ntasks = (s_end - s_begin) + has_head;
+    const int gid = threadIdx.x / G, gl = threadIdx.x & (G - 1);
+    constexpr int NG = BS / G;
+    for (int64_t t = gid; t < ntasks; t += NG) {
+        int64_t s, lo, hi;
+        if (has_head && t == 0) {
+            s = s_begin - 1;
+            lo = c0;
+        } else {
+            s = s_begin + t - has_head;
+            lo = sp[s];
+        }
+        const int64_t send = sp[s + 1];
+        hi = send < c1 ? send : c1;
+        T acc = 0;
+        for (int64_t i = lo + gl; i < hi; i += G) acc += prod[i - c0];
+        acc = group_sum<T, G>(acc);
+        if (gl == 0) {
+            if (has_head && t == 0) head[k] = acc;
+            else if (send > c1) tail[k] = acc;
+            else out[s] = apply_epi<T, EPI>(acc, a, z, s);
+        }
+    }
+}
+
+template <typename T, int EPI>
+__global__ __launch_bounds__(BS) void k_stream_fixup(int64_t nnz, int64_t nchunks, const int64_t* __restrict__ sp,
+                                                     const int32_t* __restrict__ fo, T* __restrict__ out, T a,
+                                                     const T* __restrict__ z, const T* __restrict__ head,
+                                                     const T* __restrict__ tail) {
+    for (int64_t k = (int64_t)blockIdx.x * BS + threadIdx.x; k < nchunks; k += (int64_t)gridDim.x * BS) {
+        const int64_t s_begin = fo[k], s_end = fo[k + 1];
+        if (s_end <= s_begin) continue;
+        const int64_t s = s_end - 1;
+        const int64_t c1 = (k + 1) * SCH < nnz ? (k + 1) * SCH : nnz;
+        if (sp[s + 1] <= c1) continue;
+        T sum = tail[k];
+        for (int64_t j = k + 1; j < nchunks; ++j) {
+            sum += head[j];
+            const int64_t cj1 = (j + 1) * SCH < nnz ? (j + 1) * SCH : nnz;
+            if (sp[s + 1] <= cj1) break;
+        }
+        out[s] = apply_epi<T, EPI>(sum, a, z, s);
+    }
+}
+
+template <typename T, int EPI>
+__global__ __launch_bounds__(BS) void k_fill_epi(int64_t n, T* __restrict__ out, T a, const T* __restrict__ z) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS)
+        out[i] = apply_epi<T, EPI>(T(0), a, z, i);
+}
+
+template <typename T, int G, int EPI, bool NT>
+static void launch_stream_e(hipStream_t st, const SegIndex& si, const int32_t* ci, const T* val, const T* x, T* out,
+                            T a, const T* z, T* head, T* tail) {
+    if (si.nnz == 0) {
+        int64_t g = (si.nseg + BS - 1) / BS;
+        if (g > 4096) g = 4096;
+        if (g > 0) k_fill_epi<T, EPI><<<g, BS, 0, st>>>(si.nseg, out, a, z);
+        return;
+    }
+    k_spmv_stream<T, G, EPI, NT><<<si.nchunks, BS, 0, st>>>(si.nnz, si.nseg, si.sp, si.fo, ci, val, x, out, a, z,
+                                                             head, tail);
+    int64_t g = (si.nchunks + BS - 1) / BS;
+    if (g > 4096) g = 4096;
+    k_stream_fixup<T, EPI><<<g, BS, 0, st>>>(si.nnz, si.nchunks, si.sp, si.fo, out, a, z, head, tail);
+}
+
+template <typename T, int G, bool NT>
+static void launch_stream_g(hipStream_t st, const SegIndex& si, const int32_t* ci, const T* val, const T* x, T* out,
+                            int epi, T a, const T* z, T* head, T* tail) {
+    switch (epi) {
+        case EPI_NONE: launch_stream_e<T, G, EPI_NONE, NT>(st, si, ci, val, x, out, a, z, head, tail); break;
+        case EPI_ADD: launch_stream_e<T, G, EPI_ADD, NT>(st, si, ci, val, x, out, a, z, head, tail); break;
+        case EPI_SUB: launch_stream_e<T, G, EPI_SUB, NT>(st, si, ci, val, x, out, a, z, head, tail); break;
+        default: launch_stream_e<T, G, EPI_RSUB, NT>(st, si, ci, val, x, out, a, z, head, tail); break;
+    }
+}
+
+template <typename T>
+static void spmv_stream(hgm_ctx* c, const SegIndex& si, int G, bool nt, const int32_t* ci, const T* val, const T* x,
+                        T* out, int epi, T a, const T* z) {
+    T* head = c->buf<T>("stream_head", si.nchunks + 1);
+    T* tail = c->buf<T>("stream_tail", si.nchunks + 1);
+    hipStream_t st = c->stream;
+#define HGM_SG(GG)                                                                              \
+    if (nt) launch_stream_g<T, GG, true>(st, si, ci, val, x, out, epi, a, z, head, tail);      \
+    else launch_stream_g<T, GG, false>(st, si, ci, val, x, out, epi, a, z, head, tail);
+    switch (G) {
+        case 64: HGM_SG(64) break;
+        case 32: HGM_SG(32) break;
+        case 16: HGM_SG(16) break;
+        case 8: HGM_SG(8) break;
+        default: HGM_SG(4) break;
+    }
+#undef HGM_SG
+}
+
 // y[r] = epi( sum_b ypart[b*rows + r] ), bands summed in increasing b (deterministic)
 template <typename T, int EPI>
 __global__ __launch_bounds__(BS) void k_band_reduce(int64_t rows, int nbands, const T* __restrict__ ypart,
@@ -272,10 +406,47 @@ static void spmv_banded(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi,
     }
 }
 
+template <typename T, int EPI>
+static void launch_band_reduce(hgm_ctx* c, const hgm_mat* M, const T* yp, T* y, T a, const T* z) {
+    int64_t g = (M->rows + BS - 1) / BS;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    k_band_reduce<T, EPI><<<g, BS, 0, c->stream>>>(M->rows, M->nbands, yp, y, a, z);
+}
+
+template <typename T>
+static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
+    const bool nt = M->variant & SPMV_NT;
+    if (M->nbands > 1) {
+        T* yp = c->buf<T>("band_part", (size_t)M->nbands * M->rows + 1);
+        SegIndex si{M->nnz, (int64_t)M->nbands * M->rows, stream_chunks(M->nnz), M->brp, M->bcfo};
+        spmv_stream<T>(c, si, M->bsgroup, nt, M->bci, reinterpret_cast<const T*>(M->bval), x, yp, EPI_NONE, T(0),
+                       nullptr);
+        switch (epi) {
+            case EPI_NONE: launch_band_reduce<T, EPI_NONE>(c, M, yp, y, a, z); break;
+            case EPI_ADD: launch_band_reduce<T, EPI_ADD>(c, M, yp, y, a, z); break;
+            case EPI_SUB: launch_band_reduce<T, EPI_SUB>(c, M, yp, y, a, z); break;
+            default: launch_band_reduce<T, EPI_RSUB>(c, M, yp, y, a, z); break;
+        }
+    } else {
+        SegIndex si{M->nnz, M->rows, stream_chunks(M->nnz), M->rp, M->cfo};
+        spmv_stream<T>(c, si, M->sgroup, nt, M->ci, reinterpret_cast<const T*>(M->val), x, y, epi, a, z);
+    }
+}
+
 template <typename T>
 void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, int kclass) {
     hipEvent_t t0 = nullptr;
     timing_begin(c, kclass, &t0);
+    if ((M->variant & SPMV_STREAM) && (M->nbands > 1 ? M->bcfo != nullptr : M->cfo != nullptr)) {
+        spmv_streamed<T>(c, M, x, y, epi, a, z);
+        HGM_HIP(hipGetLastError());
+        const double s = sizeof(T);
+        double bytes = (double)M->nnz * (s + 4) + 8.0 * (M->rows + 1) + s * M->cols + s * M->rows;
+        if (epi != EPI_NONE) bytes += s * M->rows;
+        timing_end(c, kclass, t0, bytes);
+        return;
+    }
     if (M->nbands > 1) {
         spmv_banded<T>(c, M, x, y, epi, a, z);
         HGM_HIP(hipGetLastError());
@@ -350,8 +521,36 @@ __global__ __launch_bounds__(BS) void k_finalize(const T* __restrict__ parts, in
     if (threadIdx.x == 0) out[blockIdx.x] = r;
 }
 
+// Single-launch reduction for short vectors (one 1024-thread block, fixed order).
+template <typename T, int OP>
+__global__ __launch_bounds__(1024) void k_reduce_single(int64_t n, const T* __restrict__ a,
+                                                        const T* __restrict__ b, T* out) {
+    __shared__ T sh[16];
+    T acc = 0;
+    for (int64_t i = threadIdx.x; i < n; i += 1024) {
+        if (OP == 0) acc += a[i] * b[i];
+        else if (OP == 1) acc += a[i] * a[i];
+        else { T d = a[i] - b[i]; acc += d * d; }
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T r = 0;
+        for (int w = 0; w < 16; ++w) r += sh[w];
+        *out = r;
+    }
+}
+
+constexpr int64_t SINGLE_MAX = 1 << 18;   // vectors up to 256 Ki entries: one launch
+
 template <typename T, int OP>
 static void reduce_to(hgm_ctx* c, int64_t n, const T* a, const T* b, T* out) {
+    if (n <= SINGLE_MAX) {
+        k_reduce_single<T, OP><<<1, 1024, 0, c->stream>>>(n, a, b, out);
+        HGM_HIP(hipGetLastError());
+        return;
+    }
     const int np = parts_for(n);
     T* parts = c->buf<T>("red_parts", MAX_PARTS);
     k_reduce_partial<T, OP><<<np, BS, 0, c->stream>>>(n, a, b, parts);
@@ -363,12 +562,14 @@ template <typename T> void dot(hgm_ctx* c, int64_t n, const T* a, const T* b, T*
 template <typename T> void sumsq(hgm_ctx* c, int64_t n, const T* a, T* out) { reduce_to<T, 1>(c, n, a, a, out); }
 template <typename T> void sumsq_diff(hgm_ctx* c, int64_t n, const T* a, const T* b, T* out) { reduce_to<T, 2>(c, n, a, b, out); }
 
-// partial dots of every column j (blockIdx.y) with w
+// partial dots of every column j (blockIdx.y) with w; column index ncols (if launched)
+// is the extra vector e
 template <typename T>
 __global__ __launch_bounds__(BS) void k_multidot(int64_t n, const T* __restrict__ Q, int64_t ldq,
-                                                 const T* __restrict__ w, T* __restrict__ parts) {
+                                                 const T* __restrict__ w, T* __restrict__ parts, int ncols,
+                                                 const T* __restrict__ e) {
     __shared__ T sh[4];
-    const T* q = Q + (int64_t)blockIdx.y * ldq;
+    const T* q = (int)blockIdx.y < ncols ? Q + (int64_t)blockIdx.y * ldq : e;
     T acc = 0;
     for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS)
         acc += q[i] * w[i];
@@ -377,12 +578,40 @@ __global__ __launch_bounds__(BS) void k_multidot(int64_t n, const T* __restrict_
 }
 
 template <typename T>
-void multidot(hgm_ctx* c, int64_t n, int ncols, const T* Q, int64_t ldq, const T* w, T* out) {
-    if (ncols <= 0) return;
+void multidot(hgm_ctx* c, int64_t n, int ncols, const T* Q, int64_t ldq, const T* w, T* out, const T* extra) {
+    const int nc = ncols + (extra ? 1 : 0);
+    if (nc <= 0) return;
     const int np = parts_for(n);
-    T* parts = c->buf<T>("mdot_parts", (size_t)np * ncols);
-    k_multidot<T><<<dim3(np, ncols), BS, 0, c->stream>>>(n, Q, ldq, w, parts);
-    k_finalize<T><<<ncols, BS, 0, c->stream>>>(parts, np, out);
+    T* parts = c->buf<T>("mdot_parts", (size_t)np * nc);
+    k_multidot<T><<<dim3(np, nc), BS, 0, c->stream>>>(n, Q, ldq, w, parts, ncols, extra);
+    k_finalize<T><<<nc, BS, 0, c->stream>>>(parts, np, out);
+    HGM_HIP(hipGetLastError());
+}
+
+// x = Q(:,0:k) y fused with the error monitor: parts[blk] = sum (x_i - xt_i)^2
+template <typename T>
+__global__ __launch_bounds__(BS) void k_gemv_err(int64_t n, int k, const T* __restrict__ Q, int64_t ldq,
+                                                 const T* __restrict__ y, T* __restrict__ x,
+                                                 const T* __restrict__ xt, T* __restrict__ parts) {
+    __shared__ T sh[4];
+    T acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+        T s = 0;
+        for (int j = 0; j < k; ++j) s += Q[(int64_t)j * ldq + i] * y[j];
+        x[i] = s;
+        const T d = s - xt[i];
+        acc += d * d;
+    }
+    const T tot = block_sum_all(acc, sh);
+    if (threadIdx.x == 0) parts[blockIdx.x] = tot;
+}
+
+template <typename T>
+void gemv_err(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T* x, const T* xt, T* err_out) {
+    const int np = parts_for(n);
+    T* parts = c->buf<T>("gemv_parts", MAX_PARTS);
+    k_gemv_err<T><<<np, BS, 0, c->stream>>>(n, k, Q, ldq, y, x, xt, parts);
+    k_finalize<T><<<1, BS, 0, c->stream>>>(parts, np, err_out);
     HGM_HIP(hipGetLastError());
 }
 
@@ -572,10 +801,10 @@ void cgs2(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist) 
     T* v = Q + (int64_t)k * ldq;
     T* h1 = c->buf<T>("cgs_h1", k + 8);
     T* h2 = c->buf<T>("cgs_h2", k + 8);
-    multidot<T>(c, n, k, Q, ldq, v, h1);
+    multidot<T>(c, n, k, Q, ldq, v, h1, nullptr);
     if (dist) allreduce(c, h1, k);
     gemv<T>(c, n, k, Q, ldq, h1, v, 1);
-    multidot<T>(c, n, k, Q, ldq, v, h2);
+    multidot<T>(c, n, k, Q, ldq, v, h2, nullptr);
     if (dist) allreduce(c, h2, k);
     gemv<T>(c, n, k, Q, ldq, h2, v, 1);
     k_add_store<T><<<1, BS, 0, c->stream>>>(k, h1, h2, Hcol);
@@ -677,7 +906,8 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
     template void dot<T>(hgm_ctx*, int64_t, const T*, const T*, T*);                           \
     template void sumsq<T>(hgm_ctx*, int64_t, const T*, T*);                                   \
     template void sumsq_diff<T>(hgm_ctx*, int64_t, const T*, const T*, T*);                    \
-    template void multidot<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*);        \
+    template void multidot<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, const T*); \
+    template void gemv_err<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, const T*, T*); \
     template void mgs<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool);                       \
     template void cgs2<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool);                      \
     template void gemv<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, int);       \

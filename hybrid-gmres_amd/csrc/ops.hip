@@ -39,7 +39,49 @@ hgm_mat* mat_alloc(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, int dtyp
 
 static int grid_cap(int64_t n);
 
+// fo[k] = first segment starting at or after chunk k's first entry; fo[nchunks] = nseg
+__global__ void k_chunk_fo(int64_t nchunks, int64_t nseg, const int64_t* __restrict__ sp, int32_t* __restrict__ fo) {
+    for (int64_t k = (int64_t)blockIdx.x * BS + threadIdx.x; k <= nchunks; k += (int64_t)gridDim.x * BS) {
+        if (k == nchunks) {
+            fo[k] = (int32_t)nseg;
+            continue;
+        }
+        const int64_t c0 = k * SCH;
+        int64_t lo = 0, hi = nseg;          // lower_bound over sp[0..nseg]
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (sp[mid] < c0) lo = mid + 1;
+            else hi = mid;
+        }
+        fo[k] = (int32_t)lo;
+    }
+}
+
+static int32_t* build_chunk_index(hgm_ctx* c, const int64_t* sp, int64_t nseg, int64_t nnz) {
+    const int64_t nch = stream_chunks(nnz);
+    int32_t* fo = nullptr;
+    HGM_HIP(hipMalloc(&fo, sizeof(int32_t) * (nch + 1)));
+    k_chunk_fo<<<grid_cap(nch + 1), BS, 0, c->stream>>>(nch, nseg, sp, fo);
+    HGM_HIP(hipGetLastError());
+    return fo;
+}
+
+static int stream_group(double avg) {
+    if (const char* g = std::getenv("HGM_STREAM_GROUP")) return std::atoi(g);
+    return avg >= 512 ? 64 : (avg >= 128 ? 32 : (avg >= 40 ? 16 : 8));
+}
+
+void build_stream_index(hgm_ctx* c, hgm_mat* M) {
+    HGM_REQUIRE(M->rows < (int64_t)INT32_MAX, "stream index: rows must be < 2^31");
+    if (M->cfo) (void)hipFree(M->cfo);
+    M->cfo = build_chunk_index(c, M->rp, M->rows, M->nnz);
+    M->sgroup = stream_group(M->rows ? (double)M->nnz / M->rows : 0.0);
+    HGM_HIP(hipStreamSynchronize(c->stream));
+}
+
 static void free_bands(hgm_mat* M) {
+    if (M->bcfo) (void)hipFree(M->bcfo);
+    M->bcfo = nullptr;
     if (M->brp) (void)hipFree(M->brp);
     if (M->bci) (void)hipFree(M->bci);
     if (M->bval) (void)hipFree(M->bval);
@@ -53,6 +95,7 @@ static void free_bands(hgm_mat* M) {
 void mat_free(hgm_mat* M) {
     if (!M) return;
     free_bands(M);
+    if (M->cfo) (void)hipFree(M->cfo);
     if (M->rp) (void)hipFree(M->rp);
     if (M->ci) (void)hipFree(M->ci);
     if (M->val) (void)hipFree(M->val);
@@ -81,6 +124,35 @@ __global__ void k_band_fill(int64_t rows, int64_t W, const int64_t* __restrict__
         }
 }
 
+// Kernel defaults from the gfx950 sweep (profiles/):
+//   long rows (ray-major A), x within one XCD's L2  -> row kernel, 32 lanes/row, 16-B loads
+//   long rows, x beyond L2                          -> 128 Ki-pixel column bands + streaming kernel
+//   short rows (pixel-major B), < 5e7 nnz           -> row kernel, 8 lanes/row, 8-B loads
+//   short rows, >= 5e7 nnz                          -> streaming kernel, nontemporal loads
+void finalize_operator(hgm_ctx* c, hgm_mat* M) {
+    if (M->nnz > 0) build_stream_index(c, M);
+    const double avg = M->rows ? (double)M->nnz / (double)M->rows : 0.0;
+    set_bands(c, M, auto_band_width(M));
+    if (avg >= 64) {
+        if (M->nbands > 1) {
+            M->variant = SPMV_STREAM;
+            M->bsgroup = 32;
+        } else {
+            M->variant = SPMV_VEC;
+            M->group = 32;
+        }
+    } else {
+        if (M->nnz >= 50000000) {
+            M->variant = SPMV_STREAM | SPMV_NT;
+            M->sgroup = 8;
+        } else {
+            M->variant = 0;
+            M->group = avg >= 6 ? 8 : 4;
+        }
+    }
+    if (const char* v = std::getenv("HGM_SPMV_VARIANT")) M->variant = std::atoi(v);
+}
+
 int64_t auto_band_width(const hgm_mat* M) {
     const size_t vs = M->dtype == HGM_F32 ? 4 : 8;
     if (const char* e = std::getenv("HGM_BAND_WIDTH")) return std::atoll(e);
@@ -88,7 +160,7 @@ int64_t auto_band_width(const hgm_mat* M) {
     if ((double)M->cols * vs <= 4.0 * 1024 * 1024) return 0;
     // only long-row operators benefit (the short pixel-major rows of B gather an L2-resident y)
     if (M->rows > 0 && (double)M->nnz / (double)M->rows < 64) return 0;
-    return (int64_t)(1 << 18);   // 256 Ki pixels = 2 MiB fp64 x-slice per band
+    return (int64_t)(1 << 17);   // 128 Ki pixels = 1 MiB fp64 x-slice per band
 }
 
 void set_bands(hgm_ctx* c, hgm_mat* M, int64_t W) {
@@ -134,6 +206,12 @@ void set_bands(hgm_ctx* c, hgm_mat* M, int64_t W) {
     const double avg = (double)M->nnz / (double)nseg;
     M->bgroup = avg >= 96 ? 32 : (avg >= 24 ? 16 : 8);
     if (const char* g = std::getenv("HGM_BAND_GROUP")) M->bgroup = std::atoi(g);
+    // streaming index over the (band,row) segments; ~2/3 of them are non-empty for a
+    // parallel-beam operator, hence the 1.5 factor in the average segment length
+    M->bcfo = build_chunk_index(c, M->brp, nseg, M->nnz);
+    M->bsgroup = stream_group((double)M->nnz / (double)(M->rows > 0 ? M->rows : 1) /
+                              (double)(nb > 0 ? nb : 1) * 1.5);
+    HGM_HIP(hipStreamSynchronize(st));
 }
 
 // --------------------------------------------------------------------------

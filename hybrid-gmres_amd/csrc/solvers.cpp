@@ -225,8 +225,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         if (sp.proj == PROJ_ABRTP) {
             // column k of AQk'*AQk and AQk'*b (hybrid_ab_gmres_rtp.m:31-32); A*Q(:,j) was
             // computed inside M_reg_op(Q(:,j)) at :19 — the same deterministic SpMV.
-            multidot<T>(c, m, k + 1, AQ, ldaq, AQ + (int64_t)k * ldaq, gcol);
-            dot<T>(c, m, AQ + (int64_t)k * ldaq, b, gcol + k + 1);
+            multidot<T>(c, m, k + 1, AQ, ldaq, AQ + (int64_t)k * ldaq, gcol, b);   // + gcol[k+1] = b'*AQ(:,k)
             rd.add(&G[(size_t)k * maxit], gcol, sizeof(T) * (k + 1));
             rd.add(&cvec[k], gcol + k + 1, sizeof(T));
         }
@@ -266,19 +265,21 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             for (int i = 0; i < kk; ++i) M[(size_t)i * kk + i] += lambda;
             dense::mldivide_square(kk, M.data(), cvec.data(), y.data());
         }
-        h2d(c, yd, y.data(), sizeof(double) * kk);
+        h2d_pinned(c, yd, y.data(), sizeof(double) * kk);
         // ---- reconstruction (hybrid_*_rtp.m:30/33 ; *_bounds.m:37-38) ----
         if (nspace) {
-            gemv<T>(c, n, kk, Q, ldq, yd, x, 0);                 // x = Q(:,1:k)*yk
+            // x = Q(:,1:k)*yk, fused with the error monitor ||x - x_true||^2 (:33 / :36)
+            gemv_err<T>(c, n, kk, Q, ldq, yd, x, xt, dslot<T>(c, S_ERR));
+            if (dist_n(c)) allreduce(c, dslot<T>(c, S_ERR), 1);
         } else {
             gemv<T>(c, m, kk, Q, ldq, yd, z, 0);                 // zk = Q(:,1:k)*yk
             apply_B<T>(c, B, z, x, EPI_NONE, T(0), nullptr);     // xk = B*zk
+            nsumsq_diff<T>(c, n, x, xt, dslot<T>(c, S_ERR));
         }
         x_assigned = true;
         // ---- monitors (hybrid_*_rtp.m:32-33 / :35-36) ----
         apply_A<T>(c, A, x, t, EPI_RSUB, T(0), b);              // b - A*x
         sumsq<T>(c, m, t, dslot<T>(c, S_RES));
-        nsumsq_diff<T>(c, n, x, xt, dslot<T>(c, S_ERR));
         read_scalars(c, S_RES, 2);
         res[k] = std::sqrt(c->hscal[S_RES]) / nb;
         err[k] = std::sqrt(c->hscal[S_ERR]) / nxt;
@@ -609,7 +610,7 @@ int hybrid_lsmr(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* 
         for (int i = 0; i < kk; ++i) RHS[i] = sc * Gm[i];
         y.assign(kk, 0.0);
         dense::mldivide_square(kk, LHS.data(), RHS.data(), y.data());          // :44
-        h2d(c, yd, y.data(), sizeof(double) * kk);
+        h2d_pinned(c, yd, y.data(), sizeof(double) * kk);
         gemv<T>(c, n, kk, V, ldv, yd, x, 0);                                   // :45
         nsumsq_diff<T>(c, n, x, xt, sl + S_ERR);                               // :47
         apply_A<T>(c, A, x, t, EPI_RSUB, 0.0, b);                              // :48

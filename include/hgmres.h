@@ -118,7 +118,9 @@ HGM_API int hgm_mat_create_siddon(hgm_ctx* ctx, int N, int n_angles, double det_
 HGM_API int hgm_mat_info(const hgm_mat* mat, int64_t* rows, int64_t* cols, int64_t* nnz, int* dtype);
 /* SpMV kernel selection for this operator (tuning/benchmark hook): variant bits
  * 1 = 16-byte paired loads, 2 = nontemporal val/col loads, 4 = XCD-aware row-block
- * order; group = lanes per row (4, 8, 16, 32 or 64; 0 keeps the current choice). */
+ * order, 8 = nnz-balanced streaming kernel (2048-entry chunks, LDS-staged products);
+ * group = lanes per row, or per segment reduction with bit 8 (4, 8, 16, 32 or 64;
+ * 0 keeps the current choice). */
 HGM_API int hgm_mat_tune(hgm_mat* mat, int variant, int group);
 /* Column banding of the SpMV x-gather (cache blocking): band_width pixels per band
  * (0 = off, -1 = automatic: on for long-row operators whose x exceeds one XCD's L2),

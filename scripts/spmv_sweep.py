@@ -57,16 +57,17 @@ def main():
             lib.hgm_dev_alloc(ctx.handle, 8 * rows, C.byref(yd))
             ones = np.ones(cols)
             lib.hgm_memcpy_h2d(ctx.handle, xd, ones.ctypes.data_as(C.c_void_p), 8 * cols)
+            # (band_width, band_group, group (rows kernel) or stream-reduction lanes, variant)
             if name == "A":
-                widths = [0] + ([w for w in (1 << 16, 1 << 17, 1 << 18, 1 << 19, 1 << 20) if w < cols])
+                widths = [0] + ([w for w in (1 << 17, 1 << 18, 1 << 19, 1 << 20) if w < cols])
                 cases = []
                 for w in widths:
                     if w == 0:
-                        cases += [(0, 0, g, v) for g in (32, 64) for v in (1, 3)]
+                        cases += [(0, 0, 32, 1), (0, 0, 32, 3), (0, 0, 32, 8), (0, 0, 64, 8), (0, 0, 64, 10)]
                     else:
-                        cases += [(w, g, 0, v) for g in ((16,) if a.quick else (8, 16, 32)) for v in (1, 3)]
+                        cases += [(w, 8, 0, 1), (w, 8, 8, 8), (w, 8, 16, 8), (w, 8, 32, 8), (w, 8, 16, 10)]
             else:
-                cases = [(0, 0, g, v) for g in (8, 16) for v in (0, 1, 3)]
+                cases = [(0, 0, 8, 0), (0, 0, 8, 1), (0, 0, 4, 8), (0, 0, 8, 8), (0, 0, 16, 8), (0, 0, 8, 10)]
             cur_w = None
             for (w, bg, g, v) in cases:
                 if w != cur_w:
