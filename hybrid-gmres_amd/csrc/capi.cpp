@@ -71,16 +71,32 @@ void Timing::clear() {
     }
 }
 
+// SpMV classes arm events that the kernel launches carry in their dispatch packets
+// (first launch: start, last launch: stop); other classes use stream markers.
 void timing_begin(hgm_ctx* c, int cls, hipEvent_t* start) {
     *start = nullptr;
     if (!c->timing.on || cls < 0 || cls >= KC_N) return;
     *start = c->timing.get();
-    HGM_HIP(hipEventRecord(*start, c->stream));
+    if (cls == KC_SPMV_A || cls == KC_SPMV_B) {
+        c->arm_start = *start;
+        c->arm_stop = c->cur_stop = c->timing.get();
+    } else {
+        HGM_HIP(hipEventRecord(*start, c->stream));
+    }
 }
 void timing_end(hgm_ctx* c, int cls, hipEvent_t start, double bytes) {
     if (!start) return;
-    hipEvent_t stop = c->timing.get();
-    HGM_HIP(hipEventRecord(stop, c->stream));
+    hipEvent_t stop;
+    if (cls == KC_SPMV_A || cls == KC_SPMV_B) {
+        stop = c->cur_stop;
+        // events not consumed by a launch (nothing launched) are recorded as markers
+        if (c->arm_start) HGM_HIP(hipEventRecord(c->arm_start, c->stream));
+        if (c->arm_stop) HGM_HIP(hipEventRecord(c->arm_stop, c->stream));
+        c->arm_start = c->arm_stop = c->cur_stop = nullptr;
+    } else {
+        stop = c->timing.get();
+        HGM_HIP(hipEventRecord(stop, c->stream));
+    }
     c->timing.ev[cls].push_back({start, stop});
     c->timing.bytes[cls] += bytes;
 }

@@ -73,6 +73,9 @@ struct hgm_ctx {
     size_t hstage_bytes = 0;
     double* hup = nullptr;                    // pinned upload buffer (projected-solve y)
     size_t hup_bytes = 0;
+    // kernel-timing events armed for the next launch(es): recorded inside the dispatch
+    // packets (hipExtLaunchKernelGGL), so they bracket kernel execution only
+    hipEvent_t arm_start = nullptr, arm_stop = nullptr, cur_stop = nullptr;
     hgm::Timing timing;
 
     template <typename T>

@@ -1,0 +1,412 @@
+// Sparse matrix-vector products of the Arnoldi / Golub-Kahan loop, hand-written for
+// gfx950 (CDNA4).  Three kernels, chosen per operator (ops.hip: finalize_operator):
+//  * k_spmv        one G-lane group per CSR row (G = 32 for the long ray-major rows of A,
+//                  G = 8 for the short pixel-major rows of B = A'), optional 16-byte
+//                  paired loads / nontemporal loads / XCD-aware block order;
+//  * k_spmv_band   the same over column bands of A (cache blocking of the x gather: the
+//                  blocks in flight gather from one L2-resident x-slice), followed by a
+//                  fixed-order band reduction;
+//  * k_spmv_stream nnz-balanced: fixed 2048-entry chunks streamed with 16-byte loads,
+//                  products staged in LDS, per-segment reduction, fixed-order fix-up.
+// Every reduction is a fixed tree (no atomics): repeated products are bitwise equal.
+// Epilogues of the reference's operator closures are fused into the final store:
+// `B*(A*v) + lambda*v` (hybrid_*_rtp.m:6), `A*v - alpha*u` (lsqr_solver.m:22),
+// `A'*u - beta*v` (lsqr_solver.m:26), `b - A*x` (hybrid_*_rtp.m:32/35).
+#include "device_common.h"
+
+namespace hgm {
+
+// XCD-aware block order (speed only, never correctness): consecutive logical row blocks
+// run on the same XCD so neighbouring rays share x lines in that XCD's L2
+// (cdna_hip_programming.md §5 "XCD swizzle must be bijective").
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+    const int64_t q = nb / 8, r = nb % 8, xcd = b % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
+
+// One G-lane group per CSR row.  VEC: each lane streams pairs of entries with 16-byte
+// value loads and 8-byte index loads (row heads/tails peeled to keep them aligned).
+// NT: nontemporal (streaming) loads for val/col so they do not evict x from L2/MALL.
+// Per-lane partial of the dot product of entries [s, e) with x, lane gl of a G-lane group.
+template <typename T, int G, bool VEC, bool NT>
+__device__ __forceinline__ T seg_partial(int64_t s, int64_t e, int gl, const int32_t* __restrict__ ci,
+                                         const T* __restrict__ val, const T* __restrict__ x) {
+    T a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    {
+        if (!VEC) {
+            int64_t i = s + gl;
+            for (; i + 3 * G < e; i += 4 * G) {
+                const int32_t c0 = ld<NT>(ci + i), c1 = ld<NT>(ci + i + G), c2 = ld<NT>(ci + i + 2 * G),
+                              c3 = ld<NT>(ci + i + 3 * G);
+                const T v0 = ld<NT>(val + i), v1 = ld<NT>(val + i + G), v2 = ld<NT>(val + i + 2 * G),
+                        v3 = ld<NT>(val + i + 3 * G);
+                a0 += v0 * x[c0];
+                a1 += v1 * x[c1];
+                a2 += v2 * x[c2];
+                a3 += v3 * x[c3];
+            }
+            for (; i < e; i += G) a0 += ld<NT>(val + i) * x[ld<NT>(ci + i)];
+        } else {
+            using T2 = typename NV2<T>::t;
+            using I2 = ni2;
+            const int64_t s2 = (s + 1) & ~int64_t(1);     // first even index >= s
+            const int64_t e2 = e & ~int64_t(1);           // last even bound <= e
+            if (gl == 0 && s < s2 && s < e) a0 += ld<NT>(val + s) * x[ld<NT>(ci + s)];
+            if (gl == G - 1 && e2 < e && e2 >= s2) a1 += ld<NT>(val + e2) * x[ld<NT>(ci + e2)];
+            int64_t i = s2 + 2 * gl;
+            for (; i + 2 * G < e2; i += 4 * G) {
+                const I2 c0 = ld<NT>(reinterpret_cast<const I2*>(ci + i));
+                const I2 c1 = ld<NT>(reinterpret_cast<const I2*>(ci + i + 2 * G));
+                const T2 v0 = ld<NT>(reinterpret_cast<const T2*>(val + i));
+                const T2 v1 = ld<NT>(reinterpret_cast<const T2*>(val + i + 2 * G));
+                a0 += v0.x * x[c0.x];
+                a1 += v0.y * x[c0.y];
+                a2 += v1.x * x[c1.x];
+                a3 += v1.y * x[c1.y];
+            }
+            for (; i < e2; i += 2 * G) {
+                const I2 c0 = ld<NT>(reinterpret_cast<const I2*>(ci + i));
+                const T2 v0 = ld<NT>(reinterpret_cast<const T2*>(val + i));
+                a0 += v0.x * x[c0.x];
+                a1 += v0.y * x[c0.y];
+            }
+        }
+    }
+    return (a0 + a1) + (a2 + a3);
+}
+
+template <typename T, int G, int EPI, bool VEC, bool NT>
+__global__ __launch_bounds__(BS) void k_spmv(int64_t rows, const int64_t* __restrict__ rp,
+                                             const int32_t* __restrict__ ci,
+                                             const T* __restrict__ val, const T* __restrict__ x,
+                                             T* __restrict__ y, T a, const T* __restrict__ z, int xcd) {
+    constexpr int RPB = BS / G;
+    const int64_t blk = xcd ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t row = blk * RPB + threadIdx.x / G;
+    const int gl = threadIdx.x & (G - 1);
+    T acc = 0;
+    if (row < rows) acc = seg_partial<T, G, VEC, NT>(rp[row], rp[row + 1], gl, ci, val, x);
+    acc = group_sum<T, G>(acc);
+    if (gl == 0 && row < rows) y[row] = apply_epi<T, EPI>(acc, a, z, row);
+}
+
+// Column-banded SpMV: work items (band b, block of RPB rows) in band-major order, grid-
+// stride, so the blocks resident at any moment gather x from one band's slice (L2-
+// resident).  Writes the per-band partial ypart[b*rows + r]; k_band_reduce sums them.
+template <typename T, int G, bool VEC, bool NT>
+__global__ __launch_bounds__(BS) void k_spmv_band(int64_t rows, int nbands, const int64_t* __restrict__ brp,
+                                                  const int32_t* __restrict__ ci, const T* __restrict__ val,
+                                                  const T* __restrict__ x, T* __restrict__ ypart) {
+    constexpr int RPB = BS / G;
+    const int64_t rb_per_band = (rows + RPB - 1) / RPB;
+    const int64_t items = rb_per_band * nbands;
+    const int gl = threadIdx.x & (G - 1);
+    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const int64_t b = it / rb_per_band;
+        const int64_t row = (it - b * rb_per_band) * RPB + threadIdx.x / G;
+        T acc = 0;
+        if (row < rows) {
+            const int64_t* p = brp + b * rows + row;
+            acc = seg_partial<T, G, VEC, NT>(p[0], p[1], gl, ci, val, x);
+        }
+        acc = group_sum<T, G>(acc);
+        if (gl == 0 && row < rows) ypart[b * rows + row] = acc;
+    }
+}
+
+// ------------------------------------------------------------------------------
+// nnz-balanced streaming SpMV over segments (rows, or (band,row) pairs).
+// Block k owns entries [k*CH, (k+1)*CH): it streams them with 16-byte loads, stages the
+// products in LDS, then G-lane groups reduce every segment that STARTS in the chunk
+// (fo[k] .. fo[k+1]) plus the head part of the segment that started earlier.  Complete
+// segments are written (with the epilogue); a segment running past the chunk leaves its
+// partial in tail[k] and every later chunk's share in head[j]; k_stream_fixup adds them
+// in chunk order.  Fixed chunking => fixed summation order => bitwise reproducible.
+// ------------------------------------------------------------------------------
+template <typename T, int G, int EPI, bool NT>
+__global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, const int64_t* __restrict__ sp,
+                                                    const int32_t* __restrict__ fo, const int32_t* __restrict__ ci,
+                                                    const T* __restrict__ val, const T* __restrict__ x,
+                                                    T* __restrict__ out, T a, const T* __restrict__ z,
+                                                    T* __restrict__ head, T* __restrict__ tail) {
+    using T2 = typename NV2<T>::t;
+    __shared__ T prod[SCH];
+    const int64_t k = blockIdx.x;
+    const int64_t c0 = k * SCH;
+    const int64_t c1 = (c0 + SCH < nnz) ? c0 + SCH : nnz;
+    const int n = (int)(c1 - c0);
+    if (n == SCH) {
+#pragma unroll
+        for (int u = 0; u < SCH / (2 * BS); ++u) {
+            const int j = 2 * threadIdx.x + u * 2 * BS;
+            const T2 v = ld<NT>(reinterpret_cast<const T2*>(val + c0 + j));
+            const ni2 cc = ld<NT>(reinterpret_cast<const ni2*>(ci + c0 + j));
+            prod[j] = v.x * x[cc.x];
+            prod[j + 1] = v.y * x[cc.y];
+        }
+    } else {
+        for (int j = threadIdx.x; j < n; j += BS) prod[j] = val[c0 + j] * x[ci[c0 + j]];
+    }
+    __syncthreads();
+    const int64_t s_begin = fo[k], s_end = fo[k + 1];
+    const int has_head = (s_begin > 0 && sp[s_begin] > c0) ? 1 : 0;
+    const int64_t ntasks = (s_end - s_begin) + has_head;
+    const int gid = threadIdx.x / G, gl = threadIdx.x & (G - 1);
+    constexpr int NG = BS / G;
+    for (int64_t t = gid; t < ntasks; t += NG) {
+        int64_t s, lo, hi;
+        if (has_head && t == 0) {
+            s = s_begin - 1;
+            lo = c0;
+        } else {
+            s = s_begin + t - has_head;
+            lo = sp[s];
+        }
+        const int64_t send = sp[s + 1];
+        hi = send < c1 ? send : c1;
+        T acc = 0;
+        for (int64_t i = lo + gl; i < hi; i += G) acc += prod[i - c0];
+        acc = group_sum<T, G>(acc);
+        if (gl == 0) {
+            if (has_head && t == 0) head[k] = acc;
+            else if (send > c1) tail[k] = acc;
+            else out[s] = apply_epi<T, EPI>(acc, a, z, s);
+        }
+    }
+}
+
+template <typename T, int EPI>
+__global__ __launch_bounds__(BS) void k_stream_fixup(int64_t nnz, int64_t nchunks, const int64_t* __restrict__ sp,
+                                                     const int32_t* __restrict__ fo, T* __restrict__ out, T a,
+                                                     const T* __restrict__ z, const T* __restrict__ head,
+                                                     const T* __restrict__ tail) {
+    for (int64_t k = (int64_t)blockIdx.x * BS + threadIdx.x; k < nchunks; k += (int64_t)gridDim.x * BS) {
+        const int64_t s_begin = fo[k], s_end = fo[k + 1];
+        if (s_end <= s_begin) continue;
+        const int64_t s = s_end - 1;
+        const int64_t c1 = (k + 1) * SCH < nnz ? (k + 1) * SCH : nnz;
+        if (sp[s + 1] <= c1) continue;
+        T sum = tail[k];
+        for (int64_t j = k + 1; j < nchunks; ++j) {
+            sum += head[j];
+            const int64_t cj1 = (j + 1) * SCH < nnz ? (j + 1) * SCH : nnz;
+            if (sp[s + 1] <= cj1) break;
+        }
+        out[s] = apply_epi<T, EPI>(sum, a, z, s);
+    }
+}
+
+template <typename T, int EPI>
+__global__ __launch_bounds__(BS) void k_fill_epi(int64_t n, T* __restrict__ out, T a, const T* __restrict__ z) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS)
+        out[i] = apply_epi<T, EPI>(T(0), a, z, i);
+}
+
+// y[r] = epi( sum_b ypart[b*rows + r] ), bands summed in increasing b (deterministic)
+template <typename T, int EPI>
+__global__ __launch_bounds__(BS) void k_band_reduce(int64_t rows, int nbands, const T* __restrict__ ypart,
+                                                    T* __restrict__ y, T a, const T* __restrict__ z) {
+    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BS) {
+        T s = 0;
+        for (int b = 0; b < nbands; ++b) s += ypart[(int64_t)b * rows + r];
+        y[r] = apply_epi<T, EPI>(s, a, z, r);
+    }
+}
+
+int pick_group(int64_t rows, int64_t nnz) {
+    const double avg = rows > 0 ? (double)nnz / (double)rows : 0.0;
+    if (avg >= 128) return 64;
+    if (avg >= 40) return 32;
+    if (avg >= 16) return 16;
+    if (avg >= 6) return 8;
+    return 4;
+}
+
+
+template <typename T, int EPI>
+__global__ __launch_bounds__(BS) void k_epi(int64_t n, T* __restrict__ y, T a, const T* __restrict__ z) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS)
+        y[i] = apply_epi<T, EPI>(y[i], a, z, i);
+}
+
+
+// ------------------------------------------------------------------------------
+// launchers (every SpMV launch goes through hgm::launch so armed timing events ride
+// in the dispatch packets of the first / last kernel of the product)
+// ------------------------------------------------------------------------------
+template <typename T, int G, int EPI, bool NT>
+static void launch_stream_e(hgm_ctx* c, bool last, const SegIndex& si, const int32_t* ci, const T* val, const T* x,
+                            T* out, T a, const T* z, T* head, T* tail) {
+    if (si.nnz == 0) {
+        int64_t g = (si.nseg + BS - 1) / BS;
+        if (g > 4096) g = 4096;
+        if (g > 0) launch(c, last, k_fill_epi<T, EPI>, dim3(g), dim3(BS), si.nseg, out, a, z);
+        return;
+    }
+    launch(c, false, k_spmv_stream<T, G, EPI, NT>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg, si.sp, si.fo, ci,
+           val, x, out, a, z, head, tail);
+    int64_t g = (si.nchunks + BS - 1) / BS;
+    if (g > 4096) g = 4096;
+    launch(c, last, k_stream_fixup<T, EPI>, dim3(g), dim3(BS), si.nnz, si.nchunks, si.sp, si.fo, out, a, z,
+           (const T*)head, (const T*)tail);
+}
+
+template <typename T, int G, bool NT>
+static void launch_stream_g(hgm_ctx* c, bool last, const SegIndex& si, const int32_t* ci, const T* val, const T* x,
+                            T* out, int epi, T a, const T* z, T* head, T* tail) {
+    switch (epi) {
+        case EPI_NONE: launch_stream_e<T, G, EPI_NONE, NT>(c, last, si, ci, val, x, out, a, z, head, tail); break;
+        case EPI_ADD: launch_stream_e<T, G, EPI_ADD, NT>(c, last, si, ci, val, x, out, a, z, head, tail); break;
+        case EPI_SUB: launch_stream_e<T, G, EPI_SUB, NT>(c, last, si, ci, val, x, out, a, z, head, tail); break;
+        default: launch_stream_e<T, G, EPI_RSUB, NT>(c, last, si, ci, val, x, out, a, z, head, tail); break;
+    }
+}
+
+template <typename T>
+static void spmv_stream(hgm_ctx* c, bool last, const SegIndex& si, int G, bool nt, const int32_t* ci, const T* val,
+                        const T* x, T* out, int epi, T a, const T* z) {
+    T* head = c->buf<T>("stream_head", si.nchunks + 1);
+    T* tail = c->buf<T>("stream_tail", si.nchunks + 1);
+#define HGM_SG(GG)                                                                              \
+    if (nt) launch_stream_g<T, GG, true>(c, last, si, ci, val, x, out, epi, a, z, head, tail);  \
+    else launch_stream_g<T, GG, false>(c, last, si, ci, val, x, out, epi, a, z, head, tail);
+    switch (G) {
+        case 64: HGM_SG(64) break;
+        case 32: HGM_SG(32) break;
+        case 16: HGM_SG(16) break;
+        case 8: HGM_SG(8) break;
+        default: HGM_SG(4) break;
+    }
+#undef HGM_SG
+}
+
+template <typename T, int G, bool VEC, bool NT>
+static void launch_spmv_v(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
+    const int64_t nb = (M->rows + (BS / G) - 1) / (BS / G);
+    if (nb == 0) return;
+    const T* val = reinterpret_cast<const T*>(M->val);
+    const int xcd = (M->variant & SPMV_XCD) ? 1 : 0;
+    const dim3 g((unsigned)nb), b(BS);
+    switch (epi) {
+        case EPI_NONE: launch(c, true, k_spmv<T, G, EPI_NONE, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd); break;
+        case EPI_ADD: launch(c, true, k_spmv<T, G, EPI_ADD, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd); break;
+        case EPI_SUB: launch(c, true, k_spmv<T, G, EPI_SUB, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd); break;
+        default: launch(c, true, k_spmv<T, G, EPI_RSUB, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd); break;
+    }
+}
+
+template <typename T, int G>
+static void launch_spmv_g(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
+    const bool vec = M->variant & SPMV_VEC, nt = M->variant & SPMV_NT;
+    if (vec && nt) launch_spmv_v<T, G, true, true>(c, M, x, y, epi, a, z);
+    else if (vec) launch_spmv_v<T, G, true, false>(c, M, x, y, epi, a, z);
+    else if (nt) launch_spmv_v<T, G, false, true>(c, M, x, y, epi, a, z);
+    else launch_spmv_v<T, G, false, false>(c, M, x, y, epi, a, z);
+}
+
+template <typename T, int G, bool VEC, bool NT>
+static void launch_band_v(hgm_ctx* c, const hgm_mat* M, const T* x, T* yp) {
+    constexpr int RPB = BS / G;
+    const int64_t items = (M->rows + RPB - 1) / RPB * M->nbands;
+    int64_t grid = 256 * 8;                      // ~all resident blocks, grid-stride in band-major order
+    if (grid > items) grid = items;
+    if (grid < 1) return;
+    launch(c, false, k_spmv_band<T, G, VEC, NT>, dim3((unsigned)grid), dim3(BS), M->rows, M->nbands, M->brp, M->bci,
+           reinterpret_cast<const T*>(M->bval), x, yp);
+}
+
+template <typename T, int G>
+static void launch_band_g(hgm_ctx* c, const hgm_mat* M, const T* x, T* yp) {
+    const bool vec = M->variant & SPMV_VEC, nt = M->variant & SPMV_NT;
+    if (vec && nt) launch_band_v<T, G, true, true>(c, M, x, yp);
+    else if (vec) launch_band_v<T, G, true, false>(c, M, x, yp);
+    else if (nt) launch_band_v<T, G, false, true>(c, M, x, yp);
+    else launch_band_v<T, G, false, false>(c, M, x, yp);
+}
+
+template <typename T, int EPI>
+static void launch_band_reduce(hgm_ctx* c, const hgm_mat* M, const T* yp, T* y, T a, const T* z) {
+    launch(c, true, k_band_reduce<T, EPI>, dim3(grid_for(M->rows)), dim3(BS), M->rows, M->nbands, yp, y, a, z);
+}
+
+template <typename T>
+static void band_reduce(hgm_ctx* c, const hgm_mat* M, const T* yp, T* y, int epi, T a, const T* z) {
+    switch (epi) {
+        case EPI_NONE: launch_band_reduce<T, EPI_NONE>(c, M, yp, y, a, z); break;
+        case EPI_ADD: launch_band_reduce<T, EPI_ADD>(c, M, yp, y, a, z); break;
+        case EPI_SUB: launch_band_reduce<T, EPI_SUB>(c, M, yp, y, a, z); break;
+        default: launch_band_reduce<T, EPI_RSUB>(c, M, yp, y, a, z); break;
+    }
+}
+
+template <typename T>
+static void spmv_banded(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
+    T* yp = c->buf<T>("band_part", (size_t)M->nbands * M->rows + 1);
+    switch (M->bgroup) {
+        case 64: launch_band_g<T, 64>(c, M, x, yp); break;
+        case 32: launch_band_g<T, 32>(c, M, x, yp); break;
+        case 16: launch_band_g<T, 16>(c, M, x, yp); break;
+        case 8: launch_band_g<T, 8>(c, M, x, yp); break;
+        default: launch_band_g<T, 4>(c, M, x, yp); break;
+    }
+    band_reduce<T>(c, M, yp, y, epi, a, z);
+}
+
+template <typename T>
+static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
+    const bool nt = M->variant & SPMV_NT;
+    if (M->nbands > 1) {
+        T* yp = c->buf<T>("band_part", (size_t)M->nbands * M->rows + 1);
+        SegIndex si{M->nnz, (int64_t)M->nbands * M->rows, stream_chunks(M->nnz), M->brp, M->bcfo};
+        spmv_stream<T>(c, false, si, M->bsgroup, nt, M->bci, reinterpret_cast<const T*>(M->bval), x, yp, EPI_NONE,
+                       T(0), nullptr);
+        band_reduce<T>(c, M, yp, y, epi, a, z);
+    } else {
+        SegIndex si{M->nnz, M->rows, stream_chunks(M->nnz), M->rp, M->cfo};
+        spmv_stream<T>(c, true, si, M->sgroup, nt, M->ci, reinterpret_cast<const T*>(M->val), x, y, epi, a, z);
+    }
+}
+
+template <typename T>
+void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, int kclass) {
+    hipEvent_t t0 = nullptr;
+    timing_begin(c, kclass, &t0);
+    if ((M->variant & SPMV_STREAM) && (M->nbands > 1 ? M->bcfo != nullptr : M->cfo != nullptr)) {
+        spmv_streamed<T>(c, M, x, y, epi, a, z);
+    } else if (M->nbands > 1) {
+        spmv_banded<T>(c, M, x, y, epi, a, z);
+    } else {
+        switch (M->group) {
+            case 64: launch_spmv_g<T, 64>(c, M, x, y, epi, a, z); break;
+            case 32: launch_spmv_g<T, 32>(c, M, x, y, epi, a, z); break;
+            case 16: launch_spmv_g<T, 16>(c, M, x, y, epi, a, z); break;
+            case 8: launch_spmv_g<T, 8>(c, M, x, y, epi, a, z); break;
+            default: launch_spmv_g<T, 4>(c, M, x, y, epi, a, z); break;
+        }
+    }
+    HGM_HIP(hipGetLastError());
+    // algorithmic bytes: nnz*(s+4) + 8(rows+1) + s*cols + s*rows (+ s*rows epilogue operand)
+    const double s = sizeof(T);
+    double bytes = (double)M->nnz * (s + 4) + 8.0 * (M->rows + 1) + s * M->cols + s * M->rows;
+    if (epi != EPI_NONE) bytes += s * M->rows;
+    timing_end(c, kclass, t0, bytes);
+}
+
+template <typename T>
+void epilogue(hgm_ctx* c, int64_t n, T* y, int epi, T a, const T* z) {
+    const int g = grid_for(n);
+    switch (epi) {
+        case EPI_ADD: k_epi<T, EPI_ADD><<<g, BS, 0, c->stream>>>(n, y, a, z); break;
+        case EPI_SUB: k_epi<T, EPI_SUB><<<g, BS, 0, c->stream>>>(n, y, a, z); break;
+        case EPI_RSUB: k_epi<T, EPI_RSUB><<<g, BS, 0, c->stream>>>(n, y, a, z); break;
+        default: return;
+    }
+    HGM_HIP(hipGetLastError());
+}
+
+template void spmv<double>(hgm_ctx*, const hgm_mat*, const double*, double*, int, double, const double*, int);
+template void spmv<float>(hgm_ctx*, const hgm_mat*, const float*, float*, int, float, const float*, int);
+template void epilogue<double>(hgm_ctx*, int64_t, double*, int, double, const double*);
+template void epilogue<float>(hgm_ctx*, int64_t, float*, int, float, const float*);
+
+}  // namespace hgm
