@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--orth", default="mgs", choices=["mgs", "cgs2"])
+    ap.add_argument("--explicit-residual", action="store_true",
+                    help="monitor norm(b - A*x) with an explicit SpMV (default: b - (A*Q) y)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP-event timing")
     ap.add_argument("--cpu-iters", type=int, default=0, help="oracle iterations for cpu_baseline (0 = maxit)")
@@ -98,7 +100,7 @@ def main():
     res = np.zeros(maxit)
     it = C.c_int(0)
     o = L.hgm_opts()
-    o.flags = L.HGM_DEVICE_PTRS
+    o.flags = L.HGM_DEVICE_PTRS | (L.HGM_EXPLICIT_RESIDUAL if args.explicit_residual else 0)
     o.orth = L.HGM_CGS2 if args.orth == "cgs2" else L.HGM_MGS
     o.H_out = None
     lib = L.load()
@@ -122,7 +124,7 @@ def main():
     for _ in range(args.warmup):
         step()
     timing = not args.no_timing
-    ctx.kernel_timing(timing)
+    ctx.kernel_timing(0x100 | 0b011 if timing else 0)   # SpMV classes only (HGM_TIMING_CLASSES)
 
     def barrier():
         if world > 1:
@@ -189,7 +191,8 @@ def main():
             "data": "synthetic (Siddon parallel-beam A generated on device, Shepp-Logan phantom, 1% noise)",
             "config": {
                 "workload": f"{args.workload}: {wl['solver']} {wl['N']}x{wl['N']} phantom, {wl['angles']} angles, "
-                            f"m={m}, n={n}, nnz(A)={A.nnz}, maxit={maxit}, tol=0, lambda={lam}, orth={args.orth}",
+                            f"m={m}, n={n}, nnz(A)={A.nnz}, maxit={maxit}, tol=0, lambda={lam}, orth={args.orth}, "
+                            f"residual={'explicit A*x' if args.explicit_residual else '(A*Q)*y'}",
                 "global_batch": world,
                 "parallelism": "replicas: one independent slice per GPU" if world > 1 else "single GPU",
                 "step": f"one complete {maxit}-iteration solve",

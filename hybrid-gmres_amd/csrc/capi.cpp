@@ -2,7 +2,10 @@
 // operator management and the solver entry points that replace the reference's
 // MATLAB functions.  Every entry point converts C++ exceptions into a status code
 // and keeps the message for hgm_last_error().
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -75,7 +78,7 @@ void Timing::clear() {
 // (first launch: start, last launch: stop); other classes use stream markers.
 void timing_begin(hgm_ctx* c, int cls, hipEvent_t* start) {
     *start = nullptr;
-    if (!c->timing.on || cls < 0 || cls >= KC_N) return;
+    if (!c->timing.on || cls < 0 || cls >= KC_N || !((c->timing.mask >> cls) & 1u)) return;
     *start = c->timing.get();
     if (cls == KC_SPMV_A || cls == KC_SPMV_B) {
         c->arm_start = *start;
@@ -154,7 +157,64 @@ void read_scalars(hgm_ctx* c, int first, int count) {
     HGM_HIP(hipStreamSynchronize(c->stream));
 }
 
-void sync(hgm_ctx* c) { HGM_HIP(hipStreamSynchronize(c->stream)); }
+void sync(hgm_ctx* c) {
+    HGM_HIP(hipStreamSynchronize(c->stream));
+    if (c->aux && c->aux != c->stream) HGM_HIP(hipStreamSynchronize(c->aux));
+}
+
+void pinned_ring(hgm_ctx* c, size_t bytes) {
+    HGM_HIP(hipStreamSynchronize(c->stream));
+    if (bytes > c->hring_bytes) {
+        if (c->hring) (void)hipHostFree(c->hring);
+        c->hring = nullptr;
+        c->hring_dev = nullptr;
+        c->hring_bytes = 0;
+        const size_t nb = bytes < 65536 ? 65536 : bytes;
+        HGM_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->hring), nb, hipHostMallocMapped | hipHostMallocCoherent));
+        void* d = nullptr;
+        HGM_HIP(hipHostGetDevicePointer(&d, c->hring, 0));
+        c->hring_dev = reinterpret_cast<double*>(d);
+        c->hring_bytes = nb;
+    }
+    std::memset(c->hring, 0, bytes);
+}
+
+void pipe_record(hgm_ctx* c) {
+    if (!c->ev_pipe) HGM_HIP(hipEventCreateWithFlags(&c->ev_pipe, hipEventDisableTiming));
+    HGM_HIP(hipEventRecord(c->ev_pipe, c->stream));
+}
+
+hipStream_t aux_stream(hgm_ctx* c) {
+    if (!c->aux) HGM_HIP(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    return c->aux;
+}
+
+void step_record(hgm_ctx* c, int k) {
+    hipEvent_t& e = c->ev_step[k & 7];
+    if (!e) HGM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HGM_HIP(hipEventRecord(e, c->stream));
+}
+
+void step_wait(hgm_ctx* c, int k) {
+    if (!c->host_stats) {
+        HGM_HIP(hipEventSynchronize(c->ev_step[k & 7]));
+        return;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    HGM_HIP(hipEventSynchronize(c->ev_step[k & 7]));
+    c->wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void pipe_wait(hgm_ctx* c) {
+    if (!c->host_stats) {
+        HGM_HIP(hipEventSynchronize(c->ev_pipe));
+        return;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    HGM_HIP(hipEventSynchronize(c->ev_pipe));
+    c->wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    c->waits += 1;
+}
 
 template <typename T>
 static void allreduce_t(hgm_ctx* c, T* dev, int64_t count, ncclDataType_t dt) {
@@ -205,7 +265,11 @@ using namespace hgm;
 
 static int ctx_init(hgm_ctx* c, int device) {
     c->device = device;
+    const char* hs = std::getenv("HGM_HOST_STATS");
+    c->host_stats = hs && hs[0] == '1';
     if (hipSetDevice(device) != hipSuccess) return HGM_E_HIP;
+    const char* pd = std::getenv("HGM_PIPE_DEPTH");
+    if (pd) c->pipe_depth = std::atoi(pd) < 1 ? 1 : (std::atoi(pd) > 6 ? 6 : std::atoi(pd));
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return HGM_E_HIP;
     if (hipMalloc(reinterpret_cast<void**>(&c->dscal), sizeof(double) * NSCAL) != hipSuccess) return HGM_E_NOMEM;
     if (hipMemset(c->dscal, 0, sizeof(double) * NSCAL) != hipSuccess) return HGM_E_HIP;
@@ -282,6 +346,9 @@ HGM_API void hgm_ctx_destroy(hgm_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->host_stats)
+        std::fprintf(stderr, "hgm host stats: %ld pipeline waits, %.3f ms blocked (%.2f us/wait)\n", c->waits,
+                     c->wait_s * 1e3, c->waits ? c->wait_s * 1e6 / c->waits : 0.0);
     if (c->nccl) ncclCommDestroy(c->nccl);
     c->timing.clear();
     for (auto e : c->timing.pool) (void)hipEventDestroy(e);
@@ -290,6 +357,14 @@ HGM_API void hgm_ctx_destroy(hgm_ctx* c) {
     if (c->hscal) (void)hipHostFree(c->hscal);
     if (c->hstage) (void)hipHostFree(c->hstage);
     if (c->hup) (void)hipHostFree(c->hup);
+    if (c->hring) (void)hipHostFree(c->hring);
+    if (c->ev_pipe) (void)hipEventDestroy(c->ev_pipe);
+    for (auto e : c->ev_step)
+        if (e) (void)hipEventDestroy(e);
+    if (c->aux) {
+        (void)hipStreamSynchronize(c->aux);
+        (void)hipStreamDestroy(c->aux);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -615,6 +690,7 @@ HGM_API int hgm_kernel_timing(hgm_ctx* c, int enable) {
         sync(c);
         c->timing.clear();
         c->timing.on = enable != 0;
+        c->timing.mask = (enable & 0x100) ? (unsigned)(enable & 0xff) : 0xffu;
     });
     return HGM_OK;
 }

@@ -49,6 +49,7 @@ enum KClass { KC_SPMV_A = 0, KC_SPMV_B = 1, KC_MGS = 2, KC_N = 3 };
 
 struct Timing {
     bool on = false;
+    unsigned mask = 0xffu;   // timed classes
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[KC_N];
     double bytes[KC_N] = {0, 0, 0};
     std::vector<hipEvent_t> pool;
@@ -73,6 +74,23 @@ struct hgm_ctx {
     size_t hstage_bytes = 0;
     double* hup = nullptr;                    // pinned upload buffer (projected-solve y)
     size_t hup_bytes = 0;
+    // pinned, device-mapped host memory the pipelined GMRES loop exchanges its per-iteration
+    // scalars through (kernels write H/Gram columns and monitors into it, read y from it)
+    double* hring = nullptr;
+    double* hring_dev = nullptr;
+    size_t hring_bytes = 0;
+    hipEvent_t ev_pipe = nullptr;
+    // second stream: GMRES reconstruction/monitors overlap the next Arnoldi step (single GPU)
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_step[8] = {};
+    int pipe_depth = 2;                       // speculative Arnoldi steps in flight (HGM_PIPE_DEPTH)
+    // prefix of workspace names while launching on `aux` (its scratch must not alias the
+    // main stream's scratch: the two run concurrently)
+    std::string ws_tag;
+    // host-side diagnostics (HGM_HOST_STATS=1): time the host spends blocked in pipe_wait
+    bool host_stats = false;
+    double wait_s = 0.0;
+    long waits = 0;
     // kernel-timing events armed for the next launch(es): recorded inside the dispatch
     // packets (hipExtLaunchKernelGGL), so they bracket kernel execution only
     hipEvent_t arm_start = nullptr, arm_stop = nullptr, cur_stop = nullptr;
@@ -80,7 +98,7 @@ struct hgm_ctx {
 
     template <typename T>
     T* buf(const std::string& name, size_t count) {
-        auto& b = ws[name];
+        auto& b = ws_tag.empty() ? ws[name] : ws[ws_tag + name];
         b.ensure(count * sizeof(T) + 256);
         return reinterpret_cast<T*>(b.p);
     }
@@ -132,8 +150,10 @@ enum Epi { EPI_NONE = 0, EPI_ADD = 1, EPI_SUB = 2, EPI_RSUB = 3 };
 
 int pick_group(int64_t rows, int64_t nnz);
 // y = epi(M x): EPI_ADD: t + a*z ; EPI_SUB: t - a*z ; EPI_RSUB: z - t  (two roundings, no FMA)
+// sumsq_out (optional, device): also *sumsq_out = sum_r y_r^2 (fused into the row kernel)
 template <typename T>
-void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, int kclass);
+void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, int kclass,
+          T* sumsq_out = nullptr);
 template <typename T>
 void epilogue(hgm_ctx* c, int64_t n, T* y, int epi, T a, const T* z);
 
@@ -149,6 +169,11 @@ void multidot(hgm_ctx* c, int64_t n, int ncols, const T* Q, int64_t ldq, const T
 // x = Q(:,0:k) y fused with *err_out = ||x - xt||^2 (local)
 template <typename T>
 void gemv_err(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T* x, const T* xt, T* err_out);
+// one-launch GMRES reconstruction: x = Q y, *err_out = ||x - xt||^2 (local) and
+// *res_out = ||b - AQ y||^2 over the m rows (AQ = A*Q(:,0:k), replicated)
+template <typename T>
+void recon(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T* x, const T* xt, T* err_out,
+           int64_t m, const T* AQ, int64_t ldaq, const T* b, T* res_out);
 
 // MGS sweep of v = Q(:,kk+1) against Q(:,0..kk); writes Hcol[0..kk+1] (device) and
 // normalises Q(:,kk+1) unless H(kk+1,kk) == 0.  dist: n-vectors sharded (scalar all-reduce
@@ -201,6 +226,33 @@ void h2d(hgm_ctx* c, void* dev, const void* host, size_t bytes);
 // another h2d_pinned before the stream has passed the previous one (one per iteration)
 void h2d_pinned(hgm_ctx* c, void* dev, const void* host, size_t bytes);
 void read_scalars(hgm_ctx* c, int first, int count);   // dscal -> hscal (sync)
+// zero-initialised pinned host ring of >= bytes (c->hring / c->hring_dev), after a
+// stream synchronisation (no kernel may still be writing the previous one)
+void pinned_ring(hgm_ctx* c, size_t bytes);
+// record c->ev_pipe on the stream / wait for it on the host
+void pipe_record(hgm_ctx* c);
+void pipe_wait(hgm_ctx* c);
+// the auxiliary stream (created on first use) and the per-step events on the main stream
+hipStream_t aux_stream(hgm_ctx* c);
+void step_record(hgm_ctx* c, int k);
+void step_wait(hgm_ctx* c, int k);
+
+// Launch subsequent work on stream s with workspace prefix tag (restored on scope exit).
+struct StreamScope {
+    hgm_ctx* c;
+    hipStream_t saved;
+    std::string saved_tag;
+    StreamScope(hgm_ctx* cc, hipStream_t s, const char* tag) : c(cc), saved(cc->stream), saved_tag(cc->ws_tag) {
+        if (s != saved) {
+            c->stream = s;
+            c->ws_tag = tag;
+        }
+    }
+    ~StreamScope() {
+        c->stream = saved;
+        c->ws_tag = saved_tag;
+    }
+};
 void sync(hgm_ctx* c);
 void timing_begin(hgm_ctx* c, int cls, hipEvent_t* start);
 void timing_end(hgm_ctx* c, int cls, hipEvent_t start, double bytes);

@@ -51,12 +51,24 @@ template <typename T, int OP>
 __global__ __launch_bounds__(1024) void k_reduce_single(int64_t n, const T* __restrict__ a,
                                                         const T* __restrict__ b, T* out) {
     __shared__ T sh[16];
-    T acc = 0;
-    for (int64_t i = threadIdx.x; i < n; i += 1024) {
-        if (OP == 0) acc += a[i] * b[i];
-        else if (OP == 1) acc += a[i] * a[i];
-        else { T d = a[i] - b[i]; acc += d * d; }
+    // four independent loads in flight per lane (the loop is latency-bound, not HBM-bound)
+    T a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    auto term = [&](int64_t i) -> T {
+        if (OP == 0) return a[i] * b[i];
+        if (OP == 1) return a[i] * a[i];
+        const T d = a[i] - b[i];
+        return d * d;
+    };
+    int64_t i = threadIdx.x;
+    for (; i + 3 * 1024 < n; i += 4 * 1024) {
+        const T t0 = term(i), t1 = term(i + 1024), t2 = term(i + 2048), t3 = term(i + 3072);
+        a0 += t0;
+        a1 += t1;
+        a2 += t2;
+        a3 += t3;
     }
+    for (; i < n; i += 1024) a0 += term(i);
+    T acc = (a0 + a1) + (a2 + a3);
     acc = wave_sum(acc);
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
     __syncthreads();
@@ -67,7 +79,7 @@ __global__ __launch_bounds__(1024) void k_reduce_single(int64_t n, const T* __re
     }
 }
 
-constexpr int64_t SINGLE_MAX = 1 << 18;   // vectors up to 256 Ki entries: one launch
+constexpr int64_t SINGLE_MAX = 1 << 15;   // vectors up to 32 Ki entries: one launch
 
 template <typename T, int OP>
 static void reduce_to(hgm_ctx* c, int64_t n, const T* a, const T* b, T* out) {
@@ -113,30 +125,148 @@ void multidot(hgm_ctx* c, int64_t n, int ncols, const T* Q, int64_t ldq, const T
     HGM_HIP(hipGetLastError());
 }
 
-// x = Q(:,0:k) y fused with the error monitor: parts[blk] = sum (x_i - xt_i)^2
-template <typename T>
-__global__ __launch_bounds__(BS) void k_gemv_err(int64_t n, int k, const T* __restrict__ Q, int64_t ldq,
-                                                 const T* __restrict__ y, T* __restrict__ x,
-                                                 const T* __restrict__ xt, T* __restrict__ parts) {
-    __shared__ T sh[4];
+// ------------------------------------------------------------------------------
+// GEMV over the Krylov basis, x = Q(:,0:k) y (MODE 0), x -= Q y (MODE 1), or MODE 0
+// fused with the error monitor (ERR: parts[blk] = sum (x_i - xt_i)^2).  y (k values,
+// possibly in pinned host memory written by the projected solve) is staged once per
+// block in LDS; every lane owns a pair of rows and keeps four column loads in flight.
+// The sum over j runs in increasing j (s = ((q0 y0 + q1 y1) + q2 y2) + ...).
+// ------------------------------------------------------------------------------
+constexpr int GEMV_KMAX = 8192;   // LDS staging of y (64 KiB of doubles)
+
+// Rows [blk*BS .. ) of a block-range [0, nblk) of the GEMV s = Q(:,0:k) y with y staged in
+// LDS (ys).  MODE 0: x = s ; MODE 1: x = x - s ; MODE 2: nothing written.  ACC: returns
+// this lane's sum of (s_i - z_i)^2 (the error monitor with z = x_true, or the residual
+// monitor norm(b - A*x)^2 with Q = A*Q, z = b).
+template <typename T, int MODE, bool ACC>
+__device__ __forceinline__ T gemv_rows(int64_t n, int k, const T* __restrict__ Q, int64_t ldq, const T* ys,
+                                       T* __restrict__ x, const T* __restrict__ z, int64_t blk, int64_t nblk) {
+    using T2 = typename V2<T>::t;
     T acc = 0;
-    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
-        T s = 0;
-        for (int j = 0; j < k; ++j) s += Q[(int64_t)j * ldq + i] * y[j];
-        x[i] = s;
-        const T d = s - xt[i];
-        acc += d * d;
+    const int64_t n2 = n >> 1;
+    const int64_t stride = nblk * BS;
+    const int64_t ld2 = ldq >> 1;
+    for (int64_t i = blk * BS + threadIdx.x; i < n2; i += stride) {
+        const T2* q2 = reinterpret_cast<const T2*>(Q) + i;
+        T s0 = 0, s1 = 0;
+        int j = 0;
+        for (; j + 4 <= k; j += 4) {
+            const T2 a = q2[(int64_t)j * ld2], b = q2[(int64_t)(j + 1) * ld2];
+            const T2 cc = q2[(int64_t)(j + 2) * ld2], d = q2[(int64_t)(j + 3) * ld2];
+            s0 += a.x * ys[j];
+            s1 += a.y * ys[j];
+            s0 += b.x * ys[j + 1];
+            s1 += b.y * ys[j + 1];
+            s0 += cc.x * ys[j + 2];
+            s1 += cc.y * ys[j + 2];
+            s0 += d.x * ys[j + 3];
+            s1 += d.y * ys[j + 3];
+        }
+        for (; j < k; ++j) {
+            const T2 a = q2[(int64_t)j * ld2];
+            s0 += a.x * ys[j];
+            s1 += a.y * ys[j];
+        }
+        if (MODE == 0) {
+            reinterpret_cast<T2*>(x)[i] = T2{s0, s1};
+        } else if (MODE == 1) {
+            T2 xv = reinterpret_cast<T2*>(x)[i];
+            xv.x = xv.x - s0;
+            xv.y = xv.y - s1;
+            reinterpret_cast<T2*>(x)[i] = xv;
+        }
+        if (ACC) {
+            const T2 t = reinterpret_cast<const T2*>(z)[i];
+            const T d0 = s0 - t.x, d1 = s1 - t.y;
+            acc += d0 * d0;
+            acc += d1 * d1;
+        }
     }
+    if ((n & 1) && blk == nblk - 1 && threadIdx.x == 0) {
+        const int64_t i = n - 1;
+        T s = 0;
+        for (int j = 0; j < k; ++j) s += Q[(int64_t)j * ldq + i] * ys[j];
+        if (MODE == 0) x[i] = s;
+        else if (MODE == 1) x[i] = x[i] - s;
+        if (ACC) { const T d = s - z[i]; acc += d * d; }
+    }
+    return acc;
+}
+
+template <typename T>
+__device__ __forceinline__ T* stage_y(const T* __restrict__ y, int k) {
+    extern __shared__ unsigned char gemv_smem[];
+    T* ys = reinterpret_cast<T*>(gemv_smem);
+    for (int j = threadIdx.x; j < k; j += BS) ys[j] = y[j];
+    __syncthreads();
+    return ys;
+}
+
+template <typename T, int MODE, bool ERR>
+__global__ __launch_bounds__(BS) void k_gemv2(int64_t n, int k, const T* __restrict__ Q, int64_t ldq,
+                                              const T* __restrict__ y, T* __restrict__ x,
+                                              const T* __restrict__ xt, T* __restrict__ parts) {
+    __shared__ T sh[4];
+    const T* ys = stage_y(y, k);
+    const T acc = gemv_rows<T, MODE, ERR>(n, k, Q, ldq, ys, x, xt, blockIdx.x, gridDim.x);
+    if (ERR) {
+        const T tot = block_sum_all(acc, sh);
+        if (threadIdx.x == 0) parts[blockIdx.x] = tot;
+    }
+}
+
+// GMRES reconstruction of iteration k in one launch (n-space side): blocks [0, nbx)
+// compute x = Q(:,0:k) y with the error monitor sum (x - x_true)^2; blocks [nbx, grid)
+// the residual monitor sum (b - AQ(:,0:k) y)^2 over the m rows (A*x = (A*Q) y: the
+// columns A*Q(:,j) are the operator's own products, kept from the Arnoldi steps).
+template <typename T>
+__global__ __launch_bounds__(BS) void k_recon(int64_t n, int k, const T* __restrict__ Q, int64_t ldq,
+                                              const T* __restrict__ y, T* __restrict__ x, const T* __restrict__ xt,
+                                              int64_t m, const T* __restrict__ AQ, int64_t ldaq,
+                                              const T* __restrict__ b, T* __restrict__ parts, int nbx) {
+    __shared__ T sh[4];
+    const T* ys = stage_y(y, k);
+    T acc;
+    if ((int)blockIdx.x < nbx) acc = gemv_rows<T, 0, true>(n, k, Q, ldq, ys, x, xt, blockIdx.x, nbx);
+    else acc = gemv_rows<T, 2, true>(m, k, AQ, ldaq, ys, nullptr, b, blockIdx.x - nbx, gridDim.x - nbx);
     const T tot = block_sum_all(acc, sh);
     if (threadIdx.x == 0) parts[blockIdx.x] = tot;
 }
 
+// block 0: out0 = sum parts[0, n0) ; block 1: out1 = sum parts[n0, n0 + n1)
+template <typename T>
+__global__ __launch_bounds__(BS) void k_finalize2(const T* __restrict__ parts, int n0, int n1, T* out0, T* out1) {
+    __shared__ T sh[4];
+    const T r = blockIdx.x == 0 ? reduce_parts(parts, n0, sh) : reduce_parts(parts + n0, n1, sh);
+    if (threadIdx.x == 0) *(blockIdx.x == 0 ? out0 : out1) = r;
+}
+
+static int gemv_blocks(int64_t n) {
+    int64_t nb = ((n >> 1) + BS - 1) / BS;   // one row pair per lane ...
+    if (nb > MAX_PARTS) nb = MAX_PARTS;      // ... up to 1024 blocks, then grid-stride
+    if (nb < 1) nb = 1;
+    return (int)nb;
+}
+
 template <typename T>
 void gemv_err(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T* x, const T* xt, T* err_out) {
-    const int np = parts_for(n);
+    HGM_REQUIRE(k <= GEMV_KMAX && ldq % 2 == 0, "gemv: k too large");
+    const int np = gemv_blocks(n);
     T* parts = c->buf<T>("gemv_parts", MAX_PARTS);
-    k_gemv_err<T><<<np, BS, 0, c->stream>>>(n, k, Q, ldq, y, x, xt, parts);
+    k_gemv2<T, 0, true><<<np, BS, sizeof(T) * (k > 0 ? k : 1), c->stream>>>(n, k, Q, ldq, y, x, xt, parts);
     k_finalize<T><<<1, BS, 0, c->stream>>>(parts, np, err_out);
+    HGM_HIP(hipGetLastError());
+}
+
+template <typename T>
+void recon(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T* x, const T* xt, T* err_out,
+           int64_t m, const T* AQ, int64_t ldaq, const T* b, T* res_out) {
+    HGM_REQUIRE(k <= GEMV_KMAX && ldq % 2 == 0 && ldaq % 2 == 0, "recon: k too large");
+    const int nbx = gemv_blocks(n), nbr = gemv_blocks(m);
+    T* parts = c->buf<T>("recon_parts", 2 * MAX_PARTS);
+    k_recon<T><<<nbx + nbr, BS, sizeof(T) * (k > 0 ? k : 1), c->stream>>>(n, k, Q, ldq, y, x, xt, m, AQ, ldaq, b,
+                                                                          parts, nbx);
+    k_finalize2<T><<<2, BS, 0, c->stream>>>(parts, nbx, nbr, err_out, res_out);
     HGM_HIP(hipGetLastError());
 }
 
@@ -176,19 +306,28 @@ __global__ __launch_bounds__(BS) void k_mgs_pass(int64_t n, const T* __restrict_
                                                  const T* hsrc, T* hdst, T* __restrict__ pout) {
     using T2 = typename V2<T>::t;
     __shared__ T sh[4];
+    const int64_t n2 = n >> 1;
+    const int64_t stride = (int64_t)gridDim.x * BS;
+    T2* v2 = reinterpret_cast<T2*>(v);
+    const T2* qa2 = reinterpret_cast<const T2*>(qa);
+    const T2* qd2 = reinterpret_cast<const T2*>(qd);
+    // The first pair's loads do not depend on h: issue them before the re-reduction of
+    // the previous pass's partials so the two latencies overlap.
+    int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x;
+    T2 vv{0, 0}, qq{0, 0}, dd{0, 0};
+    if (i < n2) {
+        vv = v2[i];
+        if (MODE != 0) qq = qa2[i];
+        if (MODE != 2) dd = qd2[i];
+    }
     T h = 0;
     if (MODE != 0) {
         h = (np_in > 0) ? reduce_parts(pin, np_in, sh) : *hsrc;
         if (hdst != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *hdst = h;
     }
     T acc0 = 0, acc1 = 0;
-    const int64_t n2 = n >> 1;
-    const int64_t stride = (int64_t)gridDim.x * BS;
-    T2* v2 = reinterpret_cast<T2*>(v);
-    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n2; i += stride) {
-        T2 vv = v2[i];
+    while (i < n2) {
         if (MODE != 0) {
-            const T2 qq = reinterpret_cast<const T2*>(qa)[i];
             const T p0 = h * qq.x, p1 = h * qq.y;
             vv.x = vv.x - p0;
             vv.y = vv.y - p1;
@@ -198,9 +337,14 @@ __global__ __launch_bounds__(BS) void k_mgs_pass(int64_t n, const T* __restrict_
             acc0 += vv.x * vv.x;
             acc1 += vv.y * vv.y;
         } else {
-            const T2 dd = reinterpret_cast<const T2*>(qd)[i];
             acc0 += dd.x * vv.x;
             acc1 += dd.y * vv.y;
+        }
+        i += stride;
+        if (i < n2) {
+            vv = v2[i];
+            if (MODE != 0) qq = qa2[i];
+            if (MODE != 2) dd = qd2[i];
         }
     }
     if ((n & 1) && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
@@ -224,17 +368,21 @@ __global__ __launch_bounds__(BS) void k_mgs_normalize(int64_t n, T* __restrict__
                                                       const T* ssrc, T* hdst) {
     using T2 = typename V2<T>::t;
     __shared__ T sh[4];
+    const int64_t n2 = n >> 1;
+    T2* v2 = reinterpret_cast<T2*>(v);
+    int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x;
+    T2 vv{0, 0};
+    if (i < n2) vv = v2[i];                       // overlaps the partial re-reduction
     const T ss = (np_in > 0) ? reduce_parts(pin, np_in, sh) : *ssrc;
     const T nrm = sqrt(ss);
     if (blockIdx.x == 0 && threadIdx.x == 0) *hdst = nrm;
     if (nrm == 0) return;
-    const int64_t n2 = n >> 1;
-    T2* v2 = reinterpret_cast<T2*>(v);
-    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n2; i += (int64_t)gridDim.x * BS) {
-        T2 vv = v2[i];
+    while (i < n2) {
         vv.x = vv.x / nrm;
         vv.y = vv.y / nrm;
         v2[i] = vv;
+        i += (int64_t)gridDim.x * BS;
+        if (i < n2) vv = v2[i];
     }
     if ((n & 1) && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) v[n - 1] = v[n - 1] / nrm;
 }
@@ -243,7 +391,11 @@ template <typename T>
 void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist) {
     hipEvent_t t0 = nullptr;
     timing_begin(c, KC_MGS, &t0);
-    const int np = parts_for(n);
+    const double s = sizeof(T);
+    // One launch per pass: a dependent launch is the cheapest grid-wide exchange of the
+    // block partials on gfx950 (2.6-2.9 us vs 3-25 us for in-kernel grid barriers,
+    // scripts/barrier_bench.hip).
+    const int np = gemv_blocks(n);
     T* P = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
     T* Pb[2] = {P, P + MAX_PARTS};
     T* v = Q + (int64_t)(kk + 1) * ldq;
@@ -282,32 +434,17 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist) {
     }
     HGM_HIP(hipGetLastError());
     // algorithmic bytes: (32k+24)n-style count for k+1 = kk+1 columns
-    const double s = sizeof(T);
     const double bytes = s * n * (2.0 + 4.0 * kk + 3.0 + 2.0);
     timing_end(c, KC_MGS, t0, bytes);
 }
 
-// ------------------------------------------------------------------------------
-// GEMV over the Krylov basis: x = Q(:,0:k) y  or  x -= Q y
-// ------------------------------------------------------------------------------
-template <typename T, int MODE>
-__global__ __launch_bounds__(BS) void k_gemv(int64_t n, int k, const T* __restrict__ Q, int64_t ldq,
-                                             const T* __restrict__ y, T* __restrict__ x) {
-    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
-        T s = 0;
-        for (int j = 0; j < k; ++j) s += Q[(int64_t)j * ldq + i] * y[j];
-        if (MODE == 0) x[i] = s;
-        else x[i] = x[i] - s;
-    }
-}
-
 template <typename T>
 void gemv(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T* x, int mode) {
-    int64_t nb = (n + BS - 1) / BS;
-    if (nb > 8192) nb = 8192;
-    if (nb < 1) nb = 1;
-    if (mode == 0) k_gemv<T, 0><<<nb, BS, 0, c->stream>>>(n, k, Q, ldq, y, x);
-    else k_gemv<T, 1><<<nb, BS, 0, c->stream>>>(n, k, Q, ldq, y, x);
+    HGM_REQUIRE(k <= GEMV_KMAX && ldq % 2 == 0, "gemv: k too large");
+    const int nb = gemv_blocks(n);
+    const size_t sm = sizeof(T) * (k > 0 ? k : 1);
+    if (mode == 0) k_gemv2<T, 0, false><<<nb, BS, sm, c->stream>>>(n, k, Q, ldq, y, x, nullptr, nullptr);
+    else k_gemv2<T, 1, false><<<nb, BS, sm, c->stream>>>(n, k, Q, ldq, y, x, nullptr, nullptr);
     HGM_HIP(hipGetLastError());
 }
 
@@ -431,6 +568,8 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
     template void sumsq_diff<T>(hgm_ctx*, int64_t, const T*, const T*, T*);                    \
     template void multidot<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, const T*); \
     template void gemv_err<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, const T*, T*); \
+    template void recon<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, const T*, T*, int64_t, \
+                           const T*, int64_t, const T*, T*);                                   \
     template void mgs<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool);                       \
     template void cgs2<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool);                      \
     template void gemv<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, int);       \

@@ -9,7 +9,9 @@
 // (A_g = A(:,P_g), B_g = B(P_g,:)); every `A*v` is followed by an all-reduce of the
 // m-vector, every inner product of n-vectors by a scalar all-reduce; m-vectors
 // (b, u, the AB-side Krylov basis, A*Q columns) are replicated.
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <limits>
 #include <type_traits>
@@ -150,6 +152,9 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     HGM_REQUIRE(B != nullptr, "B is NULL");
     HGM_REQUIRE(b_in != nullptr && xt_in != nullptr, "b and x_true are required");
     HGM_REQUIRE(A->dtype == HGM_F64, "GMRES family is fp64 (the reference's precision)");
+    const auto t_start = std::chrono::steady_clock::now();
+    const double wait0 = c->wait_s;
+    const long waits0 = c->waits;
     HGM_REQUIRE(maxit >= 1, "maxit must be >= 1");
     using T = double;
     const bool dev = o && (o->flags & HGM_DEVICE_PTRS);
@@ -164,16 +169,37 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     const T* b = stage_in<T>(c, "in_b", b_in, m, dev);
     const T* xt = stage_in<T>(c, "in_xt", xt_in, n, dev);
     T* Q = c->buf<T>("Q", (size_t)ldq * (maxit + 1));
-    T* Hd = c->buf<T>("H", (size_t)(maxit + 1) * maxit);
     T* x = c->buf<T>("x", n > 0 ? n : 1);
     T* t = c->buf<T>("t_m", m > 0 ? m : 1);        // m-vector scratch (A*q, residual)
     T* tn = c->buf<T>("t_n", n > 0 ? n : 1);       // n-vector scratch (AB side: B*q)
     T* z = c->buf<T>("z_m", m > 0 ? m : 1);        // AB side: z = Q*y
-    T* yd = c->buf<T>("y", maxit + 8);
+    T* tr = c->buf<T>("t_res", m > 0 ? m : 1);     // m-vector of the residual monitor (aux stream)
     const int64_t ldaq = round_up(m > 0 ? m : 1, 64);
-    T* AQ = sp.proj == PROJ_ABRTP ? c->buf<T>("AQ", (size_t)ldaq * maxit) : nullptr;
-    T* gcol = c->buf<T>("gcol", maxit + 8);
-    HGM_HIP(hipMemsetAsync(Hd, 0, sizeof(T) * (maxit + 1) * maxit, st));
+    // n-space side: keep the operator's products A*Q(:,j) (the RTP Gram matrix needs them,
+    // and the residual monitor b - A*x = b - (A*Q) y reuses them instead of another SpMV)
+    const bool aq_res = nspace && !(o && (o->flags & HGM_EXPLICIT_RESIDUAL));
+    T* AQ = (sp.proj == PROJ_ABRTP || aq_res) ? c->buf<T>("AQ", (size_t)ldaq * maxit) : nullptr;
+    // Per-iteration exchange ring in pinned host memory: slot k holds
+    // [H(:,k) | Gram column k, AQk'b] (LH doubles), the monitors [res^2, err^2] of
+    // iteration k, and the projected solution y_k.  Single GPU: the kernels write the
+    // slots in place and read y from it (zero-copy, no copy kernels).  Multi-GPU: the
+    // all-reduced scalars live in a device mirror and each slot is copied out once.
+    const size_t LH = 2 * (size_t)(maxit + 2);
+    const size_t offM = (size_t)maxit * LH, offY = offM + 2 * (size_t)maxit;
+    const size_t ring_n = offY + (size_t)maxit * maxit;
+    const bool zc = !dist_n(c);
+    // single GPU: reconstructions run on the auxiliary stream, concurrently with the
+    // Arnoldi steps (multi-GPU keeps one stream: the communicator's collectives must be
+    // issued in one order)
+    hipStream_t rs_stream = zc ? aux_stream(c) : st;
+    if (zc) HGM_HIP(hipStreamSynchronize(rs_stream));
+    pinned_ring(c, sizeof(double) * ring_n);
+    const double* hr = c->hring;
+    T* dr = zc ? c->hring_dev : c->buf<T>("ring_dev", ring_n);
+    auto publish = [&](size_t off, size_t cnt) {
+        if (!zc)
+            HGM_HIP(hipMemcpyAsync(c->hring + off, dr + off, sizeof(T) * cnt, hipMemcpyDeviceToHost, c->stream));
+    };
     fill<T>(c, n, x, T(0));
 
     std::vector<double> H((size_t)(maxit + 1) * maxit, 0.0);
@@ -203,12 +229,13 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     int k = 0;
     std::vector<double> y, rhs, M;
     std::vector<double> G((size_t)maxit * maxit, 0.0), cvec(maxit, 0.0);
-    for (k = 0; k < maxit; ++k) {
-        T* qk = Q + (int64_t)k * ldq;
-        T* v = Q + (int64_t)(k + 1) * ldq;
+    // Enqueue Arnoldi step kq: operator application + orthogonalisation (+ Gram column).
+    auto enqueue_step = [&](int kq) {
+        T* qk = Q + (int64_t)kq * ldq;
+        T* v = Q + (int64_t)(kq + 1) * ldq;
         // ---- operator (hybrid_*_rtp.m:19 ; *_bounds.m:25) ----
         if (nspace) {
-            T* Aq = AQ ? AQ + (int64_t)k * ldaq : t;
+            T* Aq = AQ ? AQ + (int64_t)kq * ldaq : t;
             apply_A<T>(c, A, qk, Aq, EPI_NONE, T(0), nullptr);
             if (sp.lambda_in_op) apply_B<T>(c, B, Aq, v, EPI_ADD, T(lambda), qk);   // B*(A*v) + lambda*v
             else apply_B<T>(c, B, Aq, v, EPI_NONE, T(0), nullptr);                  // B*(A*v)
@@ -217,20 +244,91 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             apply_A<T>(c, A, tn, v, EPI_NONE, T(0), nullptr);                       // A*(B*Q(:,k))
         }
         // ---- orthogonalisation (hybrid_*_rtp.m:20-26) ----
-        T* Hcol = Hd + (int64_t)k * (maxit + 1);
-        if (orth == HGM_CGS2) cgs2<T>(c, dim, Q, ldq, k, Hcol, dist);
-        else mgs<T>(c, dim, Q, ldq, k, Hcol, dist);
-        Reader rd(c);
-        rd.add(&Hh(0, k), Hcol, sizeof(T) * (k + 2));
+        T* Hcol = dr + (size_t)kq * LH;                  // -> host H(:,k)
+        if (orth == HGM_CGS2) cgs2<T>(c, dim, Q, ldq, kq, Hcol, dist);
+        else mgs<T>(c, dim, Q, ldq, kq, Hcol, dist);
         if (sp.proj == PROJ_ABRTP) {
             // column k of AQk'*AQk and AQk'*b (hybrid_ab_gmres_rtp.m:31-32); A*Q(:,j) was
             // computed inside M_reg_op(Q(:,j)) at :19 — the same deterministic SpMV.
-            multidot<T>(c, m, k + 1, AQ, ldaq, AQ + (int64_t)k * ldaq, gcol, b);   // + gcol[k+1] = b'*AQ(:,k)
-            rd.add(&G[(size_t)k * maxit], gcol, sizeof(T) * (k + 1));
-            rd.add(&cvec[k], gcol + k + 1, sizeof(T));
+            multidot<T>(c, m, kq + 1, AQ, ldaq, AQ + (int64_t)kq * ldaq, Hcol + (maxit + 2), b);   // + b'*AQ(:,k)
         }
-        rd.go();
-        if (Hh(k + 1, k) == 0) break;                    // :25  if H(k+1,k) == 0, break
+        publish((size_t)kq * LH, LH);
+        step_record(c, kq);
+    };
+    // Reconstruction + monitors of iteration kq from y_kq (in the ring) on the auxiliary
+    // stream, then the event the host waits on.  Everything it reads (Q(:,0..kq), y_kq)
+    // is complete when it is enqueued (the host has seen step kq finish), so it needs no
+    // stream dependency; it writes only x, its own scratch and ring slot kq.
+    auto enqueue_recon = [&](int kq) {
+        StreamScope scope(c, rs_stream, "aux:");
+        const int kk = kq + 1;
+        const T* yk = c->hring_dev + offY + (size_t)kq * maxit;
+        T* rslot = dr + offM + 2 * (size_t)kq;
+        T* eslot = rslot + 1;
+        // ---- reconstruction (hybrid_*_rtp.m:30/33 ; *_bounds.m:37-38) ----
+        if (aq_res) {
+            // x = Q(:,1:k)*yk with ||x - x_true||^2 (:33/:36) and ||b - A*x||^2 (:32/:35)
+            // evaluated as ||b - (A*Q(:,1:k))*yk||^2, all in one launch (+ finalize)
+            recon<T>(c, n, kk, Q, ldq, yk, x, xt, eslot, m, AQ, ldaq, b, rslot);
+            if (dist_n(c)) allreduce(c, eslot, 1);
+            publish(offM + 2 * (size_t)kq, 2);
+            pipe_record(c);
+            return;
+        }
+        if (nspace) {
+            // x = Q(:,1:k)*yk, fused with the error monitor ||x - x_true||^2 (:33 / :36)
+            gemv_err<T>(c, n, kk, Q, ldq, yk, x, xt, eslot);
+            if (dist_n(c)) allreduce(c, eslot, 1);
+        } else {
+            gemv<T>(c, m, kk, Q, ldq, yk, z, 0);                 // zk = Q(:,1:k)*yk
+            apply_B<T>(c, B, z, x, EPI_NONE, T(0), nullptr);     // xk = B*zk
+            nsumsq_diff<T>(c, n, x, xt, eslot);
+        }
+        // ---- monitors (hybrid_*_rtp.m:32-33 / :35-36): norm(b - A*x) ----
+        if (!dist_n(c)) {
+            spmv<T>(c, A, x, tr, EPI_RSUB, T(0), b, KC_SPMV_A, rslot);   // sum of squares fused
+        } else {
+            apply_A<T>(c, A, x, tr, EPI_RSUB, T(0), b);
+            sumsq<T>(c, m, tr, rslot);
+        }
+        publish(offM + 2 * (size_t)kq, 2);
+        pipe_record(c);
+    };
+    // Software pipeline over two streams, L = ctx->pipe_depth:
+    //     main: S0 S1 S2 S3 ...          (S_k: Arnoldi step k -> H(:,k), Q(:,k+1))
+    //     aux :       R0 R1 R2 ...       (R_k: x = Q y_k, monitors of iteration k)
+    // At iteration k the host waits for S_k and R_{k-1}, solves for y_k, enqueues R_k
+    // and then S_{k+L+1}; the GPU meanwhile runs S_{k+1..k+L} and overlaps R_k with
+    // them, so it never waits for the host.  When `residual_norm(k) <= tol` stops the loop the
+    // speculative steps are discarded: they write only Q(:,>k+1), AQ(:,>k), their own
+    // ring slots and scratch — never x or a history — so every output equals the
+    // reference's.  (Multi-GPU: both sequences share one stream, same semantics.)
+    const int L = c->pipe_depth;                         // speculative steps in flight
+    for (int j = 0; j <= L && j < maxit; ++j) enqueue_step(j);
+    bool done = false;
+    for (k = 0; k < maxit; ++k) {
+        if (k >= 1) pipe_wait(c);                        // R_{k-1}
+        step_wait(c, k);                                 // S_k: H(:,k) (+ Gram column k)
+        if (k >= 1) {
+            const double* mk = hr + offM + 2 * (size_t)(k - 1);
+            res[k - 1] = std::sqrt(mk[0]) / nb;
+            err[k - 1] = std::sqrt(mk[1]) / nxt;
+            if (res[k - 1] <= tol) {                     // :35 / :38 / *_bounds :79-83
+                k = k - 1;
+                done = true;
+                break;
+            }
+        }
+        const double* hk = hr + (size_t)k * LH;
+        for (int i = 0; i < k + 2; ++i) Hh(i, k) = hk[i];
+        if (sp.proj == PROJ_ABRTP) {
+            for (int i = 0; i <= k; ++i) G[(size_t)k * maxit + i] = hk[(maxit + 2) + i];
+            cvec[k] = hk[(maxit + 2) + k + 1];
+        }
+        if (Hh(k + 1, k) == 0) {                         // :25  if H(k+1,k) == 0, break
+            done = true;
+            break;
+        }
         const int kk = k + 1;                            // MATLAB k
         y.assign(kk, 0.0);
         if (sp.proj == PROJ_LS) {
@@ -265,30 +363,29 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             for (int i = 0; i < kk; ++i) M[(size_t)i * kk + i] += lambda;
             dense::mldivide_square(kk, M.data(), cvec.data(), y.data());
         }
-        h2d_pinned(c, yd, y.data(), sizeof(double) * kk);
-        // ---- reconstruction (hybrid_*_rtp.m:30/33 ; *_bounds.m:37-38) ----
-        if (nspace) {
-            // x = Q(:,1:k)*yk, fused with the error monitor ||x - x_true||^2 (:33 / :36)
-            gemv_err<T>(c, n, kk, Q, ldq, yd, x, xt, dslot<T>(c, S_ERR));
-            if (dist_n(c)) allreduce(c, dslot<T>(c, S_ERR), 1);
-        } else {
-            gemv<T>(c, m, kk, Q, ldq, yd, z, 0);                 // zk = Q(:,1:k)*yk
-            apply_B<T>(c, B, z, x, EPI_NONE, T(0), nullptr);     // xk = B*zk
-            nsumsq_diff<T>(c, n, x, xt, dslot<T>(c, S_ERR));
-        }
+        std::memcpy(c->hring + offY + (size_t)k * maxit, y.data(), sizeof(double) * kk);
+        enqueue_recon(k);
         x_assigned = true;
-        // ---- monitors (hybrid_*_rtp.m:32-33 / :35-36) ----
-        apply_A<T>(c, A, x, t, EPI_RSUB, T(0), b);              // b - A*x
-        sumsq<T>(c, m, t, dslot<T>(c, S_RES));
-        read_scalars(c, S_RES, 2);
-        res[k] = std::sqrt(c->hscal[S_RES]) / nb;
-        err[k] = std::sqrt(c->hscal[S_ERR]) / nxt;
-        if (res[k] <= tol) break;                        // :35 / :38 / *_bounds :79-83
+        if (k + L + 1 < maxit) enqueue_step(k + L + 1);  // speculative, see above
+    }
+    if (!done) {
+        // all maxit iterations ran: the last monitors are still outstanding
+        pipe_wait(c);
+        k = maxit - 1;
+        const double* mk = hr + offM + 2 * (size_t)k;
+        res[k] = std::sqrt(mk[0]) / nb;
+        err[k] = std::sqrt(mk[1]) / nxt;
     }
     if (k == maxit) k = maxit - 1;
     const int nit = k + 1;                               // niters = k
+    if (rs_stream != st) HGM_HIP(hipStreamSynchronize(rs_stream));
     if (!x_assigned) throw Error{HGM_E_NOT_ASSIGNED, "Output argument \"x\" not assigned during call (breakdown at k = 1)"};
     stage_out<T>(c, x_out, x, n, dev);
+    if (c->host_stats) {
+        const double tot = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+        std::fprintf(stderr, "hgm gmres: %d iters, %.1f us total, %.1f us blocked in %ld waits\n", nit, tot * 1e6,
+                     (c->wait_s - wait0) * 1e6, c->waits - waits0);
+    }
     if (err_out) std::memcpy(err_out, err.data(), sizeof(double) * nit);
     if (res_out) std::memcpy(res_out, res.data(), sizeof(double) * nit);
     if (niters) *niters = nit;

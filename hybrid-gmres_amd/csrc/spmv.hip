@@ -75,11 +75,14 @@ __device__ __forceinline__ T seg_partial(int64_t s, int64_t e, int gl, const int
     return (a0 + a1) + (a2 + a3);
 }
 
-template <typename T, int G, int EPI, bool VEC, bool NT>
+// NRM: also write the block's sum of y_r^2 (rows in increasing order) to nparts[blk] —
+// the residual monitor norm(b - A*x) (hybrid_*_rtp.m:32/35) without re-reading y.
+template <typename T, int G, int EPI, bool VEC, bool NT, bool NRM = false>
 __global__ __launch_bounds__(BS) void k_spmv(int64_t rows, const int64_t* __restrict__ rp,
                                              const int32_t* __restrict__ ci,
                                              const T* __restrict__ val, const T* __restrict__ x,
-                                             T* __restrict__ y, T a, const T* __restrict__ z, int xcd) {
+                                             T* __restrict__ y, T a, const T* __restrict__ z, int xcd,
+                                             T* __restrict__ nparts) {
     constexpr int RPB = BS / G;
     const int64_t blk = xcd ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
     const int64_t row = blk * RPB + threadIdx.x / G;
@@ -87,7 +90,31 @@ __global__ __launch_bounds__(BS) void k_spmv(int64_t rows, const int64_t* __rest
     T acc = 0;
     if (row < rows) acc = seg_partial<T, G, VEC, NT>(rp[row], rp[row + 1], gl, ci, val, x);
     acc = group_sum<T, G>(acc);
-    if (gl == 0 && row < rows) y[row] = apply_epi<T, EPI>(acc, a, z, row);
+    T r = 0;
+    if (gl == 0 && row < rows) {
+        r = apply_epi<T, EPI>(acc, a, z, row);
+        y[row] = r;
+    }
+    if (NRM) {
+        __shared__ T rs[RPB];
+        if (gl == 0) rs[threadIdx.x / G] = r * r;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            T s = 0;
+            for (int j = 0; j < RPB; ++j) s += rs[j];
+            nparts[blk] = s;
+        }
+    }
+}
+
+// fixed-order sum of np partials by one block
+template <typename T>
+__global__ __launch_bounds__(BS) void k_sum_parts(const T* __restrict__ parts, int64_t np, T* out) {
+    __shared__ T sh[4];
+    T a = 0;
+    for (int64_t i = threadIdx.x; i < np; i += BS) a += parts[i];
+    const T r = block_sum_all(a, sh);
+    if (threadIdx.x == 0) *out = r;
 }
 
 // Column-banded SpMV: work items (band b, block of RPB rows) in band-major order, grid-
@@ -287,17 +314,44 @@ static void launch_spmv_v(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int ep
     const T* val = reinterpret_cast<const T*>(M->val);
     const int xcd = (M->variant & SPMV_XCD) ? 1 : 0;
     const dim3 g((unsigned)nb), b(BS);
+    T* np_ = nullptr;
     switch (epi) {
-        case EPI_NONE: launch(c, true, k_spmv<T, G, EPI_NONE, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd); break;
-        case EPI_ADD: launch(c, true, k_spmv<T, G, EPI_ADD, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd); break;
-        case EPI_SUB: launch(c, true, k_spmv<T, G, EPI_SUB, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd); break;
-        default: launch(c, true, k_spmv<T, G, EPI_RSUB, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd); break;
+        case EPI_NONE: launch(c, true, k_spmv<T, G, EPI_NONE, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, np_); break;
+        case EPI_ADD: launch(c, true, k_spmv<T, G, EPI_ADD, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, np_); break;
+        case EPI_SUB: launch(c, true, k_spmv<T, G, EPI_SUB, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, np_); break;
+        default: launch(c, true, k_spmv<T, G, EPI_RSUB, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, np_); break;
     }
 }
 
+// row kernel with the fused sum of squares of the output (EPI_SUB / EPI_RSUB)
+template <typename T, int G, bool VEC, bool NT>
+static void launch_spmv_nrm_v(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, T* out) {
+    const int64_t nb = (M->rows + (BS / G) - 1) / (BS / G);
+    if (nb == 0) {
+        HGM_HIP(hipMemsetAsync(out, 0, sizeof(T), c->stream));
+        return;
+    }
+    const T* val = reinterpret_cast<const T*>(M->val);
+    const int xcd = (M->variant & SPMV_XCD) ? 1 : 0;
+    T* parts = c->buf<T>("spmv_nparts", nb + 1);
+    const dim3 g((unsigned)nb), b(BS);
+    if (epi == EPI_SUB)
+        launch(c, true, k_spmv<T, G, EPI_SUB, VEC, NT, true>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, parts);
+    else
+        launch(c, true, k_spmv<T, G, EPI_RSUB, VEC, NT, true>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, parts);
+    hipLaunchKernelGGL(k_sum_parts<T>, dim3(1), dim3(BS), 0, c->stream, (const T*)parts, nb, out);
+}
+
 template <typename T, int G>
-static void launch_spmv_g(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
+static void launch_spmv_g(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, T* nrm = nullptr) {
     const bool vec = M->variant & SPMV_VEC, nt = M->variant & SPMV_NT;
+    if (nrm) {
+        if (vec && nt) launch_spmv_nrm_v<T, G, true, true>(c, M, x, y, epi, a, z, nrm);
+        else if (vec) launch_spmv_nrm_v<T, G, true, false>(c, M, x, y, epi, a, z, nrm);
+        else if (nt) launch_spmv_nrm_v<T, G, false, true>(c, M, x, y, epi, a, z, nrm);
+        else launch_spmv_nrm_v<T, G, false, false>(c, M, x, y, epi, a, z, nrm);
+        return;
+    }
     if (vec && nt) launch_spmv_v<T, G, true, true>(c, M, x, y, epi, a, z);
     else if (vec) launch_spmv_v<T, G, true, false>(c, M, x, y, epi, a, z);
     else if (nt) launch_spmv_v<T, G, false, true>(c, M, x, y, epi, a, z);
@@ -368,22 +422,27 @@ static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int ep
 }
 
 template <typename T>
-void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, int kclass) {
+void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, int kclass, T* sumsq_out) {
     hipEvent_t t0 = nullptr;
     timing_begin(c, kclass, &t0);
-    if ((M->variant & SPMV_STREAM) && (M->nbands > 1 ? M->bcfo != nullptr : M->cfo != nullptr)) {
+    const bool stream = (M->variant & SPMV_STREAM) && (M->nbands > 1 ? M->bcfo != nullptr : M->cfo != nullptr);
+    const bool rowk = !stream && M->nbands <= 1;
+    T* nrm = (rowk && (epi == EPI_SUB || epi == EPI_RSUB)) ? sumsq_out : nullptr;
+    if (stream) {
         spmv_streamed<T>(c, M, x, y, epi, a, z);
     } else if (M->nbands > 1) {
         spmv_banded<T>(c, M, x, y, epi, a, z);
     } else {
         switch (M->group) {
-            case 64: launch_spmv_g<T, 64>(c, M, x, y, epi, a, z); break;
-            case 32: launch_spmv_g<T, 32>(c, M, x, y, epi, a, z); break;
-            case 16: launch_spmv_g<T, 16>(c, M, x, y, epi, a, z); break;
-            case 8: launch_spmv_g<T, 8>(c, M, x, y, epi, a, z); break;
-            default: launch_spmv_g<T, 4>(c, M, x, y, epi, a, z); break;
+            case 64: launch_spmv_g<T, 64>(c, M, x, y, epi, a, z, nrm); break;
+            case 32: launch_spmv_g<T, 32>(c, M, x, y, epi, a, z, nrm); break;
+            case 16: launch_spmv_g<T, 16>(c, M, x, y, epi, a, z, nrm); break;
+            case 8: launch_spmv_g<T, 8>(c, M, x, y, epi, a, z, nrm); break;
+            default: launch_spmv_g<T, 4>(c, M, x, y, epi, a, z, nrm); break;
         }
     }
+    // other kernels: separate fixed-order reduction of the output
+    if (sumsq_out && !nrm) sumsq<T>(c, M->rows, y, sumsq_out);
     HGM_HIP(hipGetLastError());
     // algorithmic bytes: nnz*(s+4) + 8(rows+1) + s*cols + s*rows (+ s*rows epilogue operand)
     const double s = sizeof(T);
@@ -404,8 +463,8 @@ void epilogue(hgm_ctx* c, int64_t n, T* y, int epi, T a, const T* z) {
     HGM_HIP(hipGetLastError());
 }
 
-template void spmv<double>(hgm_ctx*, const hgm_mat*, const double*, double*, int, double, const double*, int);
-template void spmv<float>(hgm_ctx*, const hgm_mat*, const float*, float*, int, float, const float*, int);
+template void spmv<double>(hgm_ctx*, const hgm_mat*, const double*, double*, int, double, const double*, int, double*);
+template void spmv<float>(hgm_ctx*, const hgm_mat*, const float*, float*, int, float, const float*, int, float*);
 template void epilogue<double>(hgm_ctx*, int64_t, double*, int, double, const double*);
 template void epilogue<float>(hgm_ctx*, int64_t, float*, int, float, const float*);
 

@@ -22,6 +22,7 @@ HGM_F64, HGM_F32 = 0, 1
 HGM_MGS, HGM_CGS2 = 0, 1
 HGM_SIDE_AB, HGM_SIDE_BA = 0, 1
 HGM_DEVICE_PTRS = 1
+HGM_EXPLICIT_RESIDUAL = 2
 HGM_UNIQUE_ID_BYTES = 128
 
 c_int, c_int64, c_double, c_void_p = C.c_int, C.c_int64, C.c_double, C.c_void_p

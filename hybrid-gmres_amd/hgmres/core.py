@@ -285,15 +285,15 @@ def _ops(A, B, ctx):
     return ctx, Ao, Bo
 
 
-def _opts(orth="mgs", H_out=None, device_ptrs=False):
+def _opts(orth="mgs", H_out=None, device_ptrs=False, explicit_residual=False):
     o = L.hgm_opts()
-    o.flags = L.HGM_DEVICE_PTRS if device_ptrs else 0
+    o.flags = (L.HGM_DEVICE_PTRS if device_ptrs else 0) | (L.HGM_EXPLICIT_RESIDUAL if explicit_residual else 0)
     o.orth = L.HGM_CGS2 if str(orth).lower() == "cgs2" else L.HGM_MGS
     o.H_out = _dp(H_out) if H_out is not None else None
     return o
 
 
-def _gmres_call(fn_name, A, B, b, x_true, tol, maxit, lam, ctx, orth, return_H, extra=()):
+def _gmres_call(fn_name, A, B, b, x_true, tol, maxit, lam, ctx, orth, return_H, extra=(), explicit_residual=False):
     ctx, Ao, Bo = _ops(A, B, ctx)
     m, n = Ao.shape
     maxit = int(maxit)
@@ -304,7 +304,7 @@ def _gmres_call(fn_name, A, B, b, x_true, tol, maxit, lam, ctx, orth, return_H, 
     res = np.zeros(maxit)
     it = C.c_int(0)
     H = np.zeros((maxit + 1) * maxit) if return_H else None
-    o = _opts(orth, H)
+    o = _opts(orth, H, explicit_residual=explicit_residual)
     fn = getattr(L.load(), fn_name)
     if fn_name == "hgm_gmres_bounds_ex":
         lam_, side, hyb = extra
@@ -324,16 +324,21 @@ def _gmres_call(fn_name, A, B, b, x_true, tol, maxit, lam, ctx, orth, return_H, 
 # ---------------------------------------------------------------------------
 # Reference solver signatures
 # ---------------------------------------------------------------------------
-def hybrid_ab_gmres_rtp(A, B, b, x_true, tol, maxit, lambda_, *, ctx=None, orth="mgs", return_H=False):
+def hybrid_ab_gmres_rtp(A, B, b, x_true, tol, maxit, lambda_, *, ctx=None, orth="mgs", return_H=False,
+                        explicit_residual=False):
     """``[x, error_norm, residual_norm, niters] = hybrid_ab_gmres_rtp(A,B,b,x_true,tol,maxit,lambda)``
     (hybrid_ab_gmres_rtp.m:1-45): n-space Arnoldi on ``B*A + lambda*I``, projected
-    Tikhonov ``(AQk'AQk + lambda I) y = AQk' b``."""
-    return _gmres_call("hgm_hybrid_ab_gmres_rtp_ex", A, B, b, x_true, tol, maxit, lambda_, ctx, orth, return_H)
+    Tikhonov ``(AQk'AQk + lambda I) y = AQk' b``.  ``explicit_residual`` monitors
+    ``norm(b - A*x)`` with an SpMV of x instead of ``b - (A*Q) y`` (HGM_EXPLICIT_RESIDUAL)."""
+    return _gmres_call("hgm_hybrid_ab_gmres_rtp_ex", A, B, b, x_true, tol, maxit, lambda_, ctx, orth, return_H,
+                       explicit_residual=explicit_residual)
 
 
-def hybrid_ba_gmres_rtp(A, B, b, x_true, tol, maxit, lambda_, *, ctx=None, orth="mgs", return_H=False):
+def hybrid_ba_gmres_rtp(A, B, b, x_true, tol, maxit, lambda_, *, ctx=None, orth="mgs", return_H=False,
+                        explicit_residual=False):
     """``hybrid_ba_gmres_rtp.m:1-42``: Arnoldi on ``B*A + lambda*I``, ``yk = Hk \\ beta e1``."""
-    return _gmres_call("hgm_hybrid_ba_gmres_rtp_ex", A, B, b, x_true, tol, maxit, lambda_, ctx, orth, return_H)
+    return _gmres_call("hgm_hybrid_ba_gmres_rtp_ex", A, B, b, x_true, tol, maxit, lambda_, ctx, orth, return_H,
+                       explicit_residual=explicit_residual)
 
 
 def _bounds(A, B, b, x_true, tol, maxit, lam, side, hybrid, ctx, orth, return_H):

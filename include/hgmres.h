@@ -70,7 +70,9 @@ enum hgm_side { HGM_SIDE_AB = 0, HGM_SIDE_BA = 1 };
 
 /* Flags for the *_ex entry points. */
 enum hgm_flags {
-    HGM_DEVICE_PTRS = 1  /* b, x_true, x are device pointers (inputs resident in HBM) */
+    HGM_DEVICE_PTRS = 1,       /* b, x_true, x are device pointers (inputs resident in HBM) */
+    HGM_EXPLICIT_RESIDUAL = 2  /* BA-side GMRES: monitor norm(b - A*x) with an explicit SpMV of x
+                                  instead of b - (A*Q) y from the kept operator products */
 };
 
 typedef struct hgm_opts {
@@ -210,7 +212,10 @@ HGM_API int hgm_gcv_fminbnd(const double* H, int k, double beta, double trace_m,
 /* ---- timing hooks used by bench.py ---------------------------------------- */
 /* Average device time (ms) of the named kernel class over the calls since the
  * last reset, measured with HIP events on the context stream.  classes:
- * 0 = SpMV on A (ray-major), 1 = SpMV on B/Aᵀ (pixel-major), 2 = MGS pass. */
+ * 0 = SpMV on A (ray-major), 1 = SpMV on B/Aᵀ (pixel-major), 2 = MGS pass.
+ * enable: 0 = off, 1 = every class, HGM_TIMING_CLASSES(mask) = only the classes whose
+ * bit is set (each timed launch carries events, so time only what is read). */
+#define HGM_TIMING_CLASSES(mask) (0x100 | (mask))
 HGM_API int hgm_kernel_timing(hgm_ctx* ctx, int enable);
 HGM_API int hgm_kernel_timing_read(hgm_ctx* ctx, int cls, double* total_ms, int64_t* calls,
                                    double* bytes);
