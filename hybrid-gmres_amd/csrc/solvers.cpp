@@ -177,8 +177,16 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     const int64_t ldaq = round_up(m > 0 ? m : 1, 64);
     // n-space side: keep the operator's products A*Q(:,j) (the RTP Gram matrix needs them,
     // and the residual monitor b - A*x = b - (A*Q) y reuses them instead of another SpMV)
-    const bool aq_res = nspace && !(o && (o->flags & HGM_EXPLICIT_RESIDUAL));
+    const bool reuse = !(o && (o->flags & HGM_EXPLICIT_RESIDUAL));
+    const bool aq_res = nspace && reuse;
     T* AQ = (sp.proj == PROJ_ABRTP || aq_res) ? c->buf<T>("AQ", (size_t)ldaq * maxit) : nullptr;
+    // m-space side: keep B*Q(:,j) and A*(B*Q(:,j)) (the latter is the new Arnoldi vector
+    // before orthogonalisation), so x = B*(Q y) = (B*Q) y and b - A*x = b - (A*B*Q) y are
+    // GEMVs over k kept columns instead of two SpMVs per iteration (*_bounds.m:37-40)
+    const bool bq_res = !nspace && reuse;
+    const int64_t ldbq = round_up(n > 0 ? n : 1, 64);
+    T* BQ = bq_res ? c->buf<T>("BQ", (size_t)ldbq * maxit) : nullptr;
+    T* ABQ = bq_res ? c->buf<T>("ABQ", (size_t)ldaq * maxit) : nullptr;
     // Per-iteration exchange ring in pinned host memory: slot k holds
     // [H(:,k) | Gram column k, AQk'b] (LH doubles), the monitors [res^2, err^2] of
     // iteration k, and the projected solution y_k.  Single GPU: the kernels write the
@@ -240,8 +248,11 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             if (sp.lambda_in_op) apply_B<T>(c, B, Aq, v, EPI_ADD, T(lambda), qk);   // B*(A*v) + lambda*v
             else apply_B<T>(c, B, Aq, v, EPI_NONE, T(0), nullptr);                  // B*(A*v)
         } else {
-            apply_B<T>(c, B, qk, tn, EPI_NONE, T(0), nullptr);                      // B*Q(:,k)
-            apply_A<T>(c, A, tn, v, EPI_NONE, T(0), nullptr);                       // A*(B*Q(:,k))
+            T* Bq = BQ ? BQ + (int64_t)kq * ldbq : tn;
+            apply_B<T>(c, B, qk, Bq, EPI_NONE, T(0), nullptr);                      // B*Q(:,k)
+            apply_A<T>(c, A, Bq, v, EPI_NONE, T(0), nullptr);                       // A*(B*Q(:,k))
+            if (ABQ)
+                HGM_HIP(hipMemcpyAsync(ABQ + (int64_t)kq * ldaq, v, sizeof(T) * m, hipMemcpyDeviceToDevice, c->stream));
         }
         // ---- orthogonalisation (hybrid_*_rtp.m:20-26) ----
         T* Hcol = dr + (size_t)kq * LH;                  // -> host H(:,k)
@@ -270,6 +281,15 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             // x = Q(:,1:k)*yk with ||x - x_true||^2 (:33/:36) and ||b - A*x||^2 (:32/:35)
             // evaluated as ||b - (A*Q(:,1:k))*yk||^2, all in one launch (+ finalize)
             recon<T>(c, n, kk, Q, ldq, yk, x, xt, eslot, m, AQ, ldaq, b, rslot);
+            if (dist_n(c)) allreduce(c, eslot, 1);
+            publish(offM + 2 * (size_t)kq, 2);
+            pipe_record(c);
+            return;
+        }
+        if (bq_res) {
+            // xk = B*(Q(:,1:k)*yk) = (B*Q(:,1:k))*yk with ||xk - x_true||^2, and
+            // ||b - A*xk||^2 = ||b - (A*B*Q(:,1:k))*yk||^2 (*_bounds.m:37-40), one launch
+            recon<T>(c, n, kk, BQ, ldbq, yk, x, xt, eslot, m, ABQ, ldaq, b, rslot);
             if (dist_n(c)) allreduce(c, eslot, 1);
             publish(offM + 2 * (size_t)kq, 2);
             pipe_record(c);

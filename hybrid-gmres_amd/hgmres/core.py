@@ -341,32 +341,40 @@ def hybrid_ba_gmres_rtp(A, B, b, x_true, tol, maxit, lambda_, *, ctx=None, orth=
                        explicit_residual=explicit_residual)
 
 
-def _bounds(A, B, b, x_true, tol, maxit, lam, side, hybrid, ctx, orth, return_H):
+def _bounds(A, B, b, x_true, tol, maxit, lam, side, hybrid, ctx, orth, return_H, explicit_residual=False):
     out = _gmres_call("hgm_gmres_bounds_ex", A, B, b, x_true, tol, maxit, lam, ctx, orth, return_H,
-                      extra=(lam, side, hybrid))
+                      extra=(lam, side, hybrid), explicit_residual=explicit_residual)
     # outputs 5-8 (phi_final, dphi_final, phi_iter, dphi_iter): dense spectral bounds, out of scope
     return out[:4] + (None, None, None, None) + out[4:]
 
 
-def ABgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lambda_, DeltaM=None, *, ctx=None, orth="mgs", return_H=False):
+def ABgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lambda_, DeltaM=None, *, ctx=None, orth="mgs", return_H=False,
+                             explicit_residual=False):
     """``ABgmres_hybrid_bounds.m`` outputs 1-4: m-space Arnoldi on ``A*B``, PTR Tikhonov, ``x = B*z``."""
-    return _bounds(A, B, b, x_true, tol, maxit, lambda_, L.HGM_SIDE_AB, 1, ctx, orth, return_H)
+    return _bounds(A, B, b, x_true, tol, maxit, lambda_, L.HGM_SIDE_AB, 1, ctx, orth, return_H,
+                   explicit_residual=explicit_residual)
 
 
-def ABgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, *, ctx=None, orth="mgs", return_H=False):
+def ABgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, *, ctx=None, orth="mgs", return_H=False,
+                             explicit_residual=False):
     """``ABgmres_nonhybrid_bounds.m`` outputs 1-4."""
-    return _bounds(A, B, b, x_true, tol, maxit, 0.0, L.HGM_SIDE_AB, 0, ctx, orth, return_H)
+    return _bounds(A, B, b, x_true, tol, maxit, 0.0, L.HGM_SIDE_AB, 0, ctx, orth, return_H,
+                   explicit_residual=explicit_residual)
 
 
-def BAgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lambda_, DeltaM=None, *, ctx=None, orth="mgs", return_H=False):
+def BAgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lambda_, DeltaM=None, *, ctx=None, orth="mgs", return_H=False,
+                             explicit_residual=False):
     """``BAgmres_hybrid_bounds.m`` outputs 1-4: n-space Arnoldi on ``B*A``, PTR Tikhonov."""
-    return _bounds(A, B, b, x_true, tol, maxit, lambda_, L.HGM_SIDE_BA, 1, ctx, orth, return_H)
+    return _bounds(A, B, b, x_true, tol, maxit, lambda_, L.HGM_SIDE_BA, 1, ctx, orth, return_H,
+                   explicit_residual=explicit_residual)
 
 
-def BAgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, *, ctx=None, orth="mgs", return_H=False):
+def BAgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, *, ctx=None, orth="mgs", return_H=False,
+                             explicit_residual=False):
     """``BAgmres_nonhybrid_bounds.m`` outputs 1-4.  The reference forms ``M = B*A``
     explicitly (``:4``); here the operator is applied as ``B*(A*q)``."""
-    return _bounds(A, B, b, x_true, tol, maxit, 0.0, L.HGM_SIDE_BA, 0, ctx, orth, return_H)
+    return _bounds(A, B, b, x_true, tol, maxit, 0.0, L.HGM_SIDE_BA, 0, ctx, orth, return_H,
+                   explicit_residual=explicit_residual)
 
 
 def _gkb_ops(A, ctx, At=None, dtype=L.HGM_F64):

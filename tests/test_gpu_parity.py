@@ -262,17 +262,24 @@ def test_gmres_c1_golden(gpu_ctx):
         hist_ok(out[1], g[f"{tag}_err"], TOL)
 
 
-@pytest.mark.parametrize("fn", [hgmres.hybrid_ab_gmres_rtp, hgmres.hybrid_ba_gmres_rtp])
-def test_residual_monitor_forms_agree(gpu_ctx, P64, fn):
-    """The n-space GMRES monitors norm(b - A*x) (hybrid_*_rtp.m:32/35) as b - (A*Q) y from
-    the kept operator products by default; HGM_EXPLICIT_RESIDUAL recomputes A*x.  Both
-    histories agree with each other and with the oracle to 1e-10, and everything else
-    (x, H, error history) is bitwise identical."""
-    o1 = fn(P64.A, P64.B, P64.b, P64.x_true, 0.0, 20, 1e-2, ctx=gpu_ctx, return_H=True)
-    o2 = fn(P64.A, P64.B, P64.b, P64.x_true, 0.0, 20, 1e-2, ctx=gpu_ctx, return_H=True, explicit_residual=True)
-    assert np.array_equal(o1[0], o2[0]) and np.array_equal(o1[4], o2[4]) and np.array_equal(o1[1], o2[1])
+@pytest.mark.parametrize("tag,fn,haslam", GM)
+def test_residual_monitor_forms_agree(gpu_ctx, P64, tag, fn, haslam):
+    """By default the GMRES family forms its monitors from the operator products it
+    already computed: n-space x = Q y and norm(b - A*x) as b - (A*Q) y (hybrid_*_rtp.m:30-35);
+    m-space x = B*(Q y) as (B*Q) y and b - A*x as b - (A*B*Q) y (*_bounds.m:37-40).
+    HGM_EXPLICIT_RESIDUAL applies the SpMVs instead.  The Hessenberg matrix is bitwise
+    identical (the Arnoldi part is shared) and the outputs agree with each other and with
+    the oracle to 1e-10."""
+    args = (1e-2,) if haslam else ()
+    o1 = fn(P64.A, P64.B, P64.b, P64.x_true, 0.0, 20, *args, ctx=gpu_ctx, return_H=True)
+    o2 = fn(P64.A, P64.B, P64.b, P64.x_true, 0.0, 20, *args, ctx=gpu_ctx, return_H=True, explicit_residual=True)
+    assert o1[3] == o2[3] and np.array_equal(o1[-1], o2[-1])
+    assert rel(o1[0], o2[0]) < 1e-12
+    hist_ok(o1[1], o2[1], 1e-12)
     hist_ok(o1[2], o2[2], 1e-12)
-    ref = getattr(R, fn.__name__)(P64.A, P64.B.tocsr(), P64.b, P64.x_true, 0.0, 20, 1e-2)
+    ref = getattr(R, fn.__name__)(P64.A, P64.B.tocsr(), P64.b, P64.x_true, 0.0, 20, *args)
+    assert rel(o1[0], ref[0]) < TOL
+    hist_ok(o1[1], ref[1], TOL)
     hist_ok(o1[2], ref[2], TOL)
 
 
