@@ -263,6 +263,25 @@ using namespace hgm;
         return HGM_E_HIP;                                       \
     }
 
+// y = A x with x and y in the reference index order (the operator may store a pixel space
+// in a tiled order: permute on the way in / out)
+template <typename T>
+static void spmv_ref(hgm_ctx* c, const hgm_mat* A, const T* x, T* y) {
+    const T* xs = x;
+    if (!A->col_order.trivial()) {
+        T* t = c->buf<T>("spmv_x_pix", A->cols);
+        pix_permute<T>(c, A->col_order, x, t, 0);
+        xs = t;
+    }
+    if (A->row_order.trivial()) {
+        spmv<T>(c, A, xs, y, EPI_NONE, T(0), nullptr, KC_SPMV_A);
+        return;
+    }
+    T* t = c->buf<T>("spmv_y_pix", A->rows);
+    spmv<T>(c, A, xs, t, EPI_NONE, T(0), nullptr, KC_SPMV_A);
+    pix_permute<T>(c, A->row_order, t, y, 1);
+}
+
 static int ctx_init(hgm_ctx* c, int device) {
     c->device = device;
     const char* hs = std::getenv("HGM_HOST_STATS");
@@ -459,6 +478,26 @@ HGM_API int hgm_mat_create_siddon(hgm_ctx* c, int N, int n_angles, double det_of
     return HGM_OK;
 }
 
+HGM_API int hgm_mat_create_siddon_ordered(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype, int tile,
+                                          int super_block, hgm_mat** out) {
+    if (!c || !out) return HGM_E_ARG;
+    *out = nullptr;
+    HGM_TRY(c, {
+        *out = siddon(c, N, n_angles, det_offset, dtype, tile, super_block);
+        finalize_operator(c, *out);
+    });
+    return HGM_OK;
+}
+
+HGM_API int hgm_mat_order(const hgm_mat* M, int which, int* N, int* tile, int* super_block) {
+    if (!M || (which != 0 && which != 1)) return HGM_E_ARG;
+    const PixOrder& o = which == 0 ? M->row_order : M->col_order;
+    if (N) *N = o.N;
+    if (tile) *tile = o.trivial() ? 1 : o.tile;
+    if (super_block) *super_block = o.trivial() ? 0 : o.super;
+    return HGM_OK;
+}
+
 HGM_API int hgm_mat_info(const hgm_mat* M, int64_t* rows, int64_t* cols, int64_t* nnz, int* dtype) {
     if (!M) return HGM_E_ARG;
     if (rows) *rows = M->rows;
@@ -488,22 +527,67 @@ HGM_API int hgm_mat_tune(hgm_mat* M, int variant, int group) {
     return HGM_OK;
 }
 
-HGM_API int hgm_mat_download(hgm_ctx* c, const hgm_mat* M, int64_t* row_ptr, int32_t* col_idx, double* val) {
-    if (!c || !M) return HGM_E_ARG;
-    HGM_TRY(c, {
-        if (row_ptr) HGM_HIP(hipMemcpy(row_ptr, M->rp, sizeof(int64_t) * (M->rows + 1), hipMemcpyDeviceToHost));
-        if (col_idx && M->nnz) HGM_HIP(hipMemcpy(col_idx, M->ci, sizeof(int32_t) * M->nnz, hipMemcpyDeviceToHost));
-        if (val && M->nnz) {
+}  // extern "C"
+
+namespace hgm {
+// CSR in the reference index orders (see hgm_mat_create_siddon_ordered)
+static void mat_download_impl(hgm_ctx* c, const hgm_mat* M, int64_t* row_ptr, int32_t* col_idx, double* val) {
+    {
+        HGM_HIP(hipSetDevice(c->device));
+        // stored arrays (column indices mapped back to the reference order on the device)
+        std::vector<int64_t> rp((size_t)M->rows + 1);
+        std::vector<int32_t> ci((size_t)M->nnz);
+        std::vector<double> vv((size_t)M->nnz);
+        HGM_HIP(hipMemcpy(rp.data(), M->rp, sizeof(int64_t) * (M->rows + 1), hipMemcpyDeviceToHost));
+        if (M->nnz) {
+            const int32_t* src = M->ci;
+            if (!M->col_order.trivial()) {
+                int32_t* t = c->buf<int32_t>("mat_ci_ref", M->nnz);
+                HGM_HIP(hipMemcpyAsync(t, M->ci, sizeof(int32_t) * M->nnz, hipMemcpyDeviceToDevice, c->stream));
+                pix_unmap_indices(c, M->col_order, t, M->nnz);
+                HGM_HIP(hipStreamSynchronize(c->stream));
+                src = t;
+            }
+            HGM_HIP(hipMemcpy(ci.data(), src, sizeof(int32_t) * M->nnz, hipMemcpyDeviceToHost));
             if (M->dtype == HGM_F64) {
-                HGM_HIP(hipMemcpy(val, M->val, sizeof(double) * M->nnz, hipMemcpyDeviceToHost));
+                HGM_HIP(hipMemcpy(vv.data(), M->val, sizeof(double) * M->nnz, hipMemcpyDeviceToHost));
             } else {
                 double* tmp = c->buf<double>("mat_f64", M->nnz);
                 convert_back<float>(c, M->nnz, reinterpret_cast<const float*>(M->val), tmp);
                 HGM_HIP(hipStreamSynchronize(c->stream));
-                HGM_HIP(hipMemcpy(val, tmp, sizeof(double) * M->nnz, hipMemcpyDeviceToHost));
+                HGM_HIP(hipMemcpy(vv.data(), tmp, sizeof(double) * M->nnz, hipMemcpyDeviceToHost));
             }
         }
-    });
+        if (M->row_order.trivial()) {
+            if (row_ptr) std::memcpy(row_ptr, rp.data(), sizeof(int64_t) * (M->rows + 1));
+            if (col_idx && M->nnz) std::memcpy(col_idx, ci.data(), sizeof(int32_t) * M->nnz);
+            if (val && M->nnz) std::memcpy(val, vv.data(), sizeof(double) * M->nnz);
+        } else {
+            // rows stored in a pixel order: emit them in the reference order
+            HGM_REQUIRE((int64_t)M->row_order.N * M->row_order.N == M->rows, "download: row order size");
+            const std::vector<int64_t> ref = pix_reference_of_stored(M->row_order);
+            std::vector<int64_t> stored_of(ref.size());
+            for (size_t s = 0; s < ref.size(); ++s) stored_of[(size_t)ref[s]] = (int64_t)s;
+            int64_t off = 0;
+            for (int64_t p = 0; p < M->rows; ++p) {
+                const int64_t s = stored_of[(size_t)p];
+                const int64_t b = rp[(size_t)s], e = rp[(size_t)s + 1];
+                if (row_ptr) row_ptr[p] = off;
+                if (col_idx) std::memcpy(col_idx + off, ci.data() + b, sizeof(int32_t) * (e - b));
+                if (val) std::memcpy(val + off, vv.data() + b, sizeof(double) * (e - b));
+                off += e - b;
+            }
+            if (row_ptr) row_ptr[M->rows] = off;
+        }
+    }
+}
+}  // namespace hgm
+
+extern "C" {
+
+HGM_API int hgm_mat_download(hgm_ctx* c, const hgm_mat* M, int64_t* row_ptr, int32_t* col_idx, double* val) {
+    if (!c || !M) return HGM_E_ARG;
+    HGM_TRY(c, hgm::mat_download_impl(c, M, row_ptr, col_idx, val));
     return HGM_OK;
 }
 
@@ -516,10 +600,8 @@ HGM_API void hgm_mat_destroy(hgm_mat* M) {
 HGM_API int hgm_spmv(hgm_ctx* c, const hgm_mat* A, const void* x, void* y) {
     if (!c || !A || !x || !y) return HGM_E_ARG;
     HGM_TRY(c, {
-        if (A->dtype == HGM_F64)
-            spmv<double>(c, A, (const double*)x, (double*)y, EPI_NONE, 0.0, nullptr, KC_SPMV_A);
-        else
-            spmv<float>(c, A, (const float*)x, (float*)y, EPI_NONE, 0.0f, nullptr, KC_SPMV_A);
+        if (A->dtype == HGM_F64) spmv_ref<double>(c, A, (const double*)x, (double*)y);
+        else spmv_ref<float>(c, A, (const float*)x, (float*)y);
     });
     return HGM_OK;
 }

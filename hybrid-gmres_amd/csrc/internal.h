@@ -104,9 +104,28 @@ struct hgm_ctx {
     }
 };
 
+namespace hgm {
+// Storage order of an N x N pixel index space.  Trivial (N == 0): the
+// reference's column-major x(:).  Otherwise pixel (r, c) is stored at
+// pixel_index(N, tile, super, r, c): super x super blocks (column-major over blocks, each
+// contiguous; super == 0: one block), tile x tile tiles inside (tile-column-major), and
+// column-major inside a tile.  A 4 x 4 tile of doubles is one 128-B cache line, so the x
+// gathers of a ray share lines; a super-block is the x-slice a column band keeps in L2.
+struct PixOrder {
+    int N = 0, tile = 1, super = 0;
+    bool trivial() const { return N == 0; }
+    bool operator==(const PixOrder& o) const {
+        return trivial() ? o.trivial() : (N == o.N && tile == o.tile && super == o.super);
+    }
+    bool operator!=(const PixOrder& o) const { return !(*this == o); }
+};
+}  // namespace hgm
+
 struct hgm_mat {
     hgm_ctx* ctx = nullptr;
     int64_t rows = 0, cols = 0, nnz = 0;
+    // index-space orders of the rows / columns (pixel spaces may be stored tiled)
+    hgm::PixOrder row_order, col_order;
     int dtype = HGM_F64;
     int64_t* rp = nullptr;   // rows+1
     int32_t* ci = nullptr;   // nnz
@@ -207,7 +226,15 @@ void build_stream_index(hgm_ctx* c, hgm_mat* M);
 // everything a freshly created operator gets: automatic bands + streaming index
 void finalize_operator(hgm_ctx* c, hgm_mat* M);
 int64_t auto_band_width(const hgm_mat* M);
-hgm_mat* siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype);
+hgm_mat* siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype, int tile = 1, int super = 0);
+// n-vector between the reference order and a pixel order o: dir 0: out[stored(p)] = in[p]
+// (reference -> stored), dir 1: out[p] = in[stored(p)] (stored -> reference)
+template <typename T>
+void pix_permute(hgm_ctx* c, const PixOrder& o, const T* in, T* out, int dir);
+// stored pixel index -> reference (column-major) index, in place on n indices
+void pix_unmap_indices(hgm_ctx* c, const PixOrder& o, int32_t* idx, int64_t n);
+// reference index of every stored position (host vector, for host-side row reordering)
+std::vector<int64_t> pix_reference_of_stored(const PixOrder& o);
 
 // ---------------- comm / scalars (capi.cpp) ----------------
 void allreduce(hgm_ctx* c, double* dev, int64_t count);

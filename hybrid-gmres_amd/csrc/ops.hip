@@ -136,15 +136,17 @@ void finalize_operator(hgm_ctx* c, hgm_mat* M) {
     if (avg >= 64) {
         if (M->nbands > 1) {
             M->variant = SPMV_STREAM;
-            M->bsgroup = 32;
+            // super-block pixel order: a band segment is a short ray chord through a compact
+            // block -> 16 lanes per segment (C4 sweep, profiles/r1_spmv_sweep_c4_order.jsonl)
+            M->bsgroup = M->col_order.super > 1 ? 16 : 32;
         } else {
             M->variant = SPMV_VEC;
             M->group = 32;
         }
     } else {
         if (M->nnz >= 50000000) {
-            M->variant = SPMV_STREAM | SPMV_NT;
-            M->sgroup = 8;
+            M->variant = SPMV_STREAM;
+            M->sgroup = avg < 16 ? 4 : 8;
         } else {
             M->variant = 0;
             M->group = avg >= 6 ? 8 : 4;
@@ -160,6 +162,8 @@ int64_t auto_band_width(const hgm_mat* M) {
     if ((double)M->cols * vs <= 4.0 * 1024 * 1024) return 0;
     // only long-row operators benefit (the short pixel-major rows of B gather an L2-resident y)
     if (M->rows > 0 && (double)M->nnz / (double)M->rows < 64) return 0;
+    // super-block pixel order: 256 Ki pixels (a few compact blocks, 2 MiB fp64 x-slice)
+    if (M->col_order.super > 1) return (int64_t)(1 << 18);
     return (int64_t)(1 << 17);   // 128 Ki pixels = 1 MiB fp64 x-slice per band
 }
 
@@ -261,6 +265,8 @@ hgm_mat* transpose(hgm_ctx* c, const hgm_mat* M) {
     hipStream_t st = c->stream;
     const int64_t nnz = M->nnz;
     hgm_mat* T = mat_alloc(c, M->cols, M->rows, nnz, M->dtype);
+    T->row_order = M->col_order;
+    T->col_order = M->row_order;
     if (nnz == 0) {
         HGM_HIP(hipMemsetAsync(T->rp, 0, sizeof(int64_t) * (T->rows + 1), st));
         HGM_HIP(hipStreamSynchronize(st));
@@ -342,8 +348,90 @@ __device__ __forceinline__ RayGeom ray_geom(int N, double c, double s_, double s
 
 // Walk the merged, sorted crossing sequence [tmin, x/y-plane crossings in range, tmax]
 // and emit segments with length > 1e-10 (problems.py: valid = isfinite & L > 1e-10).
+// pixel (row r, column c) -> column index: column-major r + c*N (the reference's
+// x(:) order) or, for tile > 1, tile-major over tile x tile blocks (column-major inside)
+__device__ __forceinline__ int64_t tiled_index(int64_t S, int tile, int64_t r, int64_t c) {
+    if (tile <= 1) return r + c * S;
+    const int64_t tr = r / tile, tc = c / tile;
+    return ((tc * (S / tile) + tr) * tile + (c % tile)) * tile + (r % tile);
+}
+// super > 1: super x super blocks (column-major over blocks), each contiguous, tiled inside
+__host__ __device__ __forceinline__ int64_t pixel_index(int N, int tile, int64_t r, int64_t c, int super = 0) {
+    if (super <= 1) return tiled_index(N, tile, r, c);
+    const int64_t sr = r / super, sc = c / super;
+    return (sc * (N / super) + sr) * (int64_t)super * super + tiled_index(super, tile, r % super, c % super);
+}
+
+// inverse of pixel_index: stored index -> (r, c)
+__host__ __device__ __forceinline__ void pixel_rc(int N, int tile, int super, int64_t idx, int64_t& r, int64_t& c) {
+    const int64_t S = super > 1 ? super : N;
+    const int64_t blk = idx / (S * S), rem = idx % (S * S);
+    const int64_t nb = N / S;
+    const int64_t sc = blk / nb, sr = blk % nb;
+    int64_t rr, cc;
+    if (tile > 1) {
+        const int64_t t = rem / ((int64_t)tile * tile), w = rem % ((int64_t)tile * tile);
+        const int64_t tc = t / (S / tile), tr = t % (S / tile);
+        rr = tr * tile + w % tile;
+        cc = tc * tile + w / tile;
+    } else {
+        rr = rem % S;
+        cc = rem / S;
+    }
+    r = sr * S + rr;
+    c = sc * S + cc;
+}
+
+// reference index p = r + c*N <-> stored index pixel_index(r, c)
+template <typename T>
+__global__ __launch_bounds__(BS) void k_pix_permute(int N, int tile, int super, const T* __restrict__ in,
+                                                    T* __restrict__ out, int dir) {
+    const int64_t n = (int64_t)N * N;
+    for (int64_t p = (int64_t)blockIdx.x * BS + threadIdx.x; p < n; p += (int64_t)gridDim.x * BS) {
+        const int64_t s = pixel_index(N, tile, p % N, p / N, super);
+        if (dir == 0) out[s] = in[p];
+        else out[p] = in[s];
+    }
+}
+
+__global__ __launch_bounds__(BS) void k_pix_unmap(int N, int tile, int super, int32_t* __restrict__ idx, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+        int64_t r, c;
+        pixel_rc(N, tile, super, idx[i], r, c);
+        idx[i] = (int32_t)(r + c * N);
+    }
+}
+
+template <typename T>
+void pix_permute(hgm_ctx* c, const PixOrder& o, const T* in, T* out, int dir) {
+    HGM_REQUIRE(!o.trivial(), "pix_permute: trivial order");
+    const int64_t n = (int64_t)o.N * o.N;
+    k_pix_permute<T><<<grid_cap(n), BS, 0, c->stream>>>(o.N, o.tile, o.super, in, out, dir);
+    HGM_HIP(hipGetLastError());
+}
+template void pix_permute<double>(hgm_ctx*, const PixOrder&, const double*, double*, int);
+template void pix_permute<float>(hgm_ctx*, const PixOrder&, const float*, float*, int);
+
+void pix_unmap_indices(hgm_ctx* c, const PixOrder& o, int32_t* idx, int64_t n) {
+    if (o.trivial() || n == 0) return;
+    k_pix_unmap<<<grid_cap(n), BS, 0, c->stream>>>(o.N, o.tile, o.super, idx, n);
+    HGM_HIP(hipGetLastError());
+}
+
+std::vector<int64_t> pix_reference_of_stored(const PixOrder& o) {
+    const int64_t n = (int64_t)o.N * o.N;
+    std::vector<int64_t> ref(n);
+    for (int64_t s = 0; s < n; ++s) {
+        int64_t r, c;
+        pixel_rc(o.N, o.tile, o.super, s, r, c);
+        ref[s] = r + c * o.N;
+    }
+    return ref;
+}
+
 template <bool FILL, typename T>
-__device__ int64_t siddon_walk(int N, const RayGeom& g, int64_t out0, int32_t* ci, T* val) {
+__device__ int64_t siddon_walk(int N, const RayGeom& g, int64_t out0, int32_t* ci, T* val, int tile = 1,
+                               int super = 0) {
     if (!g.hit) return 0;
     const double half = N / 2.0;
     // next in-range crossing of each family in increasing t
@@ -388,7 +476,7 @@ __device__ int64_t siddon_walk(int N, const RayGeom& g, int64_t out0, int32_t* c
                 fx = fmin(fmax(fx, 0.0), (double)(N - 1));
                 fy = fmin(fmax(fy, 0.0), (double)(N - 1));
                 const int64_t ix = (int64_t)fx, iy = (int64_t)fy;
-                ci[out0 + cnt] = (int32_t)(ix * N + (N - 1 - iy));
+                ci[out0 + cnt] = (int32_t)pixel_index(N, tile, N - 1 - iy, ix, super);
                 val[out0 + cnt] = (T)L;
             }
             ++cnt;
@@ -402,17 +490,22 @@ template <bool FILL, typename T>
 __global__ __launch_bounds__(BS) void k_siddon(int N, int p, int64_t m, const double* __restrict__ cth,
                                                const double* __restrict__ sth, const double* __restrict__ sdet,
                                                int64_t* __restrict__ counts, const int64_t* __restrict__ rp,
-                                               int32_t* __restrict__ ci, T* __restrict__ val) {
+                                               int32_t* __restrict__ ci, T* __restrict__ val, int tile,
+                                               int super) {
     for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < m; r += (int64_t)gridDim.x * BS) {
         const int a = (int)(r / p), d = (int)(r % p);
         const RayGeom g = ray_geom(N, cth[a], sth[a], sdet[d]);
-        if (FILL) siddon_walk<true, T>(N, g, rp[r], ci, val);
+        if (FILL) siddon_walk<true, T>(N, g, rp[r], ci, val, tile, super);
         else counts[r] = siddon_walk<false, T>(N, g, 0, nullptr, nullptr);
     }
 }
 
-hgm_mat* siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype) {
+hgm_mat* siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype, int tile, int super) {
     HGM_REQUIRE(N > 0 && n_angles > 0, "siddon: N and n_angles must be positive");
+    if (tile < 1) tile = 1;
+    if (super < 2) super = 0;
+    HGM_REQUIRE(N % tile == 0 && (super == 0 || (N % super == 0 && super % tile == 0)),
+                "siddon: tile must divide N (and super), super must divide N");
     hipStream_t st = c->stream;
     const int p = (int)std::ceil(std::sqrt(2.0) * N);
     const int64_t m = (int64_t)p * n_angles;
@@ -441,7 +534,7 @@ hgm_mat* siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype) {
         HGM_HIP(hipMemcpyAsync(dd, sdet.data(), 8 * p, hipMemcpyHostToDevice, st));
         HGM_HIP(hipMemsetAsync(counts, 0, 8 * (m + 1), st));
         const int g = grid_cap(m);
-        k_siddon<false, double><<<g, BS, 0, st>>>(N, p, m, dc, ds, dd, counts, nullptr, nullptr, nullptr);
+        k_siddon<false, double><<<g, BS, 0, st>>>(N, p, m, dc, ds, dd, counts, nullptr, nullptr, nullptr, 1, 0);
         HGM_HIP(hipGetLastError());
         HGM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, rp, (int)(m + 1), st));
         HGM_HIP(hipMalloc(&tmp, tmp_bytes));
@@ -452,10 +545,13 @@ hgm_mat* siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype) {
         HGM_REQUIRE(nnz < (int64_t)INT32_MAX * 2, "siddon: nnz overflow");
         M = mat_alloc(c, m, (int64_t)N * N, nnz, dtype);
         HGM_HIP(hipMemcpyAsync(M->rp, rp, 8 * (m + 1), hipMemcpyDeviceToDevice, st));
+        if (tile > 1 || super > 1) M->col_order = PixOrder{N, tile, super};
         if (dtype == HGM_F32)
-            k_siddon<true, float><<<g, BS, 0, st>>>(N, p, m, dc, ds, dd, nullptr, M->rp, M->ci, (float*)M->val);
+            k_siddon<true, float><<<g, BS, 0, st>>>(N, p, m, dc, ds, dd, nullptr, M->rp, M->ci, (float*)M->val, tile,
+                                                    super);
         else
-            k_siddon<true, double><<<g, BS, 0, st>>>(N, p, m, dc, ds, dd, nullptr, M->rp, M->ci, (double*)M->val);
+            k_siddon<true, double><<<g, BS, 0, st>>>(N, p, m, dc, ds, dd, nullptr, M->rp, M->ci, (double*)M->val,
+                                                     tile, super);
         HGM_HIP(hipGetLastError());
         HGM_HIP(hipStreamSynchronize(st));
     } catch (...) {

@@ -122,6 +122,38 @@ void stage_out(hgm_ctx* c, double* out, const T* d, int64_t n, bool dev) {
     }
 }
 
+// The stored order of the pixel (n) space shared by A's columns and B's (or A''s) rows;
+// the ray (m) space is always in the reference order.
+PixOrder n_order(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
+    HGM_REQUIRE(A->row_order.trivial() && (!B || B->col_order.trivial()),
+                "the ray (m) space must be stored in the reference order");
+    if (B) HGM_REQUIRE(B->row_order == A->col_order, "A's columns and B's rows must share one pixel order");
+    HGM_REQUIRE(A->col_order.trivial() || !dist_n(c), "pixel-sharded solves need the reference pixel order");
+    return A->col_order;
+}
+
+// n-vector hand-over in the reference order, permuted into / out of the stored order
+template <typename T>
+const T* stage_in_n(hgm_ctx* c, const char* name, const double* p, int64_t n, bool dev, const PixOrder& o) {
+    const T* d = stage_in<T>(c, name, p, n, dev);
+    if (d == nullptr || o.trivial()) return d;
+    T* q = c->buf<T>(std::string(name) + "_pix", n);
+    pix_permute<T>(c, o, d, q, 0);
+    return q;
+}
+
+template <typename T>
+void stage_out_n(hgm_ctx* c, double* out, const T* d, int64_t n, bool dev, const PixOrder& o) {
+    if (out == nullptr || n == 0) return;
+    if (o.trivial()) {
+        stage_out<T>(c, out, d, n, dev);
+        return;
+    }
+    T* q = c->buf<T>("out_pix", n);
+    pix_permute<T>(c, o, d, q, 1);
+    stage_out<T>(c, out, q, n, dev);
+}
+
 void check_dims(const hgm_mat* A, const hgm_mat* B) {
     HGM_REQUIRE(A != nullptr, "A is NULL");
     if (B) {
@@ -150,6 +182,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
                  double* err_out, double* res_out, int* niters) {
     check_dims(A, B);
     HGM_REQUIRE(B != nullptr, "B is NULL");
+    const PixOrder po = n_order(c, A, B);
     HGM_REQUIRE(b_in != nullptr && xt_in != nullptr, "b and x_true are required");
     HGM_REQUIRE(A->dtype == HGM_F64, "GMRES family is fp64 (the reference's precision)");
     const auto t_start = std::chrono::steady_clock::now();
@@ -167,7 +200,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     hipStream_t st = c->stream;
 
     const T* b = stage_in<T>(c, "in_b", b_in, m, dev);
-    const T* xt = stage_in<T>(c, "in_xt", xt_in, n, dev);
+    const T* xt = stage_in_n<T>(c, "in_xt", xt_in, n, dev, po);
     T* Q = c->buf<T>("Q", (size_t)ldq * (maxit + 1));
     T* x = c->buf<T>("x", n > 0 ? n : 1);
     T* t = c->buf<T>("t_m", m > 0 ? m : 1);        // m-vector scratch (A*q, residual)
@@ -400,7 +433,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     const int nit = k + 1;                               // niters = k
     if (rs_stream != st) HGM_HIP(hipStreamSynchronize(rs_stream));
     if (!x_assigned) throw Error{HGM_E_NOT_ASSIGNED, "Output argument \"x\" not assigned during call (breakdown at k = 1)"};
-    stage_out<T>(c, x_out, x, n, dev);
+    stage_out_n<T>(c, x_out, x, n, dev, po);
     if (c->host_stats) {
         const double tot = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
         std::fprintf(stderr, "hgm gmres: %d iters, %.1f us total, %.1f us blocked in %ld waits\n", nit, tot * 1e6,
@@ -422,12 +455,13 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
            double* err_out, double* res_out, int* niters) {
     check_dims(A, At);
     HGM_REQUIRE(At != nullptr, "At is NULL");
+    const PixOrder po = n_order(c, A, At);
     HGM_REQUIRE(b_in != nullptr && xt_in != nullptr, "b and x_true are required");
     HGM_REQUIRE(maxit >= 1, "maxit must be >= 1");
     const bool dev = o && (o->flags & HGM_DEVICE_PTRS);
     const int64_t m = A->rows, n = A->cols;
     const T* b = stage_in<T>(c, "in_b", b_in, m, dev);
-    const T* xt = stage_in<T>(c, "in_xt", xt_in, n, dev);
+    const T* xt = stage_in_n<T>(c, "in_xt", xt_in, n, dev, po);
     T* x = c->buf<T>("x", n + 1);
     T* w = c->buf<T>("w", n + 1);
     T* v = c->buf<T>("v", n + 1);
@@ -525,7 +559,7 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         sumsq<T>(c, m, t, sl + S_RES);
         res[nit - 1] = std::sqrt((double)read1<T>(c, sl + S_RES)) / nb;
     }
-    stage_out<T>(c, x_out, x, n, dev);
+    stage_out_n<T>(c, x_out, x, n, dev, po);
     if (err_out) std::memcpy(err_out, err.data(), sizeof(double) * nit);
     if (res_out) std::memcpy(res_out, res.data(), sizeof(double) * nit);
     if (niters) *niters = nit;
@@ -541,13 +575,14 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
            double* ar_out, int* iters) {
     check_dims(A, At);
     HGM_REQUIRE(At != nullptr, "At is NULL");
+    const PixOrder po = n_order(c, A, At);
     HGM_REQUIRE(b_in != nullptr, "b is required");
     const bool dev = o && (o->flags & HGM_DEVICE_PTRS);
     const int64_t m = A->rows, n = A->cols;
     if (maxit <= 0) maxit = (int)std::min<int64_t>(m, n);                    // :5 default min(m,n)
     HGM_REQUIRE(maxit >= 1, "maxit must be >= 1");
     const T* b = stage_in<T>(c, "in_b", b_in, m, dev);
-    const T* xt = stage_in<T>(c, "in_xt", xt_in, n, dev);
+    const T* xt = stage_in_n<T>(c, "in_xt", xt_in, n, dev, po);
     T* x = c->buf<T>("x", n + 1);
     T* v = c->buf<T>("v", n + 1);
     T* h = c->buf<T>("h", n + 1);
@@ -636,7 +671,7 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     }
     if (k == maxit) k = maxit - 1;
     const int nit = k + 1;
-    stage_out<T>(c, x_out, x, n, dev);
+    stage_out_n<T>(c, x_out, x, n, dev, po);
     if (err_out) std::memcpy(err_out, err.data(), sizeof(double) * nit);
     if (res_out) std::memcpy(res_out, res.data(), sizeof(double) * nit);
     if (ar_out) std::memcpy(ar_out, ar.data(), sizeof(double) * nit);
@@ -652,6 +687,7 @@ int hybrid_lsmr(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* 
                 double* res_out, int* niters) {
     check_dims(A, At);
     HGM_REQUIRE(At != nullptr, "At is NULL");
+    const PixOrder po = n_order(c, A, At);
     HGM_REQUIRE(A->dtype == HGM_F64, "hybrid LSMR is fp64");
     HGM_REQUIRE(b_in != nullptr && xt_in != nullptr, "b and x_true are required");
     HGM_REQUIRE(maxit >= 1, "maxit must be >= 1");
@@ -660,7 +696,7 @@ int hybrid_lsmr(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* 
     const int64_t m = A->rows, n = A->cols;
     const int64_t ldv = round_up(n > 0 ? n : 1, 64);
     const T* b = stage_in<T>(c, "in_b", b_in, m, dev);
-    const T* xt = stage_in<T>(c, "in_xt", xt_in, n, dev);
+    const T* xt = stage_in_n<T>(c, "in_xt", xt_in, n, dev, po);
     T* V = c->buf<T>("Q", (size_t)ldv * maxit);
     T* x = c->buf<T>("x", n + 1);
     T* u = c->buf<T>("u", m + 1);
@@ -739,7 +775,7 @@ int hybrid_lsmr(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* 
     }
     if (k == maxit) k = maxit - 1;
     const int nit = k + 1;
-    stage_out<T>(c, x_out, x, n, dev);
+    stage_out_n<T>(c, x_out, x, n, dev, po);
     if (err_out) std::memcpy(err_out, err.data(), sizeof(double) * nit);
     if (res_out) std::memcpy(res_out, res.data(), sizeof(double) * nit);
     if (niters) *niters = nit;
@@ -753,6 +789,7 @@ int arnoldi(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b_in, 
             double btol, int orth, double* H_out, double* beta_out, int* kdone) {
     check_dims(A, B);
     HGM_REQUIRE(B != nullptr, "B is NULL");
+    (void)n_order(c, A, B);   // H does not depend on the stored pixel order (up to rounding)
     HGM_REQUIRE(A->dtype == HGM_F64, "Arnoldi is fp64");
     HGM_REQUIRE(kg >= 1, "k must be >= 1");
     using T = double;

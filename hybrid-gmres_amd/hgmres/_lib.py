@@ -55,6 +55,9 @@ _SIGS = {
     "hgm_mat_create_csc": (c_int, [c_void_p, c_int64, c_int64, c_int64, ip64, ip64, dp, c_int, P(c_void_p)]),
     "hgm_mat_transpose": (c_int, [c_void_p, c_void_p, P(c_void_p)]),
     "hgm_mat_create_siddon": (c_int, [c_void_p, c_int, c_int, c_double, c_int, P(c_void_p)]),
+    "hgm_mat_create_siddon_ordered": (c_int, [c_void_p, c_int, c_int, c_double, c_int, c_int, c_int,
+                                              P(c_void_p)]),
+    "hgm_mat_order": (c_int, [c_void_p, c_int, P(c_int), P(c_int), P(c_int)]),
     "hgm_mat_info": (c_int, [c_void_p, ip64, ip64, ip64, P(c_int)]),
     "hgm_mat_tune": (c_int, [c_void_p, c_int, c_int]),
     "hgm_mat_set_bands": (c_int, [c_void_p, c_void_p, c_int64, c_int]),

@@ -140,6 +140,15 @@ def default_context() -> Context:
         return _default_ctx
 
 
+def auto_pixel_order(N):
+    """Stored pixel order for an N x N image: 4 x 4 tiles (one 128-B
+    line of fp64 per tile) whenever 4 | N, inside 256 x 256 super-blocks (the x-slice one
+    column band keeps in L2) from N = 2048 up.  Returns (tile, super_block)."""
+    tile = 4 if N % 4 == 0 else 1
+    sup = 256 if (N >= 2048 and N % 256 == 0 and tile > 1) else 0
+    return tile, sup
+
+
 class SparseOperator:
     """A CSR operator resident in HBM (``hgm_mat``)."""
 
@@ -182,14 +191,28 @@ class SparseOperator:
         return cls(ctx, h, M.shape, int(M.nnz), dtype)
 
     @classmethod
-    def siddon(cls, N, n_angles, ctx: Context | None = None, dtype=L.HGM_F64, det_offset=None):
-        """Parallel-beam projector generated on the device."""
+    def siddon(cls, N, n_angles, ctx: Context | None = None, dtype=L.HGM_F64, det_offset=None,
+               order="auto"):
+        """Parallel-beam projector generated on the device.
+
+        ``order`` is the STORED pixel order (invisible at the boundary: products,
+        downloads and solves use the reference column-major ``x(:)``): ``"reference"``,
+        ``(tile, super_block)``, or ``"auto"`` = :func:`auto_pixel_order`."""
         from .problems import DETECTOR_OFFSET
         ctx = ctx or default_context()
         off = DETECTOR_OFFSET if det_offset is None else det_offset
+        tile, sup = auto_pixel_order(N) if order == "auto" else ((1, 0) if order == "reference" else order)
         h = C.c_void_p()
-        _check(L.load().hgm_mat_create_siddon(ctx.handle, N, n_angles, off, dtype, C.byref(h)), ctx)
+        _check(L.load().hgm_mat_create_siddon_ordered(ctx.handle, N, n_angles, off, dtype, int(tile), int(sup),
+                                                      C.byref(h)), ctx)
         return cls._wrap(ctx, h)
+
+    def pixel_order(self, which="cols"):
+        """(N, tile, super_block) of the stored row/column index order; N = 0: reference order."""
+        n_, t_, s_ = C.c_int(), C.c_int(), C.c_int()
+        _check(L.load().hgm_mat_order(self._h, 0 if which == "rows" else 1, C.byref(n_), C.byref(t_),
+                                      C.byref(s_)), self.ctx)
+        return n_.value, t_.value, s_.value
 
     @classmethod
     def _wrap(cls, ctx, h):

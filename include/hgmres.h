@@ -117,6 +117,17 @@ HGM_API int hgm_mat_transpose(hgm_ctx* ctx, const hgm_mat* in, hgm_mat** out);
  * bit-compatible geometry with hgmres.problems.siddon_projector). */
 HGM_API int hgm_mat_create_siddon(hgm_ctx* ctx, int N, int n_angles, double det_offset,
                                   int dtype, hgm_mat** out);
+/* The same operator with its N x N pixel (column) space STORED in a tiled order: tile x tile
+ * tiles (4 x 4 fp64 = one 128-B line) inside super x super blocks (0 = none).  This is
+ * invisible at the boundary: hgm_spmv, hgm_mat_download and every solver take and return
+ * vectors and indices in the reference's column-major x(:) order; the permutation is
+ * applied once per vector on the way in and out.  Transposes inherit it (rows of A').
+ * tile must divide N (and super); super must divide N. */
+HGM_API int hgm_mat_create_siddon_ordered(hgm_ctx* ctx, int N, int n_angles, double det_offset,
+                                          int dtype, int tile, int super_block, hgm_mat** out);
+/* Stored order of the row (which = 0) or column (which = 1) index space: N = 0 means the
+ * reference order. */
+HGM_API int hgm_mat_order(const hgm_mat* mat, int which, int* N, int* tile, int* super_block);
 HGM_API int hgm_mat_info(const hgm_mat* mat, int64_t* rows, int64_t* cols, int64_t* nnz, int* dtype);
 /* SpMV kernel selection for this operator (tuning/benchmark hook): variant bits
  * 1 = 16-byte paired loads, 2 = nontemporal val/col loads, 4 = XCD-aware row-block

@@ -75,7 +75,7 @@ def main():
     lib = L.load()
     ctx = hgmres.Context(0)
     N, na = CONFIGS[cfg]
-    A0 = hgmres.SparseOperator.siddon(N, na, ctx=ctx).to_scipy().tocsc()
+    A0 = hgmres.SparseOperator.siddon(N, na, ctx=ctx, order="reference").to_scipy().tocsc()
     orders = {"colmajor": np.arange(N * N)}
     for T in (2, 4, 8, 16):
         orders[f"tile{T}"] = tile_perm(N, T)

@@ -1,7 +1,8 @@
 """Run a few SpMV launches per (operator, variant, group) — the target of rocprofv3
 PMC passes (FETCH_SIZE / WRITE_SIZE / TCC_HIT / TCC_MISS) in scripts/profile_spmv.sh.
 Prints the launch order so counter rows can be matched to cases.
-usage: python scripts/spmv_once.py CFG [A:v:g ...] [--reps 3]
+usage: python scripts/spmv_once.py CFG [A:v:g[:band_w:band_group] ...] [--reps 3]
+(stored pixel order of the generated operator: env HGM_SIDDON_TILE / HGM_SIDDON_SUPER)
 """
 import ctypes as C
 import os
@@ -27,7 +28,8 @@ def main():
     lib = L.load()
     ctx = hgmres.Context(0)
     N, na = CONFIGS[cfg]
-    A = hgmres.SparseOperator.siddon(N, na, ctx=ctx)
+    order = (int(os.environ.get("HGM_SIDDON_TILE", "1")), int(os.environ.get("HGM_SIDDON_SUPER", "0")))
+    A = hgmres.SparseOperator.siddon(N, na, ctx=ctx, order=order)
     B = A.T
     ops = {"A": A, "B": B}
     bufs = {}
@@ -40,8 +42,11 @@ def main():
         lib.hgm_memcpy_h2d(ctx.handle, xd, ones.ctypes.data_as(C.c_void_p), 8 * cols)
         bufs[nm] = (xd, yd)
     for case in cases:
-        nm, v, g = case.split(":")
+        parts = case.split(":")
+        nm, v, g = parts[:3]
         M = ops[nm]
+        if len(parts) >= 5:                      # A:variant:group:band_width:band_group
+            M.set_bands(int(parts[3]), int(parts[4]))
         M.tune(int(v), int(g))
         xd, yd = bufs[nm]
         for _ in range(reps):

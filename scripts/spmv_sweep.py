@@ -40,13 +40,16 @@ def main():
     ap.add_argument("configs", nargs="*", default=["c2", "c3", "c4"])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--tiles", default="1", help="comma list of stored pixel orders tile[:super_block]")
     a = ap.parse_args()
     lib = L.load()
     ctx = hgmres.Context(0)
-    for cfg in a.configs:
+    for cfg, tile in [(c, t) for c in a.configs for t in a.tiles.split(",")]:
+        tt, _, ss = tile.partition(":")
+        sup = int(ss or 0)
         N, na = CONFIGS[cfg]
         t0 = time.time()
-        A = hgmres.SparseOperator.siddon(N, na, ctx=ctx)
+        A = hgmres.SparseOperator.siddon(N, na, ctx=ctx, order=(int(tt), sup))
         B = A.T
         ctx.synchronize()
         gen_s = time.time() - t0
@@ -58,7 +61,15 @@ def main():
             ones = np.ones(cols)
             lib.hgm_memcpy_h2d(ctx.handle, xd, ones.ctypes.data_as(C.c_void_p), 8 * cols)
             # (band_width, band_group, group (rows kernel) or stream-reduction lanes, variant)
-            if name == "A":
+            if name == "A" and a.quick and sup:
+                cases = [(0, 0, 32, 1)]
+                for w in (sup * sup, 2 * sup * sup, 4 * sup * sup):
+                    if w < cols:
+                        cases += [(w, 8, 32, 8), (w, 8, 16, 8), (w, 16, 0, 1)]
+            elif name == "A" and a.quick:
+                cases = [(0, 0, 32, 1), (0, 0, 64, 1), (0, 0, 32, 8)]
+                cases += [(w, 8, 32, 8) for w in (1 << 17, 1 << 19, 1 << 21) if w < cols]
+            elif name == "A":
                 widths = [0] + ([w for w in (1 << 17, 1 << 18, 1 << 19, 1 << 20) if w < cols])
                 cases = []
                 for w in widths:
@@ -66,6 +77,8 @@ def main():
                         cases += [(0, 0, 32, 1), (0, 0, 32, 3), (0, 0, 32, 8), (0, 0, 64, 8), (0, 0, 64, 10)]
                     else:
                         cases += [(w, 8, 0, 1), (w, 8, 8, 8), (w, 8, 16, 8), (w, 8, 32, 8), (w, 8, 16, 10)]
+            elif a.quick:
+                cases = [(0, 0, 8, 0), (0, 0, 4, 8), (0, 0, 8, 8)]
             else:
                 cases = [(0, 0, 8, 0), (0, 0, 8, 1), (0, 0, 4, 8), (0, 0, 8, 8), (0, 0, 16, 8), (0, 0, 8, 10)]
             cur_w = None
@@ -77,7 +90,7 @@ def main():
                     M.set_bands(w, bg)
                 M.tune(v, g if g else 0)
                 us, gbs = time_case(ctx, lib, M, xd, yd, a.reps)
-                print(json.dumps({"cfg": cfg, "op": name, "rows": rows, "cols": cols, "nnz": M.nnz,
+                print(json.dumps({"cfg": cfg, "tile": tile, "op": name, "rows": rows, "cols": cols, "nnz": M.nnz,
                                   "band_w": w, "band_group": bg, "group": g, "variant": v,
                                   "avg_us": round(us, 2), "GBps": round(gbs, 1), "gen_s": round(gen_s, 2)}),
                       flush=True)

@@ -195,15 +195,56 @@ def test_banded_spmv(gpu_ctx, P64, width, group):
     assert rel(xs, xr) < TOL
 
 
+@pytest.mark.parametrize("order", ["reference", "auto", (4, 16), (8, 32)])
 @pytest.mark.parametrize("N,na", [(24, 12), (64, 90), (128, 37), (512, 30)])
-def test_device_siddon_bitwise(gpu_ctx, N, na):
+def test_device_siddon_bitwise(gpu_ctx, N, na, order):
+    """Device generator == numpy generator, in every stored pixel order (the download maps
+    the stored column indices back to the reference x(:) order)."""
     from hgmres.problems import siddon_projector
+    if isinstance(order, tuple) and (N % order[1] or N % order[0]):
+        pytest.skip("order does not divide N")
     A = siddon_projector(N, na)
-    Ad = hgmres.SparseOperator.siddon(N, na, ctx=gpu_ctx).to_scipy()
+    Ad = hgmres.SparseOperator.siddon(N, na, ctx=gpu_ctx, order=order).to_scipy()
     assert Ad.shape == A.shape
     assert np.array_equal(Ad.indptr, A.indptr)
     assert np.array_equal(Ad.indices, A.indices)
     assert np.array_equal(Ad.data, A.data)
+
+
+@pytest.mark.parametrize("order", [(4, 0), (4, 16), (8, 32)])
+def test_pixel_order_invisible(gpu_ctx, order):
+    """A tiled stored order changes nothing at the boundary: the transposes download
+    identically, A*x and A'*u are bitwise equal (the row sums keep their entry order), and
+    the solvers return the reference-order x and histories of the reference-order operator
+    (MGS inner products then sum in another order: agreement to rounding)."""
+    N, na = 64, 45
+    R_ = hgmres.SparseOperator.siddon(N, na, ctx=gpu_ctx, order="reference")
+    Tt = hgmres.SparseOperator.siddon(N, na, ctx=gpu_ctx, order=order)
+    assert Tt.pixel_order("cols") == (N, order[0], order[1]) and Tt.T.pixel_order("rows") == (N, order[0], order[1])
+    assert R_.pixel_order("cols")[0] == 0
+    Bt, Br = Tt.T.to_scipy(), R_.T.to_scipy()
+    assert np.array_equal(Bt.indptr, Br.indptr) and np.array_equal(Bt.indices, Br.indices)
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal(N * N)
+    u = rng.standard_normal(R_.shape[0])
+    assert np.array_equal(Tt @ x, R_ @ x)
+    assert np.array_equal(Tt.T @ u, R_.T @ u)
+    xt = rng.random(N * N)
+    b = R_ @ xt
+    for tag, fn, haslam in GM:
+        args = (1e-2,) if haslam else ()
+        o1 = fn(R_, R_.T, b, xt, 0.0, 15, *args, ctx=gpu_ctx, return_H=True)
+        o2 = fn(Tt, Tt.T, b, xt, 0.0, 15, *args, ctx=gpu_ctx, return_H=True)
+        assert o1[3] == o2[3], tag
+        H_ok(o2[-1], o1[-1], 1e-12)
+        assert rel(o2[0], o1[0]) < 1e-12, tag
+        hist_ok(o2[1], o1[1], 1e-12)
+        hist_ok(o2[2], o1[2], 1e-12)
+    l1 = hgmres.lsqr_solver(R_, b, xt, 0.0, 10, ctx=gpu_ctx)
+    l2 = hgmres.lsqr_solver(Tt, b, xt, 0.0, 10, ctx=gpu_ctx)
+    assert rel(l2[0], l1[0]) < 1e-9
+    with pytest.raises(ValueError):
+        hgmres.hybrid_ba_gmres_rtp(Tt, R_.T, b, xt, 0.0, 3, 1e-2, ctx=gpu_ctx)   # mixed pixel orders
 
 
 def test_device_transpose_bitwise(gpu_ctx, P64):
