@@ -152,7 +152,12 @@ namespace hgm {
 // SpMV kernel variants (bit flags): 16-byte paired loads, nontemporal val/col loads,
 // XCD-aware row-block order, nnz-balanced streaming (chunked) kernel.
 enum SpmvVariant { SPMV_VEC = 1, SPMV_NT = 2, SPMV_XCD = 4, SPMV_STREAM = 8 };
-constexpr int SCH = 2048;   // entries per streaming chunk (256 threads x 8)
+// entries per streaming chunk (256 threads x 16): C4 sweep, 2048 -> 4096 took A from
+// 2.90 to 2.48 ms and B from 2.78 to 2.47 ms (profiles/r1_spmv_sweep_c4_sch.jsonl)
+#ifndef HGM_SCH
+#define HGM_SCH 4096
+#endif
+constexpr int SCH = HGM_SCH;
 
 struct SegIndex {
     int64_t nnz, nseg, nchunks;

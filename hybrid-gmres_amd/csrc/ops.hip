@@ -135,18 +135,22 @@ void finalize_operator(hgm_ctx* c, hgm_mat* M) {
     set_bands(c, M, auto_band_width(M));
     if (avg >= 64) {
         if (M->nbands > 1) {
-            M->variant = SPMV_STREAM;
-            // super-block pixel order: a band segment is a short ray chord through a compact
-            // block -> 16 lanes per segment (C4 sweep, profiles/r1_spmv_sweep_c4_order.jsonl)
-            M->bsgroup = M->col_order.super > 1 ? 16 : 32;
+            // band segments are short ray chords (tens to hundreds of entries): 4 lanes per
+            // segment keeps every lane busy; with the super-block order the wider bands also
+            // gain from nontemporal val/col loads (C4 sweeps, profiles/r1_spmv_sweep_c4_*.jsonl:
+            // 2.90 ms vs 3.31 ms at 16 lanes; reference order 2.96 ms vs 4.18 ms at 32 lanes)
+            M->variant = SPMV_STREAM | SPMV_NT;
+            M->bsgroup = 4;
         } else {
             M->variant = SPMV_VEC;
             M->group = 32;
         }
     } else {
         if (M->nnz >= 50000000) {
-            M->variant = SPMV_STREAM;
-            M->sgroup = avg < 16 ? 4 : 8;
+            // C3/C4 sweeps: 4 lanes per row with nontemporal val/col loads is best for the
+            // ~60-entry pixel rows (C4 2.75 ms = 4.48 TB/s, C3 240 us = 5.35 TB/s)
+            M->variant = SPMV_STREAM | SPMV_NT;
+            M->sgroup = 4;
         } else {
             M->variant = 0;
             M->group = avg >= 6 ? 8 : 4;
@@ -162,8 +166,8 @@ int64_t auto_band_width(const hgm_mat* M) {
     if ((double)M->cols * vs <= 4.0 * 1024 * 1024) return 0;
     // only long-row operators benefit (the short pixel-major rows of B gather an L2-resident y)
     if (M->rows > 0 && (double)M->nnz / (double)M->rows < 64) return 0;
-    // super-block pixel order: 256 Ki pixels (a few compact blocks, 2 MiB fp64 x-slice)
-    if (M->col_order.super > 1) return (int64_t)(1 << 18);
+    // tiled pixel order: 256 Ki pixels (2 MiB fp64 x-slice: compact tile strips / blocks)
+    if (!M->col_order.trivial()) return (int64_t)(1 << 18);
     return (int64_t)(1 << 17);   // 128 Ki pixels = 1 MiB fp64 x-slice per band
 }
 

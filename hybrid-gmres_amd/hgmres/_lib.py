@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhgmres.so")
+LIB_PATH = os.environ.get("HGM_LIB") or os.path.join(_HERE, "libhgmres.so")   # HGM_LIB: experiment builds
 
 HGM_OK = 0
 HGM_E_ARG = -1

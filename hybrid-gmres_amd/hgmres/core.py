@@ -142,11 +142,10 @@ def default_context() -> Context:
 
 def auto_pixel_order(N):
     """Stored pixel order for an N x N image: 4 x 4 tiles (one 128-B
-    line of fp64 per tile) whenever 4 | N, inside 256 x 256 super-blocks (the x-slice one
-    column band keeps in L2) from N = 2048 up.  Returns (tile, super_block)."""
-    tile = 4 if N % 4 == 0 else 1
-    sup = 256 if (N >= 2048 and N % 256 == 0 and tile > 1) else 0
-    return tile, sup
+    line of fp64 per tile) whenever 4 | N.  Super-blocks (a second tiling level) are
+    supported but measured no better once the banded kernel runs 4 lanes per segment
+    (profiles/r1_spmv_sweep_c4_order.jsonl).  Returns (tile, super_block)."""
+    return (4 if N % 4 == 0 else 1), 0
 
 
 class SparseOperator:

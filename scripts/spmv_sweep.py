@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--tiles", default="1", help="comma list of stored pixel orders tile[:super_block]")
+    ap.add_argument("--cases", default="", help="comma list band_w:band_group:group:variant (only --ops)")
+    ap.add_argument("--ops", default="A", help="operators the --cases apply to (A, B or AB)")
     a = ap.parse_args()
     lib = L.load()
     ctx = hgmres.Context(0)
@@ -61,7 +63,11 @@ def main():
             ones = np.ones(cols)
             lib.hgm_memcpy_h2d(ctx.handle, xd, ones.ctypes.data_as(C.c_void_p), 8 * cols)
             # (band_width, band_group, group (rows kernel) or stream-reduction lanes, variant)
-            if name == "A" and a.quick and sup:
+            if a.cases and name in a.ops:
+                cases = [tuple(int(v) for v in cs.split(":")) for cs in a.cases.split(",")]
+            elif a.cases:
+                continue
+            elif name == "A" and a.quick and sup:
                 cases = [(0, 0, 32, 1)]
                 for w in (sup * sup, 2 * sup * sup, 4 * sup * sup):
                     if w < cols:
