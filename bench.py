@@ -33,11 +33,16 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
+# cpu_iters: iterations of the oracle timed for cpu_baseline (a bounded 10-30 s sample)
 WORKLOADS = {
-    "c2": dict(N=512, angles=30, solver="hybrid_ab_gmres_rtp", maxit=20, lam=1e-2),
-    "c3": dict(N=2048, angles=19, solver="hybrid_ba_gmres_rtp", maxit=20, lam=1e-2),
-    "c4": dict(N=4096, angles=47, solver="ABgmres_nonhybrid_bounds", maxit=20, lam=0.0),
+    "c2": dict(N=512, angles=30, solver="hybrid_ab_gmres_rtp", maxit=20, lam=1e-2, cpu_iters=20),
+    "c3": dict(N=2048, angles=19, solver="hybrid_ba_gmres_rtp", maxit=20, lam=1e-2, cpu_iters=3),
+    "c4": dict(N=4096, angles=47, solver="ABgmres_nonhybrid_bounds", maxit=20, lam=0.0, cpu_iters=1),
+    # BASELINE configs[4]: the Golub-Kahan path on the 4096^2 operator in fp32
+    "c5": dict(N=4096, angles=47, solver="lsqr_solver", maxit=20, lam=0.0, f32=True, cpu_iters=1),
+    "c5m": dict(N=4096, angles=47, solver="lsmr_solver", maxit=20, lam=0.0, f32=True, cpu_iters=1),
 }
+UNITS = {"lsqr_solver": "LSQR iters/s", "lsmr_solver": "LSMR iters/s"}
 
 
 def parse():
@@ -59,12 +64,16 @@ def build_problem(ctx, wl, seed):
     """A generated on the device (bit-identical to hgmres.problems.siddon_projector),
     B = A' by the device transpose, b = A x_true + noise."""
     import hgmres
+    from hgmres import _lib as L
     from hgmres.problems import shepp_logan
     N, na = wl["N"], wl["angles"]
     A = hgmres.SparseOperator.siddon(N, na, ctx=ctx)
-    B = A.T
     x_true = shepp_logan(N).ravel(order="F")
-    b_exact = A @ x_true
+    b_exact = A @ x_true                      # fp64 data even for the fp32 operator
+    if wl.get("f32"):
+        A.close()
+        A = hgmres.SparseOperator.siddon(N, na, ctx=ctx, dtype=L.HGM_F32)
+    B = A.T
     rng = np.random.default_rng(seed)
     e = rng.standard_normal(A.shape[0])
     e = e / np.linalg.norm(e) * 1e-2 * np.linalg.norm(b_exact)
@@ -105,7 +114,8 @@ def main():
     o.H_out = None
     lib = L.load()
     dptr = lambda t: C.cast(C.c_void_p(t.data_ptr()), L.dp)   # noqa: E731
-    ep, rp = err.ctypes.data_as(L.dp), res.ctypes.data_as(L.dp)
+    arh = np.zeros(maxit)                      # lsmr_solver's ar_hist
+    ep, rp, aph = err.ctypes.data_as(L.dp), res.ctypes.data_as(L.dp), arh.ctypes.data_as(L.dp)
 
     def step():
         if wl["solver"] == "hybrid_ab_gmres_rtp":
@@ -114,6 +124,12 @@ def main():
         elif wl["solver"] == "hybrid_ba_gmres_rtp":
             rc = lib.hgm_hybrid_ba_gmres_rtp_ex(ctx.handle, C.byref(o), A._h, B._h, dptr(b_d), dptr(xt_d), 0.0,
                                                 maxit, lam, dptr(x_d), ep, rp, C.byref(it))
+        elif wl["solver"] == "lsqr_solver":        # B = A' is the transpose operand At
+            rc = lib.hgm_lsqr_solver_ex(ctx.handle, C.byref(o), A._h, B._h, dptr(b_d), dptr(xt_d), 0.0, maxit,
+                                        dptr(x_d), ep, rp, C.byref(it))
+        elif wl["solver"] == "lsmr_solver":
+            rc = lib.hgm_lsmr_solver_ex(ctx.handle, C.byref(o), A._h, B._h, dptr(b_d), dptr(xt_d), 0.0, maxit,
+                                        dptr(x_d), ep, rp, aph, C.byref(it))
         else:
             rc = lib.hgm_gmres_bounds_ex(ctx.handle, C.byref(o), A._h, B._h, dptr(b_d), dptr(xt_d), 0.0, maxit,
                                          lam, L.HGM_SIDE_AB, 0, dptr(x_d), ep, rp, C.byref(it))
@@ -173,13 +189,13 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(A, B, b, x_true, wl, args.cpu_iters)
+        cpu = cpu_baseline(A, B, b, x_true, wl, args.cpu_iters or wl["cpu_iters"])
 
     if rank == 0:
         line = {
             "metric": "GMRES iters/sec + SpMV GB/s (% HBM roofline), 2-D phantom A, 1/2/4/8 GPU",
             "value": round(value, 3),
-            "unit": "GMRES iters/s",
+            "unit": UNITS.get(wl["solver"], "GMRES iters/s"),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -187,7 +203,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f32" if wl.get("f32") else "f64",
             "data": "synthetic (Siddon parallel-beam A generated on device, Shepp-Logan phantom, 1% noise)",
             "config": {
                 "workload": f"{args.workload}: {wl['solver']} {wl['N']}x{wl['N']} phantom, {wl['angles']} angles, "
@@ -213,17 +229,23 @@ def cpu_baseline(A, B, b, x_true, wl, iters):
         from threadpoolctl import threadpool_limits
     except ImportError:   # pragma: no cover
         threadpool_limits = None
-    As, Bs = A.to_scipy(), B.to_scipy()
     maxit = iters or wl["maxit"]
     fn = getattr(R, wl["solver"])
-    args = (As, Bs, b, x_true, 0.0, maxit) + ((wl["lam"],) if wl["solver"] != "ABgmres_nonhybrid_bounds" else ())
+    gkb = wl["solver"] in UNITS
+    As = A.to_scipy()
+    if gkb:   # the restatement forms A' itself (lsqr_solver.m:10); fp64 arithmetic, fp32-rounded values
+        args = (As, b, x_true, 0.0, maxit)
+    else:
+        args = (As, B.to_scipy(), b, x_true, 0.0, maxit) + \
+            ((wl["lam"],) if wl["solver"] != "ABgmres_nonhybrid_bounds" else ())
     import contextlib
     with (threadpool_limits(limits=1) if threadpool_limits else contextlib.nullcontext()):
         t0 = time.perf_counter()
         out = fn(*args)
         dt = time.perf_counter() - t0
-    k = out[3]
-    return {"value": round(k / dt, 4), "unit": "GMRES iters/s", "cores": 1, "kind": "port",
+    k = out[-1] if wl["solver"] == "lsmr_solver" else out[3]
+    return {"value": round(k / dt, 4), "unit": UNITS.get(wl["solver"], "GMRES iters/s"), "cores": 1,
+            "kind": "port",
             "sample": f"oracle/restatement.py {wl['solver']} on the same {wl['N']}^2 operator, {k} iterations "
                       f"({dt:.1f} s, scipy CSR SpMV + numpy, 1 thread)"}
 

@@ -15,6 +15,8 @@ template <> struct V2<float> { using t = float2; };
 typedef double nd2 __attribute__((ext_vector_type(2)));
 typedef float nf2 __attribute__((ext_vector_type(2)));
 typedef int ni2 __attribute__((ext_vector_type(2)));
+typedef int ni4 __attribute__((ext_vector_type(4)));
+typedef float nf4 __attribute__((ext_vector_type(4)));
 template <typename T> struct NV2;
 template <> struct NV2<double> { using t = nd2; };
 template <> struct NV2<float> { using t = nf2; };

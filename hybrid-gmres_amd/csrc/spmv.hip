@@ -162,7 +162,22 @@ __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, c
     const int64_t c0 = k * SCH;
     const int64_t c1 = (c0 + SCH < nnz) ? c0 + SCH : nnz;
     const int n = (int)(c1 - c0);
-    if (n == SCH) {
+    if (n == SCH && sizeof(T) == 4) {
+        // fp32: four entries per lane per step (16-B value and 16-B index loads, both fully
+        // coalesced across the wave)
+#pragma unroll
+        for (int u = 0; u < SCH / (4 * BS); ++u) {
+            const int j = 4 * threadIdx.x + u * 4 * BS;
+            const ni4 cc = ld<NT>(reinterpret_cast<const ni4*>(ci + c0 + j));
+            const nf4 v = ld<NT>(reinterpret_cast<const nf4*>(val + c0 + j));
+            prod[j] = v.x * x[cc.x];
+            prod[j + 1] = v.y * x[cc.y];
+            prod[j + 2] = v.z * x[cc.z];
+            prod[j + 3] = v.w * x[cc.w];
+        }
+    } else if (n == SCH) {
+        // fp64: a pair per lane per step (16-B value loads; four entries per lane would leave
+        // every 16-B wave load half-coalesced: measured 17% slower at C4)
 #pragma unroll
         for (int u = 0; u < SCH / (2 * BS); ++u) {
             const int j = 2 * threadIdx.x + u * 2 * BS;
