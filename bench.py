@@ -54,6 +54,11 @@ def parse():
     ap.add_argument("--orth", default="mgs", choices=["mgs", "cgs2"])
     ap.add_argument("--explicit-residual", action="store_true",
                     help="monitor norm(b - A*x) with an explicit SpMV (default: b - (A*Q) y)")
+    ap.add_argument("--shard", action="store_true",
+                    help="N>1: one pixel-sharded solve over RCCL (strong scaling) instead of N replicas")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                    help="--shard transport: RCCL, or the host all-reduce hook (single-device emulation)")
+    ap.add_argument("--same-device", action="store_true", help="run every rank on GPU 0 (shard emulation)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP-event timing")
     ap.add_argument("--cpu-iters", type=int, default=0, help="oracle iterations for cpu_baseline (0 = maxit)")
@@ -80,6 +85,34 @@ def build_problem(ctx, wl, seed):
     return A, B, b_exact + e, x_true
 
 
+def build_shard(ctx, wl, rank, world):
+    """Rank `rank`'s pixel shard of the device-generated operator: B_g = B(P_g,:) by a
+    device row slice of B = A', A_g = A(:,P_g) as its device transpose; P_g contiguous,
+    balanced by nnz(A(:,P)) + nnz(B(P,:)) = 2 nnz(B(P,:)).  b (replicated) is formed from
+    the full operator before it is released.  Reference pixel order (shards are contiguous
+    reference-order pixel ranges)."""
+    import hgmres
+    from hgmres.problems import shepp_logan
+    N, na = wl["N"], wl["angles"]
+    Af = hgmres.SparseOperator.siddon(N, na, ctx=ctx, order="reference")
+    x_true = shepp_logan(N).ravel(order="F")
+    b_exact = Af @ x_true
+    rng = np.random.default_rng(0)                         # same noise on every rank
+    e = rng.standard_normal(Af.shape[0])
+    e = e / np.linalg.norm(e) * 1e-2 * np.linalg.norm(b_exact)
+    Bf = Af.T
+    cum = np.concatenate([[0], np.cumsum(np.diff(Bf.row_ptr()))]).astype(np.float64)
+    n = Af.shape[1]
+    bounds = [0] + [int(np.searchsorted(cum, cum[-1] * g / world)) for g in range(1, world)] + [n]
+    lo, hi = bounds[rank], bounds[rank + 1]
+    B_g = Bf.row_slice(lo, hi)
+    A_g = B_g.T
+    full = Af.shape
+    Af.close()
+    Bf.close()
+    return A_g, B_g, b_exact + e, x_true, (lo, hi), full
+
+
 def main():
     args = parse()
     import torch
@@ -89,6 +122,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    if args.same_device:
+        local = 0                      # shard emulation: every rank on GPU 0
     torch.cuda.set_device(local)
     import ctypes as C
     import hgmres
@@ -96,12 +131,21 @@ def main():
     from hgmres.core import _check
 
     wl = WORKLOADS[args.workload]
-    ctx = hgmres.Context(local)
-    A, B, b, x_true = build_problem(ctx, wl, seed=rank)
+    shard = args.shard and world > 1
+    if shard:
+        # one global problem, pixel-sharded: RCCL context (or the host
+        # all-reduce hook for the single-device emulation)
+        from hgmres.dist import host_allreduce_context, init_context
+        ctx = host_allreduce_context(local, rank, world) if args.comm == "host" else init_context(local, rank, world)
+        A, B, b, x_true, (lo, hi), full = build_shard(ctx, wl, rank, world)
+    else:
+        ctx = hgmres.Context(local)
+        A, B, b, x_true = build_problem(ctx, wl, seed=rank)
+        lo, hi, full = 0, A.shape[1], A.shape
     m, n = A.shape
     dev = torch.device("cuda", local)
     b_d = torch.from_numpy(b).to(dev)
-    xt_d = torch.from_numpy(x_true).to(dev)
+    xt_d = torch.from_numpy(np.ascontiguousarray(x_true[lo:hi])).to(dev)
     x_d = torch.zeros(n, dtype=torch.float64, device=dev)
     torch.cuda.synchronize()
     maxit, lam = wl["maxit"], wl["lam"]
@@ -169,7 +213,7 @@ def main():
                 kern[nm] = {"calls": calls, "avg_us": avg_s * 1e6, "bytes_per_launch": by / calls,
                             "GBps": by / calls / avg_s / 1e9, "total_ms": ms}
         ctx.kernel_timing(False)
-    iters = args.steps * maxit * world
+    iters = args.steps * maxit * (1 if shard else world)   # sharded: one global solve
     value = iters / dt
     roof = None
     spmv = {k: v for k, v in kern.items() if k.startswith("spmv")}
@@ -201,21 +245,26 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if shard else "weak",
             "vs_baseline": None,
             "dtype": "f32" if wl.get("f32") else "f64",
             "data": "synthetic (Siddon parallel-beam A generated on device, Shepp-Logan phantom, 1% noise)",
             "config": {
                 "workload": f"{args.workload}: {wl['solver']} {wl['N']}x{wl['N']} phantom, {wl['angles']} angles, "
-                            f"m={m}, n={n}, nnz(A)={A.nnz}, maxit={maxit}, tol=0, lambda={lam}, orth={args.orth}, "
+                            f"m={full[0]}, n={full[1]}, nnz(A)={A.nnz if not shard else 'sharded'}, maxit={maxit}, "
+                            f"tol=0, lambda={lam}, orth={args.orth}, "
                             f"residual={'explicit A*x' if args.explicit_residual else '(A*Q)*y'}",
-                "global_batch": world,
-                "parallelism": "replicas: one independent slice per GPU" if world > 1 else "single GPU",
+                "global_batch": 1 if shard else world,
+                "parallelism": (f"pixel-sharded over {world} ranks ({args.comm} all-reduce of the m-vector)"
+                                if shard else
+                                "replicas: one independent slice per GPU" if world > 1 else "single GPU"),
                 "step": f"one complete {maxit}-iteration solve",
             },
             "roofline": roof,
             "kernels": kern,
             "cpu_baseline": cpu,
+            # last solve's monitors (identical across ranks / sharding up to rounding)
+            "monitors": {"residual_norm_last": float(res[maxit - 1]), "error_norm_last": float(err[maxit - 1])},
         }
         print(json.dumps(line))
     if world > 1:

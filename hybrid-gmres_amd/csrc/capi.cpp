@@ -478,6 +478,17 @@ HGM_API int hgm_mat_create_siddon(hgm_ctx* c, int N, int n_angles, double det_of
     return HGM_OK;
 }
 
+HGM_API int hgm_mat_row_slice(hgm_ctx* c, const hgm_mat* in, int64_t lo, int64_t hi, hgm_mat** out) {
+    if (!c || !in || !out) return HGM_E_ARG;
+    *out = nullptr;
+    HGM_TRY(c, {
+        HGM_HIP(hipSetDevice(c->device));
+        *out = row_slice(c, in, lo, hi);
+        finalize_operator(c, *out);
+    });
+    return HGM_OK;
+}
+
 HGM_API int hgm_mat_create_siddon_ordered(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype, int tile,
                                           int super_block, hgm_mat** out) {
     if (!c || !out) return HGM_E_ARG;
@@ -536,9 +547,13 @@ static void mat_download_impl(hgm_ctx* c, const hgm_mat* M, int64_t* row_ptr, in
         HGM_HIP(hipSetDevice(c->device));
         // stored arrays (column indices mapped back to the reference order on the device)
         std::vector<int64_t> rp((size_t)M->rows + 1);
+        HGM_HIP(hipMemcpy(rp.data(), M->rp, sizeof(int64_t) * (M->rows + 1), hipMemcpyDeviceToHost));
+        if (!col_idx && !val && M->row_order.trivial()) {   // row pointers only (e.g. a shard plan)
+            if (row_ptr) std::memcpy(row_ptr, rp.data(), sizeof(int64_t) * (M->rows + 1));
+            return;
+        }
         std::vector<int32_t> ci((size_t)M->nnz);
         std::vector<double> vv((size_t)M->nnz);
-        HGM_HIP(hipMemcpy(rp.data(), M->rp, sizeof(int64_t) * (M->rows + 1), hipMemcpyDeviceToHost));
         if (M->nnz) {
             const int32_t* src = M->ci;
             if (!M->col_order.trivial()) {

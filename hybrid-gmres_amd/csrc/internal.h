@@ -224,6 +224,8 @@ template <typename T> void fro2(hgm_ctx* c, const hgm_mat* M, double* out_dev);
 hgm_mat* mat_alloc(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, int dtype);
 void mat_free(hgm_mat* M);
 hgm_mat* transpose(hgm_ctx* c, const hgm_mat* M);
+// rows [lo, hi) as a new operator (pixel shard B(P_g,:)); rows must be in the reference order
+hgm_mat* row_slice(hgm_ctx* c, const hgm_mat* M, int64_t lo, int64_t hi);
 // build / drop the column-banded copy (band_w <= 0 or >= cols drops it)
 void set_bands(hgm_ctx* c, hgm_mat* M, int64_t band_w);
 // chunk index of the nnz-balanced streaming kernel over the rows

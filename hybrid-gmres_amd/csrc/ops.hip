@@ -39,6 +39,38 @@ hgm_mat* mat_alloc(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, int dtyp
 
 static int grid_cap(int64_t n);
 
+__global__ __launch_bounds__(BS) void k_rebase(int64_t n, const int64_t* __restrict__ in, int64_t base,
+                                               int64_t* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = in[i] - base;
+}
+
+// rows [lo, hi) of M as a new operator (same columns): B_g = B(P_g,:) of a pixel shard
+hgm_mat* row_slice(hgm_ctx* c, const hgm_mat* M, int64_t lo, int64_t hi) {
+    HGM_REQUIRE(0 <= lo && lo <= hi && hi <= M->rows, "row_slice: need 0 <= lo <= hi <= rows");
+    HGM_REQUIRE(M->row_order.trivial(), "row_slice: rows must be stored in the reference order");
+    hipStream_t st = c->stream;
+    int64_t b[2];
+    HGM_HIP(hipMemcpy(&b[0], M->rp + lo, sizeof(int64_t), hipMemcpyDeviceToHost));
+    HGM_HIP(hipMemcpy(&b[1], M->rp + hi, sizeof(int64_t), hipMemcpyDeviceToHost));
+    hgm_mat* S = mat_alloc(c, hi - lo, M->cols, b[1] - b[0], M->dtype);
+    S->col_order = M->col_order;
+    try {
+        k_rebase<<<grid_cap(hi - lo + 1), BS, 0, st>>>(hi - lo + 1, M->rp + lo, b[0], S->rp);
+        HGM_HIP(hipGetLastError());
+        const size_t vs = M->dtype == HGM_F32 ? 4 : 8;
+        if (S->nnz) {
+            HGM_HIP(hipMemcpyAsync(S->ci, M->ci + b[0], sizeof(int32_t) * S->nnz, hipMemcpyDeviceToDevice, st));
+            HGM_HIP(hipMemcpyAsync(S->val, static_cast<const char*>(M->val) + vs * b[0], vs * S->nnz,
+                                   hipMemcpyDeviceToDevice, st));
+        }
+        HGM_HIP(hipStreamSynchronize(st));
+    } catch (...) {
+        mat_free(S);
+        throw;
+    }
+    return S;
+}
+
 // fo[k] = first segment starting at or after chunk k's first entry; fo[nchunks] = nseg
 __global__ void k_chunk_fo(int64_t nchunks, int64_t nseg, const int64_t* __restrict__ sp, int32_t* __restrict__ fo) {
     for (int64_t k = (int64_t)blockIdx.x * BS + threadIdx.x; k <= nchunks; k += (int64_t)gridDim.x * BS) {

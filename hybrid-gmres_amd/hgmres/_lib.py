@@ -58,6 +58,7 @@ _SIGS = {
     "hgm_mat_create_siddon_ordered": (c_int, [c_void_p, c_int, c_int, c_double, c_int, c_int, c_int,
                                               P(c_void_p)]),
     "hgm_mat_order": (c_int, [c_void_p, c_int, P(c_int), P(c_int), P(c_int)]),
+    "hgm_mat_row_slice": (c_int, [c_void_p, c_void_p, c_int64, c_int64, P(c_void_p)]),
     "hgm_mat_info": (c_int, [c_void_p, ip64, ip64, ip64, P(c_int)]),
     "hgm_mat_tune": (c_int, [c_void_p, c_int, c_int]),
     "hgm_mat_set_bands": (c_int, [c_void_p, c_void_p, c_int64, c_int]),
@@ -101,6 +102,14 @@ def load() -> C.CDLL:
             f"libhgmres.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(hipcc --offload-arch=gfx950).  There is no CPU fallback."
         )
+    # PyTorch-ROCm ships its own libamdhip64.so.7 / libhsa-runtime64.so.1 (same sonames as
+    # /opt/rocm's).  Whichever is loaded first serves the process; loading ours first and
+    # torch later leaves two HIP runtimes' state in the process and aborts at exit (double
+    # free).  So bind to torch's runtime when torch is present.
+    try:
+        import torch  # noqa: F401
+    except ImportError:   # pragma: no cover - torch is plumbing, not required
+        pass
     lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
     for name, (res, args) in _SIGS.items():
         f = getattr(lib, name)

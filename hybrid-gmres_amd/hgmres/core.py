@@ -240,6 +240,19 @@ class SparseOperator:
         M.has_sorted_indices = False
         return M
 
+    def row_ptr(self) -> np.ndarray:
+        """The CSR row pointers only (rows + 1 int64; e.g. the nnz weights of a shard plan)."""
+        rp = np.empty(self.shape[0] + 1, dtype=np.int64)
+        _check(L.load().hgm_mat_download(self.ctx.handle, self._h, rp.ctypes.data_as(L.ip64), None, None),
+               self.ctx)
+        return rp
+
+    def row_slice(self, lo: int, hi: int) -> "SparseOperator":
+        """Rows [lo, hi) as a new device operator (pixel shard ``B(P_g,:)``)."""
+        h = C.c_void_p()
+        _check(L.load().hgm_mat_row_slice(self.ctx.handle, self._h, int(lo), int(hi), C.byref(h)), self.ctx)
+        return SparseOperator._wrap(self.ctx, h)
+
     def tune(self, variant: int, group: int = 0):
         """Select the SpMV kernel variant (bits: 1 paired 16-B loads, 2 nontemporal,
         4 XCD-aware order) and lanes per row."""

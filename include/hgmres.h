@@ -113,6 +113,10 @@ HGM_API int hgm_mat_create_csc(hgm_ctx* ctx, int64_t rows, int64_t cols, int64_t
 /* Deterministic device transpose (stable: entries of each output row keep
  * increasing column order). */
 HGM_API int hgm_mat_transpose(hgm_ctx* ctx, const hgm_mat* in, hgm_mat** out);
+/* Rows [lo, hi) of `in` as a new device operator with the same columns (the pixel
+ * shard B_g = B(P_g,:) of SURVEY.md §8(e); A_g = A(:,P_g) is then hgm_mat_transpose of
+ * it).  `in`'s rows must be stored in the reference order. */
+HGM_API int hgm_mat_row_slice(hgm_ctx* ctx, const hgm_mat* in, int64_t lo, int64_t hi, hgm_mat** out);
 /* Parallel-beam Siddon projector generated on the device (ray-major CSR,
  * bit-compatible geometry with hgmres.problems.siddon_projector). */
 HGM_API int hgm_mat_create_siddon(hgm_ctx* ctx, int N, int n_angles, double det_offset,
