@@ -37,6 +37,10 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 WORKLOADS = {
     "c2": dict(N=512, angles=30, solver="hybrid_ab_gmres_rtp", maxit=20, lam=1e-2, cpu_iters=20),
     "c3": dict(N=2048, angles=19, solver="hybrid_ba_gmres_rtp", maxit=20, lam=1e-2, cpu_iters=3),
+    # BASELINE configs[2]: GCV lambda selection (k_gcv Arnoldi steps once, fminbnd on the
+    # cached H: analyze_regularization.m:39-46) + the BA-GMRES solve at the chosen lambda
+    "c3gcv": dict(N=2048, angles=19, solver="hybrid_ba_gmres_rtp", maxit=20, lam=1e-2, cpu_iters=3,
+                  gcv=dict(k=20, lo=1e-8, hi=1.0, tolx=1e-10)),
     "c4": dict(N=4096, angles=47, solver="ABgmres_nonhybrid_bounds", maxit=20, lam=0.0, cpu_iters=1),
     # BASELINE configs[4]: the Golub-Kahan path on the 4096^2 operator in fp32
     "c5": dict(N=4096, angles=47, solver="lsqr_solver", maxit=20, lam=0.0, f32=True, cpu_iters=1),
@@ -161,7 +165,25 @@ def main():
     arh = np.zeros(maxit)                      # lsmr_solver's ar_hist
     ep, rp, aph = err.ctypes.data_as(L.dp), res.ctypes.data_as(L.dp), arh.ctypes.data_as(L.dp)
 
+    gcv = wl.get("gcv")
+    if gcv:
+        kg = gcv["k"]
+        Hg = np.zeros((kg + 1) * kg)
+        beta_g, kdone, lam_c, g_c = C.c_double(), C.c_int(), C.c_double(), C.c_double()
+        o_orth = L.HGM_CGS2 if args.orth == "cgs2" else L.HGM_MGS
+    chosen = {}
+
     def step():
+        nonlocal lam
+        if gcv:
+            _check(lib.hgm_arnoldi(ctx.handle, A._h, B._h, b.ctypes.data_as(L.dp), kg, L.HGM_SIDE_BA, 1e-12, o_orth,
+                                   Hg.ctypes.data_as(L.dp), C.byref(beta_g), C.byref(kdone)), ctx)
+            rc = lib.hgm_gcv_fminbnd(Hg.ctypes.data_as(L.dp), kdone.value, beta_g.value, float(n), gcv["lo"],
+                                     gcv["hi"], gcv["tolx"], C.byref(lam_c), C.byref(g_c))
+            if rc != 0:
+                raise RuntimeError(f"hgm_gcv_fminbnd failed ({rc})")
+            lam = lam_c.value
+            chosen.update(lam=lam, gcv=g_c.value, k_gcv=kdone.value)
         if wl["solver"] == "hybrid_ab_gmres_rtp":
             rc = lib.hgm_hybrid_ab_gmres_rtp_ex(ctx.handle, C.byref(o), A._h, B._h, dptr(b_d), dptr(xt_d), 0.0,
                                                 maxit, lam, dptr(x_d), ep, rp, C.byref(it))
@@ -258,13 +280,17 @@ def main():
                 "parallelism": (f"pixel-sharded over {world} ranks ({args.comm} all-reduce of the m-vector)"
                                 if shard else
                                 "replicas: one independent slice per GPU" if world > 1 else "single GPU"),
-                "step": f"one complete {maxit}-iteration solve",
+                "step": (f"GCV lambda selection ({gcv['k']} Arnoldi steps + fminbnd on the cached H) and one "
+                         f"complete {maxit}-iteration solve at that lambda" if gcv else
+                         f"one complete {maxit}-iteration solve"),
             },
             "roofline": roof,
             "kernels": kern,
             "cpu_baseline": cpu,
             # last solve's monitors (identical across ranks / sharding up to rounding)
-            "monitors": {"residual_norm_last": float(res[maxit - 1]), "error_norm_last": float(err[maxit - 1])},
+            "monitors": {"residual_norm_last": float(res[maxit - 1]), "error_norm_last": float(err[maxit - 1]),
+                         **({"gcv_lambda": chosen["lam"], "gcv_value": chosen["gcv"], "k_gcv": chosen["k_gcv"]}
+                            if chosen else {})},
         }
         print(json.dumps(line))
     if world > 1:
