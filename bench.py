@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--orth", default="mgs", choices=["mgs", "cgs2"])
     ap.add_argument("--explicit-residual", action="store_true",
                     help="monitor norm(b - A*x) with an explicit SpMV (default: b - (A*Q) y)")
+    ap.add_argument("--unmatched", action="store_true",
+                    help="GMRES workloads: B = the unmatched pixel-driven back-projector instead of A'")
     ap.add_argument("--shard", action="store_true",
                     help="N>1: one pixel-sharded solve over RCCL (strong scaling) instead of N replicas")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
@@ -145,6 +147,9 @@ def main():
     else:
         ctx = hgmres.Context(local)
         A, B, b, x_true = build_problem(ctx, wl, seed=rank)
+        if args.unmatched and wl["solver"] not in UNITS:
+            B.close()
+            B = hgmres.SparseOperator.pixel_backprojector(wl["N"], wl["angles"], ctx=ctx, dtype=A.dtype)
         lo, hi, full = 0, A.shape[1], A.shape
     m, n = A.shape
     dev = torch.device("cuda", local)
@@ -270,7 +275,9 @@ def main():
             "scaling": "strong" if shard else "weak",
             "vs_baseline": None,
             "dtype": "f32" if wl.get("f32") else "f64",
-            "data": "synthetic (Siddon parallel-beam A generated on device, Shepp-Logan phantom, 1% noise)",
+            "data": "synthetic (Siddon parallel-beam A generated on device, Shepp-Logan phantom, 1% noise"
+                    + (", unmatched pixel-driven B" if args.unmatched and wl["solver"] not in UNITS else ", B = A'")
+                    + ")",
             "config": {
                 "workload": f"{args.workload}: {wl['solver']} {wl['N']}x{wl['N']} phantom, {wl['angles']} angles, "
                             f"m={full[0]}, n={full[1]}, nnz(A)={A.nnz if not shard else 'sharded'}, maxit={maxit}, "

@@ -500,6 +500,18 @@ HGM_API int hgm_mat_create_siddon_ordered(hgm_ctx* c, int N, int n_angles, doubl
     return HGM_OK;
 }
 
+HGM_API int hgm_mat_create_backprojector(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype, int tile,
+                                         int super_block, hgm_mat** out) {
+    if (!c || !out) return HGM_E_ARG;
+    *out = nullptr;
+    HGM_TRY(c, {
+        HGM_HIP(hipSetDevice(c->device));
+        *out = backprojector(c, N, n_angles, det_offset, dtype, tile, super_block);
+        finalize_operator(c, *out);
+    });
+    return HGM_OK;
+}
+
 HGM_API int hgm_mat_order(const hgm_mat* M, int which, int* N, int* tile, int* super_block) {
     if (!M || (which != 0 && which != 1)) return HGM_E_ARG;
     const PixOrder& o = which == 0 ? M->row_order : M->col_order;

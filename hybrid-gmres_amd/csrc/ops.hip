@@ -536,6 +536,107 @@ __global__ __launch_bounds__(BS) void k_siddon(int N, int p, int64_t m, const do
     }
 }
 
+// --------------------------------------------------------------------------
+// Unmatched pixel-driven back-projector (mirrors hgmres/problems.py::pixel_driven_backprojector,
+// the role of PRtomo_mismatched in run_2D_phantom.m:13-14): for every pixel centre and angle,
+// linear interpolation between the two nearest detector bins.  One thread per STORED pixel row
+// (the rows follow the pixel order, so B pairs with a tiled A); entries in increasing column.
+// --------------------------------------------------------------------------
+template <bool FILL, typename T>
+__global__ __launch_bounds__(BS) void k_backproj(int N, int p, int na, const double* __restrict__ cth,
+                                                 const double* __restrict__ sth, double doff, int tile, int super,
+                                                 int64_t* __restrict__ counts, const int64_t* __restrict__ rp,
+                                                 int32_t* __restrict__ ci, T* __restrict__ val) {
+    const int64_t n = (int64_t)N * N;
+    const double half = N / 2.0;
+    for (int64_t s = (int64_t)blockIdx.x * BS + threadIdx.x; s < n; s += (int64_t)gridDim.x * BS) {
+        int64_t r, c;
+        if (tile > 1 || super > 1) pixel_rc(N, tile, super, s, r, c);
+        else { r = s % N; c = s / N; }
+        const double xc = ((double)c - half) + 0.5;
+        const double yc = ((double)(N - 1 - r) - half) + 0.5;
+        const double mxc = -xc;
+        int64_t cnt = 0;
+        const int64_t o = FILL ? rp[s] : 0;
+        for (int a = 0; a < na; ++a) {
+            const double t0 = mxc * sth[a], t1 = yc * cth[a];
+            const double sa = t0 + t1;
+            const double df = (sa + (p - 1) / 2.0) - doff;
+            const double fd = floor(df);
+            const double w1 = df - fd, w0 = 1.0 - w1;
+            const int64_t d0 = (int64_t)fd;
+            if (d0 >= 0 && d0 < p && w0 > 0) {
+                if (FILL) { ci[o + cnt] = (int32_t)((int64_t)a * p + d0); val[o + cnt] = (T)w0; }
+                ++cnt;
+            }
+            if (d0 + 1 >= 0 && d0 + 1 < p && w1 > 0) {
+                if (FILL) { ci[o + cnt] = (int32_t)((int64_t)a * p + d0 + 1); val[o + cnt] = (T)w1; }
+                ++cnt;
+            }
+        }
+        if (!FILL) counts[s] = cnt;
+    }
+}
+
+hgm_mat* backprojector(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype, int tile, int super) {
+    HGM_REQUIRE(N > 0 && n_angles > 0, "backprojector: N and n_angles must be positive");
+    if (tile < 1) tile = 1;
+    if (super < 2) super = 0;
+    HGM_REQUIRE(N % tile == 0 && (super == 0 || (N % super == 0 && super % tile == 0)),
+                "backprojector: tile must divide N (and super), super must divide N");
+    hipStream_t st = c->stream;
+    const int p = (int)std::ceil(std::sqrt(2.0) * N);
+    const int64_t n = (int64_t)N * N, m = (int64_t)p * n_angles;
+    std::vector<double> cth(n_angles), sth(n_angles);
+    const double dth = M_PI / n_angles;
+    for (int a = 0; a < n_angles; ++a) {
+        const double th = (double)a * dth;
+        cth[a] = std::cos(th);
+        sth[a] = std::sin(th);
+    }
+    double *dc = nullptr, *ds = nullptr;
+    int64_t *counts = nullptr, *rp = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    hgm_mat* M = nullptr;
+    try {
+        HGM_HIP(hipMalloc(&dc, 8 * n_angles));
+        HGM_HIP(hipMalloc(&ds, 8 * n_angles));
+        HGM_HIP(hipMalloc(&counts, 8 * (n + 1)));
+        HGM_HIP(hipMalloc(&rp, 8 * (n + 1)));
+        HGM_HIP(hipMemcpyAsync(dc, cth.data(), 8 * n_angles, hipMemcpyHostToDevice, st));
+        HGM_HIP(hipMemcpyAsync(ds, sth.data(), 8 * n_angles, hipMemcpyHostToDevice, st));
+        HGM_HIP(hipMemsetAsync(counts, 0, 8 * (n + 1), st));
+        const int g = grid_cap(n);
+        k_backproj<false, double><<<g, BS, 0, st>>>(N, p, n_angles, dc, ds, det_offset, tile, super, counts, nullptr,
+                                                    nullptr, nullptr);
+        HGM_HIP(hipGetLastError());
+        HGM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, rp, (int)(n + 1), st));
+        HGM_HIP(hipMalloc(&tmp, tmp_bytes));
+        HGM_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, counts, rp, (int)(n + 1), st));
+        int64_t nnz = 0;
+        HGM_HIP(hipMemcpyAsync(&nnz, rp + n, 8, hipMemcpyDeviceToHost, st));
+        HGM_HIP(hipStreamSynchronize(st));
+        M = mat_alloc(c, n, m, nnz, dtype);
+        if (tile > 1 || super > 1) M->row_order = PixOrder{N, tile, super};
+        HGM_HIP(hipMemcpyAsync(M->rp, rp, 8 * (n + 1), hipMemcpyDeviceToDevice, st));
+        if (dtype == HGM_F32)
+            k_backproj<true, float><<<g, BS, 0, st>>>(N, p, n_angles, dc, ds, det_offset, tile, super, nullptr, M->rp,
+                                                      M->ci, (float*)M->val);
+        else
+            k_backproj<true, double><<<g, BS, 0, st>>>(N, p, n_angles, dc, ds, det_offset, tile, super, nullptr,
+                                                       M->rp, M->ci, (double*)M->val);
+        HGM_HIP(hipGetLastError());
+        HGM_HIP(hipStreamSynchronize(st));
+    } catch (...) {
+        (void)hipFree(dc); (void)hipFree(ds); (void)hipFree(counts); (void)hipFree(rp); (void)hipFree(tmp);
+        mat_free(M);
+        throw;
+    }
+    (void)hipFree(dc); (void)hipFree(ds); (void)hipFree(counts); (void)hipFree(rp); (void)hipFree(tmp);
+    return M;
+}
+
 hgm_mat* siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype, int tile, int super) {
     HGM_REQUIRE(N > 0 && n_angles > 0, "siddon: N and n_angles must be positive");
     if (tile < 1) tile = 1;

@@ -206,6 +206,21 @@ class SparseOperator:
                                                       C.byref(h)), ctx)
         return cls._wrap(ctx, h)
 
+    @classmethod
+    def pixel_backprojector(cls, N, n_angles, ctx: Context | None = None, dtype=L.HGM_F64, det_offset=None,
+                            order="auto"):
+        """Unmatched pixel-driven back-projector B (n x m) generated on the device, bit-identical
+        to :func:`hgmres.problems.pixel_driven_backprojector`.  ``order``: stored pixel (row)
+        order, as for :meth:`siddon` (pair it with an A of the same order)."""
+        from .problems import DETECTOR_OFFSET
+        ctx = ctx or default_context()
+        off = DETECTOR_OFFSET if det_offset is None else det_offset
+        tile, sup = auto_pixel_order(N) if order == "auto" else ((1, 0) if order == "reference" else order)
+        h = C.c_void_p()
+        _check(L.load().hgm_mat_create_backprojector(ctx.handle, N, n_angles, off, dtype, int(tile), int(sup),
+                                                     C.byref(h)), ctx)
+        return cls._wrap(ctx, h)
+
     def pixel_order(self, which="cols"):
         """(N, tile, super_block) of the stored row/column index order; N = 0: reference order."""
         n_, t_, s_ = C.c_int(), C.c_int(), C.c_int()

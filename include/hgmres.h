@@ -129,6 +129,13 @@ HGM_API int hgm_mat_create_siddon(hgm_ctx* ctx, int N, int n_angles, double det_
  * tile must divide N (and super); super must divide N. */
 HGM_API int hgm_mat_create_siddon_ordered(hgm_ctx* ctx, int N, int n_angles, double det_offset,
                                           int dtype, int tile, int super_block, hgm_mat** out);
+/* Unmatched pixel-driven back-projector B (n x m, pixel-major) generated on the device:
+ * for every pixel centre and angle, linear interpolation between the two nearest detector
+ * bins (bit-identical to hgmres.problems.pixel_driven_backprojector; the role of
+ * PRtomo_mismatched in run_2D_phantom.m:13-14).  tile/super_block: stored row (pixel) order,
+ * as for hgm_mat_create_siddon_ordered, so B pairs with an operator of the same order. */
+HGM_API int hgm_mat_create_backprojector(hgm_ctx* ctx, int N, int n_angles, double det_offset, int dtype,
+                                         int tile, int super_block, hgm_mat** out);
 /* Stored order of the row (which = 0) or column (which = 1) index space: N = 0 means the
  * reference order. */
 HGM_API int hgm_mat_order(const hgm_mat* mat, int which, int* N, int* tile, int* super_block);
