@@ -241,11 +241,22 @@ __global__ __launch_bounds__(BS) void k_finalize2(const T* __restrict__ parts, i
     if (threadIdx.x == 0) *(blockIdx.x == 0 ? out0 : out1) = r;
 }
 
-static int gemv_blocks(int64_t n) {
-    int64_t nb = ((n >> 1) + BS - 1) / BS;   // one row pair per lane ...
+static int gemv_blocks(int64_t n, int ppl = 1) {
+    const int64_t per = (int64_t)BS * ppl;
+    int64_t nb = ((n >> 1) + per - 1) / per;  // ppl row pairs per lane ...
     if (nb > MAX_PARTS) nb = MAX_PARTS;      // ... up to 1024 blocks, then grid-stride
     if (nb < 1) nb = 1;
     return (int)nb;
+}
+
+// row pairs per lane of the MGS passes (experiment hook HGM_MGS_PPL; default 1)
+static int mgs_ppl() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("HGM_MGS_PPL");
+        v = (e && std::atoi(e) > 0) ? std::atoi(e) : 1;
+    }
+    return v;
 }
 
 template <typename T>
@@ -395,7 +406,7 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist) {
     // One launch per pass: a dependent launch is the cheapest grid-wide exchange of the
     // block partials on gfx950 (2.6-2.9 us vs 3-25 us for in-kernel grid barriers,
     // scripts/barrier_bench.hip).
-    const int np = gemv_blocks(n);
+    const int np = gemv_blocks(n, mgs_ppl());
     T* P = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
     T* Pb[2] = {P, P + MAX_PARTS};
     T* v = Q + (int64_t)(kk + 1) * ldq;
