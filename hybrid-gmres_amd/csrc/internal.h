@@ -215,6 +215,13 @@ template <typename T> void lsqr_update(hgm_ctx* c, int64_t n, T* x, T* w, const 
 template <typename T>
 void lsmr_update(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, const T* v, T c_hbar, T c_x, T c_h,
                  bool first);
+// LSMR kept-product monitor step (kernels.hip: k_lsmr_mon): image of v_k = c1*p1 + c0*p0 (or
+// p1 if p0 == nullptr), then the h / hbar / x image recurrences; *out = ||rhs - image(x)||^2
+template <typename T>
+void lsmr_monitor(hgm_ctx* c, int64_t n, const T* p1, const T* p0, double c1, double c0, double* Ih, double* Ihb,
+                  double* Ix, const T* rhs, double f, double e, double cx, bool first, double* out);
+// out[i] = epi(in[i], a, z[i]) (out may alias z): the epilogue of an SpMV applied to its raw product
+template <typename T> void epilogue_to(hgm_ctx* c, int64_t n, const T* in, T* out, int epi, T a, const T* z);
 template <typename T> void fill(hgm_ctx* c, int64_t n, T* x, T v);
 template <typename T> void convert(hgm_ctx* c, int64_t n, const double* in, T* out);
 template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, double* out);

@@ -544,6 +544,60 @@ void lsmr_update(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, const T* v, T c_hba
     HGM_HIP(hipGetLastError());
 }
 
+// LSMR monitors from kept products.  The images of the LSMR vectors under A
+// and A'A follow the same recurrences as the vectors (lsmr_solver.m:61-67), fed by the raw
+// products the bidiagonalisation already forms:
+//   m-space: A*h_k = A*v_k - f*A*h_{k-1};  A*hbar_k = A*h_k - e*A*hbar_{k-1};  A*x_k = A*x_{k-1} + cx*A*hbar_k
+//   n-space: A'A*v_k = beta_{k+1} A'u_{k+1} + alpha_k A'u_k  (A*v_k = beta_{k+1} u_{k+1} + alpha_k u_k,
+//            lsmr_solver.m:34-36), then the same three updates for A'A*h, A'A*hbar, A'A*x.
+// r = b - A*x (:69) and A'r = A'b - A'A*x (:71) are then norms of kept vectors.  The images are
+// accumulated in fp64 for both value types.  parts[blk] = this block's sum of the squared
+// monitor vector.
+template <typename T, bool FIRST>
+__global__ __launch_bounds__(BS) void k_lsmr_mon(int64_t n, const T* __restrict__ p1, const T* __restrict__ p0,
+                                                 double c1, double c0, double* __restrict__ Ih,
+                                                 double* __restrict__ Ihb, double* __restrict__ Ix,
+                                                 const T* __restrict__ rhs, double f, double e, double cx,
+                                                 double* __restrict__ parts) {
+    __shared__ double sh[4];
+    double acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+        double iv;                                          // image of v_k
+        if (p0) { const double a = c1 * (double)p1[i], b = c0 * (double)p0[i]; iv = a + b; }
+        else iv = (double)p1[i];
+        double ih, ihb;
+        if (FIRST) { ih = iv; ihb = ih; }                  // h_0 = v_0 (:25), hbar_0 = h_0 (:62)
+        else {
+            const double q = f * Ih[i];
+            ih = iv - q;
+            const double w = e * Ihb[i];
+            ihb = ih - w;
+        }
+        const double s = cx * ihb;
+        const double ix = Ix[i] + s;
+        Ih[i] = ih;
+        Ihb[i] = ihb;
+        Ix[i] = ix;
+        const double d = (double)rhs[i] - ix;
+        acc += d * d;
+    }
+    const double tot = block_sum_all(acc, sh);
+    if (threadIdx.x == 0) parts[blockIdx.x] = tot;
+}
+
+template <typename T>
+void lsmr_monitor(hgm_ctx* c, int64_t n, const T* p1, const T* p0, double c1, double c0, double* Ih, double* Ihb,
+                  double* Ix, const T* rhs, double f, double e, double cx, bool first, double* out) {
+    const int np = parts_for(n);
+    double* parts = c->buf<double>("lsmr_mon_parts", MAX_PARTS);
+    if (first)
+        k_lsmr_mon<T, true><<<np, BS, 0, c->stream>>>(n, p1, p0, c1, c0, Ih, Ihb, Ix, rhs, f, e, cx, parts);
+    else
+        k_lsmr_mon<T, false><<<np, BS, 0, c->stream>>>(n, p1, p0, c1, c0, Ih, Ihb, Ix, rhs, f, e, cx, parts);
+    k_finalize<double><<<1, BS, 0, c->stream>>>(parts, np, out);
+    HGM_HIP(hipGetLastError());
+}
+
 template <typename T>
 __global__ __launch_bounds__(BS) void k_fill(int64_t n, T* x, T v) {
     for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) x[i] = v;
@@ -587,6 +641,8 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
     template void div_scalar<T>(hgm_ctx*, int64_t, const T*, T*, T);                           \
     template void lsqr_update<T>(hgm_ctx*, int64_t, T*, T*, const T*, T, T);                   \
     template void lsmr_update<T>(hgm_ctx*, int64_t, T*, T*, T*, const T*, T, T, T, bool);      \
+    template void lsmr_monitor<T>(hgm_ctx*, int64_t, const T*, const T*, double, double, double*, double*, \
+                                  double*, const T*, double, double, double, bool, double*);   \
     template void fill<T>(hgm_ctx*, int64_t, T*, T);                                           \
     template void convert<T>(hgm_ctx*, int64_t, const double*, T*);                            \
     template void convert_back<T>(hgm_ctx*, int64_t, const T*, double*);                       \

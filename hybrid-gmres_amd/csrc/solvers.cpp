@@ -617,22 +617,60 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     r0.go();
     const double nb = std::sqrt((double)hs[0]);
     const double nxt = xt ? std::sqrt((double)hs[1]) : 0.0;
+    // Monitors from kept products (default; HGM_EXPLICIT_RESIDUAL applies the two extra SpMVs
+    // of :69 and :71 instead): the raw products A*v_k and A'*u_{k+1} of the bidiagonalisation
+    // are kept, and the images A*x, A'A*x follow the x/h/hbar recurrences (lsmr_monitor).  The
+    // iterates u, v, x, h, hbar are the same bits either way (the epilogues below are the
+    // fused ones, applied as a separate pass).
+    const bool kept = !(o && (o->flags & HGM_EXPLICIT_RESIDUAL));
+    T *Av = nullptr, *Atu0 = nullptr, *Atu1 = nullptr, *Atb = nullptr;
+    double *Ihm = nullptr, *Ihbm = nullptr, *Ixm = nullptr, *Ihn = nullptr, *Ihbn = nullptr, *Ixn = nullptr;
+    double* dmon = reinterpret_cast<double*>(c->dscal) + 72;   // [||r||^2, ||A'r||^2]
+    if (kept) {
+        Av = c->buf<T>("lsmr_Av", m + 1);
+        Atu0 = c->buf<T>("lsmr_Atu0", n + 1);
+        Atu1 = c->buf<T>("lsmr_Atu1", n + 1);
+        Atb = c->buf<T>("lsmr_Atb", n + 1);
+        Ihm = c->buf<double>("lsmr_Ihm", m + 1);
+        Ihbm = c->buf<double>("lsmr_Ihbm", m + 1);
+        Ixm = c->buf<double>("lsmr_Ixm", m + 1);
+        Ihn = c->buf<double>("lsmr_Ihn", n + 1);
+        Ihbn = c->buf<double>("lsmr_Ihbn", n + 1);
+        Ixn = c->buf<double>("lsmr_Ixn", n + 1);
+        fill<double>(c, m, Ixm, 0.0);                                          // A*x_0 = 0
+        fill<double>(c, n, Ixn, 0.0);                                          // A'A*x_0 = 0
+        apply_B<T>(c, At, b, Atb, EPI_NONE, T(0), nullptr);                    // A'*b (once per solve)
+    }
     HGM_HIP(hipMemcpyAsync(u, b, sizeof(T) * m, hipMemcpyDeviceToDevice, c->stream));   // :10
     double beta = nb;                                                          // :11
     if (beta > 0) div_scalar<T>(c, m, u, u, (T)beta);                          // :12
-    apply_B<T>(c, At, u, v, EPI_NONE, T(0), nullptr);                          // :14
-    nsumsq<T>(c, n, v, sl + S_ALPHA);
+    T* v0 = kept ? Atu0 : v;                                                   // raw A'*u_0 kept
+    apply_B<T>(c, At, u, v0, EPI_NONE, T(0), nullptr);                         // :14
+    nsumsq<T>(c, n, v0, sl + S_ALPHA);
     double alpha = std::sqrt((double)read1<T>(c, sl + S_ALPHA));              // :15
-    if (alpha > 0) div_scalar<T>(c, n, v, v, (T)alpha);                        // :16
+    if (alpha > 0) div_scalar<T>(c, n, v0, v, (T)alpha);                       // :16
+    else if (kept) HGM_HIP(hipMemcpyAsync(v, v0, sizeof(T) * n, hipMemcpyDeviceToDevice, c->stream));
     double zetabar = alpha * beta, alphabar = alpha, rho = 1, rhobar = 1, cbar = 1, sbar = 0;   // :19-23
     HGM_HIP(hipMemcpyAsync(h, v, sizeof(T) * n, hipMemcpyDeviceToDevice, c->stream));   // :25
+    double prev_ch = 0.0;                                                      // (theta/rho) of the previous :67
     int k = 0;
     for (k = 0; k < maxit; ++k) {
-        apply_A<T>(c, A, v, u, EPI_SUB, (T)alpha, u);                          // :34 u = A*v - alpha*u
+        const double alpha_k = alpha;
+        if (kept) {
+            apply_A<T>(c, A, v, Av, EPI_NONE, T(0), nullptr);                  // A*v_k (kept)
+            epilogue_to<T>(c, m, Av, u, EPI_SUB, (T)alpha, u);                 // :34 u = A*v - alpha*u
+        } else {
+            apply_A<T>(c, A, v, u, EPI_SUB, (T)alpha, u);                      // :34 u = A*v - alpha*u
+        }
         sumsq<T>(c, m, u, sl + S_BETA);
         beta = std::sqrt((double)read1<T>(c, sl + S_BETA));                   // :35
         if (beta > 0) div_scalar<T>(c, m, u, u, (T)beta);                      // :36
-        apply_B<T>(c, At, u, v, EPI_SUB, (T)beta, v);                          // :38 v = A.'*u - beta*v
+        if (kept) {
+            apply_B<T>(c, At, u, Atu1, EPI_NONE, T(0), nullptr);               // A'*u_{k+1} (kept)
+            epilogue_to<T>(c, n, Atu1, v, EPI_SUB, (T)beta, v);                // :38 v = A.'*u - beta*v
+        } else {
+            apply_B<T>(c, At, u, v, EPI_SUB, (T)beta, v);                      // :38 v = A.'*u - beta*v
+        }
         nsumsq<T>(c, n, v, sl + S_ALPHA);
         alpha = std::sqrt((double)read1<T>(c, sl + S_ALPHA));                 // :39
         if (alpha > 0) div_scalar<T>(c, n, v, v, (T)alpha);                    // :40
@@ -653,19 +691,35 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         const double c_x = zeta / (rho * rhobar);                              // :66
         const double c_h = thetanew / rho;                                     // :67
         lsmr_update<T>(c, n, x, h, hbar, v, (T)c_hbar, (T)c_x, (T)c_h, k == 0);
-        apply_A<T>(c, A, x, r, EPI_RSUB, T(0), b);                             // :69 r = b - A*x
-        sumsq<T>(c, m, r, sl + S_RES);
-        apply_B<T>(c, At, r, atr, EPI_NONE, T(0), nullptr);                    // :71 A.'*r
-        nsumsq<T>(c, n, atr, sl + S_AR);
-        if (xt) nsumsq_diff<T>(c, n, x, xt, sl + S_ERR);
+        double mon[2] = {0.0, 0.0};
         Reader rr(c);
-        rr.add(&hs[0], sl + S_RES, sizeof(T));
-        rr.add(&hs[1], sl + S_AR, sizeof(T));
+        if (kept) {
+            // :69 ||b - A*x||^2 and :71 ||A'b - A'A*x||^2 from the kept images
+            lsmr_monitor<T>(c, m, Av, nullptr, 1.0, 0.0, Ihm, Ihbm, Ixm, b, prev_ch, c_hbar, c_x, k == 0, dmon);
+            lsmr_monitor<T>(c, n, Atu1, Atu0, beta, alpha_k, Ihn, Ihbn, Ixn, Atb, prev_ch, c_hbar, c_x, k == 0,
+                            dmon + 1);
+            if (dist_n(c)) allreduce(c, dmon + 1, 1);
+            std::swap(Atu0, Atu1);
+            rr.add(mon, dmon, sizeof(double) * 2);
+        } else {
+            apply_A<T>(c, A, x, r, EPI_RSUB, T(0), b);                         // :69 r = b - A*x
+            sumsq<T>(c, m, r, sl + S_RES);
+            apply_B<T>(c, At, r, atr, EPI_NONE, T(0), nullptr);                // :71 A.'*r
+            nsumsq<T>(c, n, atr, sl + S_AR);
+            rr.add(&hs[0], sl + S_RES, sizeof(T));
+            rr.add(&hs[1], sl + S_AR, sizeof(T));
+        }
+        prev_ch = c_h;
+        if (xt) nsumsq_diff<T>(c, n, x, xt, sl + S_ERR);
         if (xt) rr.add(&hs[2], sl + S_ERR, sizeof(T));
         rr.go();
-        const double nr = std::sqrt((double)hs[0]);
+        if (!kept) {
+            mon[0] = (double)hs[0];
+            mon[1] = (double)hs[1];
+        }
+        const double nr = std::sqrt(mon[0]);
         res[k] = nr / (nb + EPSD);                                             // :70
-        ar[k] = std::sqrt((double)hs[1]) / (normA * std::max(nr, EPSD));       // :71
+        ar[k] = std::sqrt(mon[1]) / (normA * std::max(nr, EPSD));              // :71
         if (xt) err[k] = std::sqrt((double)hs[2]) / nxt;                       // :72-73
         if (res[k] < tol) break;                                               // :76 (<)
     }

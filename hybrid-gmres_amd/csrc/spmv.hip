@@ -478,6 +478,28 @@ void epilogue(hgm_ctx* c, int64_t n, T* y, int epi, T a, const T* z) {
     HGM_HIP(hipGetLastError());
 }
 
+template <typename T, int EPI>
+__global__ __launch_bounds__(BS) void k_epi_to(int64_t n, const T* __restrict__ in, T* out, T a, const T* z) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS)
+        out[i] = apply_epi<T, EPI>(in[i], a, z, i);
+}
+
+template <typename T>
+void epilogue_to(hgm_ctx* c, int64_t n, const T* in, T* out, int epi, T a, const T* z) {
+    const int g = grid_for(n);
+    switch (epi) {
+        case EPI_ADD: k_epi_to<T, EPI_ADD><<<g, BS, 0, c->stream>>>(n, in, out, a, z); break;
+        case EPI_SUB: k_epi_to<T, EPI_SUB><<<g, BS, 0, c->stream>>>(n, in, out, a, z); break;
+        case EPI_RSUB: k_epi_to<T, EPI_RSUB><<<g, BS, 0, c->stream>>>(n, in, out, a, z); break;
+        default:
+            if (in != out) HGM_HIP(hipMemcpyAsync(out, in, sizeof(T) * n, hipMemcpyDeviceToDevice, c->stream));
+            return;
+    }
+    HGM_HIP(hipGetLastError());
+}
+template void epilogue_to<double>(hgm_ctx*, int64_t, const double*, double*, int, double, const double*);
+template void epilogue_to<float>(hgm_ctx*, int64_t, const float*, float*, int, float, const float*);
+
 template void spmv<double>(hgm_ctx*, const hgm_mat*, const double*, double*, int, double, const double*, int, double*);
 template void spmv<float>(hgm_ctx*, const hgm_mat*, const float*, float*, int, float, const float*, int, float*);
 template void epilogue<double>(hgm_ctx*, int64_t, double*, int, double, const double*);

@@ -449,9 +449,10 @@ def lsqr_solver(A, b, x_true, tol, maxit, *, ctx=None, At=None):
     return x, err[:k].copy(), res[:k].copy(), k
 
 
-def lsmr_solver(A, b, x_true=None, tol=None, maxit=None, *, ctx=None, At=None):
+def lsmr_solver(A, b, x_true=None, tol=None, maxit=None, *, ctx=None, At=None, explicit_residual=False):
     """``[x, err_hist, res_hist, ar_hist, iters] = lsmr_solver(A,b,x_true,tol,maxit)``
-    (lsmr_solver.m:1-83; ``tol`` defaults to 1e-6, ``maxit`` to ``min(m,n)``)."""
+    (lsmr_solver.m:1-83; ``tol`` defaults to 1e-6, ``maxit`` to ``min(m,n)``).  The monitors
+    ``b - A*x`` and ``A'*r`` come from kept products unless ``explicit_residual``."""
     ctx, Ao, Ato = _gkb_ops(A, ctx, At)
     m, n = Ao.shape
     tol = 1e-6 if tol is None else float(tol)
@@ -460,7 +461,7 @@ def lsmr_solver(A, b, x_true=None, tol=None, maxit=None, *, ctx=None, At=None):
     xt = None if x_true is None or np.size(x_true) == 0 else _f64(x_true, n, "x_true")
     x = np.zeros(n)
     eh, rh, ah, it = np.zeros(maxit), np.zeros(maxit), np.zeros(maxit), C.c_int(0)
-    o = _opts()
+    o = _opts(explicit_residual=explicit_residual)
     _check(L.load().hgm_lsmr_solver_ex(ctx.handle, C.byref(o), Ao._h, Ato._h, _dp(b), _dp(xt), tol, maxit,
                                        _dp(x), _dp(eh), _dp(rh), _dp(ah), C.byref(it)), ctx)
     k = it.value

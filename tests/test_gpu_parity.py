@@ -441,6 +441,21 @@ def test_lsmr(gpu_ctx, P64):
     assert it2 == itr and np.all(np.isnan(eh2))
 
 
+@pytest.mark.parametrize("dtype", [0, 1])
+def test_lsmr_monitor_forms_agree(gpu_ctx, P64, dtype):
+    """lsmr_solver.m:69-71 monitors: kept-product images (default) vs the explicit SpMVs of
+    x and r (HGM_EXPLICIT_RESIDUAL).  The iterates are the same bits; res_hist agrees to
+    1e-11 (fp64) / 1e-5 (fp32), ar_hist (A'r = A'b - A'A x cancels as LSMR converges) to
+    1e-8 / 1e-3 relative."""
+    A, b, xt = P64.A, P64.b, P64.x_true
+    Ao = hgmres.SparseOperator.from_scipy(A, gpu_ctx, dtype=dtype)
+    o1 = hgmres.lsmr_solver(Ao, b, xt, 0.0, 20, ctx=gpu_ctx)
+    o2 = hgmres.lsmr_solver(Ao, b, xt, 0.0, 20, ctx=gpu_ctx, explicit_residual=True)
+    assert np.array_equal(o1[0], o2[0]) and np.array_equal(o1[1], o2[1]) and o1[4] == o2[4]
+    hist_ok(o1[2], o2[2], 1e-11 if dtype == 0 else 1e-5)
+    hist_ok(o1[3], o2[3], 1e-8 if dtype == 0 else 1e-3)
+
+
 def test_lsqr_fp32(gpu_ctx, P64):
     """BASELINE configs[4]: LSQR / LSMR in fp32 sharing the SpMV kernels.  fp32 GKB
     departs from fp64 by ~1e-5 at k = 4 and by ~5e-2 at k = 8 on this operator
