@@ -68,8 +68,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP-event timing")
     # default A: the roofline kernel; timing both classes costs ~11% of the C2 step, A alone ~4%
-    ap.add_argument("--time-classes", default="A", choices=["A", "B", "AB"],
-                    help="SpMV classes timed with HIP events in the timed region (roofline)")
+    ap.add_argument("--time-classes", default="A", choices=["A", "B", "AB", "MGS", "ALL"],
+                    help="kernel classes timed with HIP events in the timed region (roofline: A)")
     ap.add_argument("--cpu-iters", type=int, default=0, help="oracle iterations for cpu_baseline (0 = maxit)")
     return ap.parse_args()
 
@@ -215,7 +215,7 @@ def main():
         step()
     timing = not args.no_timing
     # HGM_TIMING_CLASSES: every timed launch carries HIP events, so time only what the line reports
-    mask = {"A": 0b001, "B": 0b010, "AB": 0b011}[args.time_classes]
+    mask = {"A": 0b001, "B": 0b010, "AB": 0b011, "MGS": 0b100, "ALL": 0b111}[args.time_classes]
     ctx.kernel_timing(0x100 | mask if timing else 0)
 
     def barrier():

@@ -35,6 +35,42 @@ __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
+// DPP lane permutations within a 16-lane row (no LDS traffic, no lane-index VGPRs).
+// Each step pairs every lane with a lane of the other half of its group, so the sums
+// differ only by commutation and every lane of the row ends with the same bits.
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <typename T>
+__device__ __forceinline__ T row16_sum(T v) {
+    v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]: lane ^ 1
+    v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]: lane ^ 2
+    v += dpp_mov<0x141>(v);   // row_half_mirror: other quad of the 8-lane half
+    v += dpp_mov<0x140>(v);   // row_mirror: other half of the row
+    return v;
+}
+__device__ __forceinline__ double lane_bcast(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ float lane_bcast(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+// 64-lane sum: row sums by DPP, then the four rows combined in fixed order from
+// scalar broadcasts — identical bits in every lane.
+template <typename T>
+__device__ __forceinline__ T wave_sum_dpp(T v) {
+    v = row16_sum(v);
+    return (lane_bcast(v, 0) + lane_bcast(v, 16)) + (lane_bcast(v, 32) + lane_bcast(v, 48));
+}
+
 template <typename T, int G>
 __device__ __forceinline__ T group_sum(T acc) {
 #pragma unroll
@@ -70,6 +106,28 @@ __device__ __forceinline__ T apply_epi(T t, T a, const T* __restrict__ z, int64_
     if (EPI == EPI_SUB) { T s = a * z[i]; return t - s; }
     if (EPI == EPI_RSUB) return z[i] - t;
     return t;
+}
+
+// Raw buffer access (gfx9 resource word 3 = 0x00020000): the range check against
+// `bytes` returns 0 for loads and drops stores past the end, and one 32-bit lane
+// offset serves every resource, so unrolled strided loops keep one address VGPR.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes < 0 ? 0 : bytes, 0x00020000);
+}
+template <typename T> __device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t r, int off);
+template <> __device__ __forceinline__ double buf_load<double>(__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+template <> __device__ __forceinline__ float buf_load<float>(__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ void buf_store(double x, __amdgpu_buffer_rsrc_t r, int off) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), x),
+                                          r, off, 0, 0);
+}
+__device__ __forceinline__ void buf_store(float x, __amdgpu_buffer_rsrc_t r, int off) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 0)), x),
+                                          r, off, 0, 0);
 }
 
 static inline int grid_for(int64_t n) {

@@ -190,6 +190,19 @@ template <typename T> void sumsq_diff(hgm_ctx* c, int64_t n, const T* a, const T
 template <typename T>
 void multidot(hgm_ctx* c, int64_t n, int ncols, const T* Q, int64_t ldq, const T* w, T* out_dev,
               const T* extra = nullptr);   // out[ncols] = extra' * w when extra != nullptr
+// A multidot (out[j] = Q(:,j)' w, j < ncols, and out[ncols] = e' w) that mgs() may run
+// as extra workgroups of its first two passes instead of two launches of its own
+// (same partial layout and summation order as multidot(), so the same bits).
+template <typename T>
+struct MdotJob {
+    int64_t n = 0;
+    int ncols = 0;
+    const T* Q = nullptr;
+    int64_t ldq = 0;
+    const T* w = nullptr;
+    const T* e = nullptr;
+    T* out = nullptr;
+};
 // x = Q(:,0:k) y fused with *err_out = ||x - xt||^2 (local)
 template <typename T>
 void gemv_err(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T* x, const T* xt, T* err_out);
@@ -202,8 +215,17 @@ void recon(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T*
 // MGS sweep of v = Q(:,kk+1) against Q(:,0..kk); writes Hcol[0..kk+1] (device) and
 // normalises Q(:,kk+1) unless H(kk+1,kk) == 0.  dist: n-vectors sharded (scalar all-reduce
 // per pass).  kclass timing under KC_MGS.
+// Leading dimension of a Krylov basis of vectors of length dim.  Short single-GPU bases
+// get ldq = 4096 k (zero-padded past dim) so one workgroup runs the whole MGS sweep with
+// no bounds checks (kernels.hip, k_mgs_single); the caller zeroes a padded basis.
+int64_t krylov_ld(int64_t dim, bool dist);
+bool krylov_padded(int64_t ldq);
+// src (optional): the vector to orthogonalise when it is not already Q(:,kk+1); the result
+// is written to Q(:,kk+1) either way.
+// side (optional): a multidot enqueued with the sweep (see MdotJob).
 template <typename T>
-void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist);
+void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, const T* src = nullptr,
+         const MdotJob<T>* side = nullptr);
 template <typename T>
 void cgs2(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist);
 

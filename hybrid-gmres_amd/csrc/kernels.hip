@@ -310,15 +310,47 @@ void fro2(hgm_ctx* c, const hgm_mat* M, double* out) {
 // h comes from the previous pass's block partials (np_in > 0, single GPU) or from a
 // device scalar already all-reduced across ranks (np_in == 0).
 // ------------------------------------------------------------------------------
+// Side job of an MGS pass (MdotJob): stage 1 = the multidot partials of block g (the
+// k_multidot block (g % np, g / np)), stage 2 = the finalize of column g (k_finalize).
+template <typename T>
+struct MdotStage {
+    MdotJob<T> j;
+    int np = 0;          // partial blocks per column
+    T* parts = nullptr;
+    int stage = 0;       // 0: none
+    int blocks() const { return stage == 1 ? np * (j.ncols + 1) : stage == 2 ? j.ncols + 1 : 0; }
+};
+
+template <typename T>
+__device__ __forceinline__ void mdot_side(const MdotStage<T>& S, int g, T* sh) {
+    if (S.stage == 1) {
+        const int col = g / S.np, p = g - col * S.np;
+        const T* q = col < S.j.ncols ? S.j.Q + (int64_t)col * S.j.ldq : S.j.e;
+        T acc = 0;
+        for (int64_t i = (int64_t)p * BS + threadIdx.x; i < S.j.n; i += (int64_t)S.np * BS) acc += q[i] * S.j.w[i];
+        const T tot = block_sum_all(acc, sh);
+        if (threadIdx.x == 0) S.parts[(int64_t)col * S.np + p] = tot;
+    } else {
+        const T r = reduce_parts(S.parts + (int64_t)g * S.np, S.np, sh);
+        if (threadIdx.x == 0) S.j.out[g] = r;
+    }
+}
+
 template <typename T, int MODE>
-__global__ __launch_bounds__(BS) void k_mgs_pass(int64_t n, const T* __restrict__ qa,
-                                                 const T* __restrict__ qd, T* __restrict__ v,
+__global__ __launch_bounds__(BS) void k_mgs_pass(int64_t n, int nb, const T* __restrict__ qa,
+                                                 const T* __restrict__ qd, const T* vin, T* v,
                                                  const T* __restrict__ pin, int np_in,
-                                                 const T* hsrc, T* hdst, T* __restrict__ pout) {
+                                                 const T* hsrc, T* hdst, T* __restrict__ pout,
+                                                 MdotStage<T> side) {
     using T2 = typename V2<T>::t;
     __shared__ T sh[4];
+    if ((int)blockIdx.x >= nb) {   // extra workgroups: the side job
+        mdot_side(side, (int)blockIdx.x - nb, sh);
+        return;
+    }
     const int64_t n2 = n >> 1;
-    const int64_t stride = (int64_t)gridDim.x * BS;
+    const int64_t stride = (int64_t)nb * BS;
+    const T2* vi2 = reinterpret_cast<const T2*>(vin);   // the vector before this pass (v or src)
     T2* v2 = reinterpret_cast<T2*>(v);
     const T2* qa2 = reinterpret_cast<const T2*>(qa);
     const T2* qd2 = reinterpret_cast<const T2*>(qd);
@@ -327,7 +359,7 @@ __global__ __launch_bounds__(BS) void k_mgs_pass(int64_t n, const T* __restrict_
     int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x;
     T2 vv{0, 0}, qq{0, 0}, dd{0, 0};
     if (i < n2) {
-        vv = v2[i];
+        vv = vi2[i];
         if (MODE != 0) qq = qa2[i];
         if (MODE != 2) dd = qd2[i];
     }
@@ -353,14 +385,14 @@ __global__ __launch_bounds__(BS) void k_mgs_pass(int64_t n, const T* __restrict_
         }
         i += stride;
         if (i < n2) {
-            vv = v2[i];
+            vv = vi2[i];
             if (MODE != 0) qq = qa2[i];
             if (MODE != 2) dd = qd2[i];
         }
     }
-    if ((n & 1) && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    if ((n & 1) && (int)blockIdx.x == nb - 1 && threadIdx.x == 0) {
         const int64_t i = n - 1;
-        T vv = v[i];
+        T vv = vin[i];
         if (MODE != 0) {
             const T p0 = h * qa[i];
             vv = vv - p0;
@@ -398,22 +430,164 @@ __global__ __launch_bounds__(BS) void k_mgs_normalize(int64_t n, T* __restrict__
     if ((n & 1) && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) v[n - 1] = v[n - 1] / nrm;
 }
 
+// Whole MGS sweep of a short vector in ONE workgroup (hybrid_*_rtp.m:20-26): v lives in
+// registers (E entries per lane, entry t + 1024 j), each pass reads q_i once, and the
+// inner product is a wave butterfly + 16-wave LDS sum read back by every lane in the
+// same order, so every lane holds identical h_i.  Replaces kk+3 dependent launches
+// (~4.9 us each at m = 21750) with one; the other CUs stay free for the aux stream.
+// The basis is stored with ldq = 1024 E and zero padding past n (krylov_ld), so the
+// kernel reads and writes whole 1024-entry chunks of the basis with no bounds checks (padding stays
+// zero: 0 - h 0 = 0, 0 / nrm = 0).  The LDS slots alternate between passes so one
+// barrier per pass suffices.
+constexpr int MGS1_BS = 1024;
+constexpr int64_t MGS1_MAX = 24 * MGS1_BS;   // E <= 24: w and q fit 4E = 96 VGPRs
+template <typename T, int E>
+__global__ __launch_bounds__(MGS1_BS) void k_mgs_single(int n, const T* __restrict__ Q, int64_t ldq, const T* src,
+                                                        T* v, int kk, T* __restrict__ Hcol) {
+    __shared__ T sh[2][MGS1_BS / 64];
+    const int t = threadIdx.x;
+    // one buffer resource per column; chunk j is the constant soffset j * 1024 * sizeof(T),
+    // so every load and store shares the single lane-offset VGPR
+    const int off = t * (int)sizeof(T);
+    constexpr int CH = MGS1_BS * (int)sizeof(T);
+    const int bytes = (int)ldq * (int)sizeof(T);
+    auto ldc = [&](__amdgpu_buffer_rsrc_t r, int j) -> T {
+        if constexpr (sizeof(T) == 8)
+            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(r, off, j * CH, 0));
+        else
+            return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, off, j * CH, 0));
+    };
+    T w[E], q[E];
+    const __amdgpu_buffer_rsrc_t rv = buf_rsrc(v, bytes);
+    // src may be another array's column (no zero padding past n): bounds-checked loads
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const int i = t + MGS1_BS * j;
+        w[j] = i < n ? src[i] : T(0);
+    }
+    // block sum: DPP wave sum, one LDS slot per wave, then a DPP sum of the 16 slots in
+    // every row (every lane, hence every wave, gets the same bits)
+    auto bsum = [&](T a, int slot) -> T {
+        static_assert(MGS1_BS / 64 == 16, "one LDS slot per wave, one 16-lane row");
+        a = wave_sum_dpp(a);
+        if ((t & 63) == 0) sh[slot][t >> 6] = a;
+        __syncthreads();
+        return row16_sum(sh[slot][t & 15]);
+    };
+    // kk >= 0: a do-while keeps w in one register set (a zero-trip-capable loop makes
+    // the compiler copy the loaded w and spill at E = 24)
+    int p = 0;
+    do {
+        const __amdgpu_buffer_rsrc_t rq = buf_rsrc(Q + (int64_t)p * ldq, bytes);
+#pragma unroll
+        for (int j = 0; j < E; ++j) q[j] = ldc(rq, j);
+        // fused multiply-adds keep the partial dot in two registers (the products are
+        // not held while the loads drain)
+        T a0 = 0, a1 = 0;
+#pragma unroll
+        for (int j = 0; j < E; j += 2) {
+            a0 = __builtin_fma(q[j], w[j], a0);
+            a1 = __builtin_fma(q[j + 1], w[j + 1], a1);
+        }
+        const T h = bsum(a0 + a1, p & 1);
+        if (t == 0) Hcol[p] = h;
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const T s = h * q[j];
+            w[j] = w[j] - s;
+        }
+    } while (++p <= kk);
+    T a0 = 0, a1 = 0;
+#pragma unroll
+    for (int j = 0; j < E; j += 2) {
+        a0 = __builtin_fma(w[j], w[j], a0);
+        a1 = __builtin_fma(w[j + 1], w[j + 1], a1);
+    }
+    const T nrm = sqrt(bsum(a0 + a1, (kk + 1) & 1));
+    if (t == 0) Hcol[kk + 1] = nrm;
+    if (nrm != 0) {
+#pragma unroll
+        for (int j = 0; j < E; ++j) w[j] = w[j] / nrm;
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        if constexpr (sizeof(T) == 8)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(rv, 0, 0, 0)), w[j]), rv, off, j * CH, 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b32(rv, 0, 0, 0)), w[j]), rv, off, j * CH, 0);
+    }
+}
+
+static bool mgs_single_on() {
+    static int mode = -1;   // HGM_MGS_SINGLE=0 disables (experiment hook)
+    if (mode < 0) {
+        const char* e = std::getenv("HGM_MGS_SINGLE");
+        mode = e ? std::atoi(e) : 1;
+    }
+    return mode != 0;
+}
+
+int64_t krylov_ld(int64_t dim, bool dist) {
+    dim = dim > 0 ? dim : 1;
+    if (!dist && dim <= MGS1_MAX && mgs_single_on()) return (dim + 4 * MGS1_BS - 1) / (4 * MGS1_BS) * (4 * MGS1_BS);
+    return (dim + 63) / 64 * 64;
+}
+
+bool krylov_padded(int64_t ldq) { return ldq % (4 * MGS1_BS) == 0 && ldq <= MGS1_MAX && mgs_single_on(); }
+
 template <typename T>
-void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist) {
+static bool mgs_single(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, const T* src) {
+    if (!krylov_padded(ldq) || n > ldq) return false;
+    T* v = Q + (int64_t)(kk + 1) * ldq;
+    hipStream_t st = c->stream;
+    switch (ldq / MGS1_BS) {
+    case 4: k_mgs_single<T, 4><<<1, MGS1_BS, 0, st>>>((int)n, Q, ldq, src, v, kk, Hcol); break;
+    case 8: k_mgs_single<T, 8><<<1, MGS1_BS, 0, st>>>((int)n, Q, ldq, src, v, kk, Hcol); break;
+    case 12: k_mgs_single<T, 12><<<1, MGS1_BS, 0, st>>>((int)n, Q, ldq, src, v, kk, Hcol); break;
+    case 16: k_mgs_single<T, 16><<<1, MGS1_BS, 0, st>>>((int)n, Q, ldq, src, v, kk, Hcol); break;
+    case 20: k_mgs_single<T, 20><<<1, MGS1_BS, 0, st>>>((int)n, Q, ldq, src, v, kk, Hcol); break;
+    case 24: k_mgs_single<T, 24><<<1, MGS1_BS, 0, st>>>((int)n, Q, ldq, src, v, kk, Hcol); break;
+    default: return false;
+    }
+    HGM_HIP(hipGetLastError());
+    return true;
+}
+
+template <typename T>
+void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, const T* src,
+         const MdotJob<T>* side) {
     hipEvent_t t0 = nullptr;
     timing_begin(c, KC_MGS, &t0);
     const double s = sizeof(T);
+    T* v = Q + (int64_t)(kk + 1) * ldq;
+    if (src == nullptr) src = v;
+    if (!dist && mgs_single<T>(c, n, Q, ldq, kk, Hcol, src)) {
+        timing_end(c, KC_MGS, t0, s * n * (kk + 3.0));   // q_0..q_kk and v read once, v written once
+        if (side) multidot<T>(c, side->n, side->ncols, side->Q, side->ldq, side->w, side->out, side->e);
+        return;
+    }
+    // the side multidot rides on passes 0 and 1 (single GPU; with ranks it keeps its own
+    // launches after the sweep, whose passes are separated by all-reduces)
+    MdotStage<T> s1, s2, none;
+    if (side && !dist) {
+        s1.j = *side;
+        s1.np = parts_for(side->n);
+        s1.parts = c->buf<T>("mdot_parts", (size_t)s1.np * (side->ncols + 1));
+        s1.stage = 1;
+        s2 = s1;
+        s2.stage = 2;
+    }
     // One launch per pass: a dependent launch is the cheapest grid-wide exchange of the
     // block partials on gfx950 (2.6-2.9 us vs 3-25 us for in-kernel grid barriers,
     // scripts/barrier_bench.hip).
     const int np = gemv_blocks(n, mgs_ppl());
     T* P = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
     T* Pb[2] = {P, P + MAX_PARTS};
-    T* v = Q + (int64_t)(kk + 1) * ldq;
     T* ss = c->buf<T>("mgs_ss", 4);
     hipStream_t st = c->stream;
     // pass 0: h_0 partials
-    k_mgs_pass<T, 0><<<np, BS, 0, st>>>(n, nullptr, Q, v, nullptr, 0, nullptr, nullptr, Pb[0]);
+    k_mgs_pass<T, 0><<<np + s1.blocks(), BS, 0, st>>>(n, np, nullptr, Q, src, v, nullptr, 0, nullptr, nullptr,
+                                                       Pb[0], s1);
     if (dist) {
         k_finalize<T><<<1, BS, 0, st>>>(Pb[0], np, Hcol + 0);
         allreduce(c, Hcol, 1);
@@ -426,13 +600,17 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist) {
         T* hdst = dist ? nullptr : Hcol + (j - 1);
         if (j <= kk) {
             const T* qd = Q + (int64_t)j * ldq;
-            k_mgs_pass<T, 1><<<np, BS, 0, st>>>(n, qa, qd, v, pin, np_in, Hcol + (j - 1), hdst, pout);
+            const MdotStage<T>& sj = j == 1 ? s2 : none;
+            k_mgs_pass<T, 1><<<np + sj.blocks(), BS, 0, st>>>(n, np, qa, qd, j == 1 ? src : v, v, pin, np_in,
+                                                               Hcol + (j - 1), hdst, pout, sj);
             if (dist) {
                 k_finalize<T><<<1, BS, 0, st>>>(pout, np, Hcol + j);
                 allreduce(c, Hcol + j, 1);
             }
         } else {
-            k_mgs_pass<T, 2><<<np, BS, 0, st>>>(n, qa, nullptr, v, pin, np_in, Hcol + (j - 1), hdst, pout);
+            const MdotStage<T>& sj = j == 1 ? s2 : none;
+            k_mgs_pass<T, 2><<<np + sj.blocks(), BS, 0, st>>>(n, np, qa, nullptr, j == 1 ? src : v, v, pin, np_in,
+                                                               Hcol + (j - 1), hdst, pout, sj);
             if (dist) {
                 k_finalize<T><<<1, BS, 0, st>>>(pout, np, ss);
                 allreduce(c, ss, 1);
@@ -444,6 +622,7 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist) {
         k_mgs_normalize<T><<<np, BS, 0, st>>>(n, v, pin, dist ? 0 : np, ss, Hcol + kk + 1);
     }
     HGM_HIP(hipGetLastError());
+    if (side && dist) multidot<T>(c, side->n, side->ncols, side->Q, side->ldq, side->w, side->out, side->e);
     // algorithmic bytes: (32k+24)n-style count for k+1 = kk+1 columns
     const double bytes = s * n * (2.0 + 4.0 * kk + 3.0 + 2.0);
     timing_end(c, KC_MGS, t0, bytes);
@@ -635,7 +814,7 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
     template void gemv_err<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, const T*, T*); \
     template void recon<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, const T*, T*, int64_t, \
                            const T*, int64_t, const T*, T*);                                   \
-    template void mgs<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool);                       \
+    template void mgs<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool, const T*, const MdotJob<T>*);                       \
     template void cgs2<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool);                      \
     template void gemv<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, int);       \
     template void div_scalar<T>(hgm_ctx*, int64_t, const T*, T*, T);                           \

@@ -195,13 +195,14 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     const int64_t m = A->rows, n = A->cols;
     const bool nspace = sp.side == HGM_SIDE_BA;
     const int64_t dim = nspace ? n : m;
-    const int64_t ldq = round_up(dim > 0 ? dim : 1, 64);
     const bool dist = nspace && dist_n(c);
+    const int64_t ldq = krylov_ld(dim, dist);
     hipStream_t st = c->stream;
 
     const T* b = stage_in<T>(c, "in_b", b_in, m, dev);
     const T* xt = stage_in_n<T>(c, "in_xt", xt_in, n, dev, po);
     T* Q = c->buf<T>("Q", (size_t)ldq * (maxit + 1));
+    if (krylov_padded(ldq)) HGM_HIP(hipMemsetAsync(Q, 0, sizeof(T) * ldq * (maxit + 1), st));
     T* x = c->buf<T>("x", n > 0 ? n : 1);
     T* t = c->buf<T>("t_m", m > 0 ? m : 1);        // m-vector scratch (A*q, residual)
     T* tn = c->buf<T>("t_n", n > 0 ? n : 1);       // n-vector scratch (AB side: B*q)
@@ -283,18 +284,38 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         } else {
             T* Bq = BQ ? BQ + (int64_t)kq * ldbq : tn;
             apply_B<T>(c, B, qk, Bq, EPI_NONE, T(0), nullptr);                      // B*Q(:,k)
-            apply_A<T>(c, A, Bq, v, EPI_NONE, T(0), nullptr);                       // A*(B*Q(:,k))
-            if (ABQ)
-                HGM_HIP(hipMemcpyAsync(ABQ + (int64_t)kq * ldaq, v, sizeof(T) * m, hipMemcpyDeviceToDevice, c->stream));
+            if (ABQ && orth != HGM_CGS2) {
+                // A*(B*Q(:,k)) lands in its kept column; MGS reads it from there and
+                // writes the orthogonalised vector to Q(:,k+1) (no copy)
+                apply_A<T>(c, A, Bq, ABQ + (int64_t)kq * ldaq, EPI_NONE, T(0), nullptr);
+            } else {
+                apply_A<T>(c, A, Bq, v, EPI_NONE, T(0), nullptr);                   // A*(B*Q(:,k))
+                if (ABQ)
+                    HGM_HIP(hipMemcpyAsync(ABQ + (int64_t)kq * ldaq, v, sizeof(T) * m, hipMemcpyDeviceToDevice,
+                                           c->stream));
+            }
         }
         // ---- orthogonalisation (hybrid_*_rtp.m:20-26) ----
         T* Hcol = dr + (size_t)kq * LH;                  // -> host H(:,k)
-        if (orth == HGM_CGS2) cgs2<T>(c, dim, Q, ldq, kq, Hcol, dist);
-        else mgs<T>(c, dim, Q, ldq, kq, Hcol, dist);
+        // column k of AQk'*AQk and AQk'*b (hybrid_ab_gmres_rtp.m:31-32); A*Q(:,j) was
+        // computed inside M_reg_op(Q(:,j)) at :19 — the same deterministic SpMV.  With MGS
+        // it runs as extra workgroups of the sweep's first two passes.
+        MdotJob<T> gram;
         if (sp.proj == PROJ_ABRTP) {
-            // column k of AQk'*AQk and AQk'*b (hybrid_ab_gmres_rtp.m:31-32); A*Q(:,j) was
-            // computed inside M_reg_op(Q(:,j)) at :19 — the same deterministic SpMV.
-            multidot<T>(c, m, kq + 1, AQ, ldaq, AQ + (int64_t)kq * ldaq, Hcol + (maxit + 2), b);   // + b'*AQ(:,k)
+            gram.n = m;
+            gram.ncols = kq + 1;
+            gram.Q = AQ;
+            gram.ldq = ldaq;
+            gram.w = AQ + (int64_t)kq * ldaq;
+            gram.e = b;                                   // + b'*AQ(:,k)
+            gram.out = Hcol + (maxit + 2);
+        }
+        const MdotJob<T>* side = sp.proj == PROJ_ABRTP ? &gram : nullptr;
+        if (orth == HGM_CGS2) {
+            cgs2<T>(c, dim, Q, ldq, kq, Hcol, dist);
+            if (side) multidot<T>(c, m, gram.ncols, AQ, ldaq, gram.w, gram.out, b);
+        } else {
+            mgs<T>(c, dim, Q, ldq, kq, Hcol, dist, (!nspace && ABQ) ? ABQ + (int64_t)kq * ldaq : nullptr, side);
         }
         publish((size_t)kq * LH, LH);
         step_record(c, kq);
@@ -850,10 +871,11 @@ int arnoldi(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b_in, 
     const int64_t m = A->rows, n = A->cols;
     const bool nspace = side == HGM_SIDE_BA;
     const int64_t dim = nspace ? n : m;
-    const int64_t ldq = round_up(dim > 0 ? dim : 1, 64);
     const bool dist = nspace && dist_n(c);
+    const int64_t ldq = krylov_ld(dim, dist);
     const T* b = stage_in<T>(c, "in_b", b_in, m, false);
     T* Q = c->buf<T>("Q", (size_t)ldq * (kg + 1));
+    if (krylov_padded(ldq)) HGM_HIP(hipMemsetAsync(Q, 0, sizeof(T) * ldq * (kg + 1), c->stream));
     T* Hd = c->buf<T>("H", (size_t)(kg + 1) * kg);
     T* t = c->buf<T>("t_m", m + 1);
     T* tn = c->buf<T>("t_n", n + 1);

@@ -398,6 +398,39 @@ def test_dimension_mismatch_raises(gpu_ctx, P64):
         hgmres.lsqr_solver(P64.A, P64.b[:-1], P64.x_true, 0.0, 3, ctx=gpu_ctx)
 
 
+_MGS_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + "/hybrid-gmres_amd")
+import hgmres
+from hgmres.problems import tomo_problem
+P = tomo_problem(int(sys.argv[3]), int(sys.argv[4]), noise=1e-2, seed=3)
+ctx = hgmres.Context(0)
+out = {}
+for side, fn in (("ab", hgmres.hybrid_ab_gmres_rtp), ("ba", hgmres.hybrid_ba_gmres_rtp)):
+    x, e, r, k, H = fn(P.A, P.B, P.b, P.x_true, 0.0, 12, 1e-2, ctx=ctx, return_H=True)
+    out[side + "_x"], out[side + "_H"] = x, H
+np.savez(sys.argv[2], **out)
+"""
+
+
+@pytest.mark.parametrize("N,na", [(64, 64), (128, 8), (40, 30)])
+def test_mgs_single_workgroup_matches_multiblock(tmp_path, N, na):
+    """The one-workgroup MGS sweep (short bases, ldq = 4096 k zero-padded) against the
+    per-pass multi-block sweep (HGM_MGS_SINGLE=0), each in its own process (the switch is
+    read once per process).  Sizes cover a padded m-space (AB) and n-space (BA) basis,
+    dim a multiple of 4096 (128^2 / 4 chunks: no padding) and a ragged dim."""
+    res = {}
+    for mode in ("1", "0"):
+        f = str(tmp_path / f"mgs{mode}.npz")
+        env = dict(os.environ, HGM_MGS_SINGLE=mode)
+        subprocess.run([sys.executable, "-c", _MGS_CHILD, ROOT, f, str(N), str(na)], env=env, check=True,
+                       timeout=600)
+        res[mode] = np.load(f)
+    for side in ("ab", "ba"):
+        H_ok(res["1"][side + "_H"], res["0"][side + "_H"], 1e-12)
+        assert rel(res["1"][side + "_x"], res["0"][side + "_x"]) < 1e-11
+
+
 def test_cgs2_matches_mgs(gpu_ctx, P64):
     o1 = hgmres.hybrid_ba_gmres_rtp(P64.A, P64.B, P64.b, P64.x_true, 0.0, 20, 1e-2, ctx=gpu_ctx, return_H=True)
     o2 = hgmres.hybrid_ba_gmres_rtp(P64.A, P64.B, P64.b, P64.x_true, 0.0, 20, 1e-2, ctx=gpu_ctx, return_H=True,
