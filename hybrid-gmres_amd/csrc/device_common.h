@@ -27,14 +27,6 @@ __device__ __forceinline__ V ld(const V* p) {
     return *p;
 }
 
-// 64-lane xor butterfly: every lane ends with the same, fixed-order sum.
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
 // DPP lane permutations within a 16-lane row (no LDS traffic, no lane-index VGPRs).
 // Each step pairs every lane with a lane of the other half of its group, so the sums
 // differ only by commutation and every lane of the row ends with the same bits.
@@ -71,31 +63,43 @@ __device__ __forceinline__ T wave_sum_dpp(T v) {
     return (lane_bcast(v, 0) + lane_bcast(v, 16)) + (lane_bcast(v, 32) + lane_bcast(v, 48));
 }
 
+// 64-lane sum, the same bits in every lane.
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) { return wave_sum_dpp(v); }
+
+// Sum over aligned groups of G lanes (G a power of two <= 64), the same bits in every
+// lane of a group: DPP within 16-lane rows, xor shuffles across rows.
 template <typename T, int G>
 __device__ __forceinline__ T group_sum(T acc) {
-#pragma unroll
-    for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    if constexpr (G >= 2) acc += dpp_mov<0xB1>(acc);
+    if constexpr (G >= 4) acc += dpp_mov<0x4E>(acc);
+    if constexpr (G >= 8) acc += dpp_mov<0x141>(acc);
+    if constexpr (G >= 16) acc += dpp_mov<0x140>(acc);
+    if constexpr (G >= 32) acc += __shfl_xor(acc, 16);
+    if constexpr (G >= 64) acc += __shfl_xor(acc, 32);
     return acc;
 }
 
-// Block (256 threads) sum, result broadcast to every thread.  Fixed order.
-template <typename T>
+// Block (256 threads) sum, result broadcast to every thread.  Fixed order.  REUSE=false
+// drops the trailing barrier that protects `sh` for a later call (the caller then never
+// writes `sh` again in this launch).
+template <typename T, bool REUSE = true>
 __device__ __forceinline__ T block_sum_all(T v, T* sh) {
     v = wave_sum(v);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) sh[w] = v;
     __syncthreads();
     T r = (sh[0] + sh[1]) + (sh[2] + sh[3]);
-    __syncthreads();
+    if (REUSE) __syncthreads();
     return r;
 }
 
 // Sum of np partials (np <= MAX_PARTS) — same bits in every block that calls it.
-template <typename T>
+template <typename T, bool REUSE = true>
 __device__ __forceinline__ T reduce_parts(const T* __restrict__ p, int np, T* sh) {
     T a = 0;
     for (int i = threadIdx.x; i < np; i += BS) a += p[i];
-    return block_sum_all(a, sh);
+    return block_sum_all<T, REUSE>(a, sh);
 }
 
 // Fused epilogues of the reference's operator closures, two roundings each (the

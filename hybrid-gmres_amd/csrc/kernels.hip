@@ -343,7 +343,7 @@ __global__ __launch_bounds__(BS) void k_mgs_pass(int64_t n, int nb, const T* __r
                                                  const T* hsrc, T* hdst, T* __restrict__ pout,
                                                  MdotStage<T> side) {
     using T2 = typename V2<T>::t;
-    __shared__ T sh[4];
+    __shared__ T sh[4], sh2[4];   // one LDS slot set per reduction: no trailing barriers
     if ((int)blockIdx.x >= nb) {   // extra workgroups: the side job
         mdot_side(side, (int)blockIdx.x - nb, sh);
         return;
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(BS) void k_mgs_pass(int64_t n, int nb, const T* __r
     }
     T h = 0;
     if (MODE != 0) {
-        h = (np_in > 0) ? reduce_parts(pin, np_in, sh) : *hsrc;
+        h = (np_in > 0) ? reduce_parts<T, false>(pin, np_in, sh) : *hsrc;
         if (hdst != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *hdst = h;
     }
     T acc0 = 0, acc1 = 0;
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(BS) void k_mgs_pass(int64_t n, int nb, const T* __r
         }
         acc0 += (MODE == 2) ? vv * vv : qd[i] * vv;
     }
-    const T tot = block_sum_all(acc0 + acc1, sh);
+    const T tot = block_sum_all<T, false>(acc0 + acc1, sh2);
     if (threadIdx.x == 0) pout[blockIdx.x] = tot;
 }
 
@@ -416,7 +416,7 @@ __global__ __launch_bounds__(BS) void k_mgs_normalize(int64_t n, T* __restrict__
     int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x;
     T2 vv{0, 0};
     if (i < n2) vv = v2[i];                       // overlaps the partial re-reduction
-    const T ss = (np_in > 0) ? reduce_parts(pin, np_in, sh) : *ssrc;
+    const T ss = (np_in > 0) ? reduce_parts<T, false>(pin, np_in, sh) : *ssrc;
     const T nrm = sqrt(ss);
     if (blockIdx.x == 0 && threadIdx.x == 0) *hdst = nrm;
     if (nrm == 0) return;

@@ -75,10 +75,12 @@ class _Rounded:
         return _Rounded(sp.vstack([self.M, np.sqrt(lam) * sp.identity(n, format="csr")]).tocsr(), self.rng, self.c)
 
 
-def _gkb_check(fn, A, out, seeds=(1, 2, 3), k=100.0, nhist=2):
+def _gkb_check(fn, A, out, seeds=tuple(range(1, 9)), k=100.0, nhist=2):
     """Compare a GPU result `out` = (x, hist1, hist2, ...) with the oracle `fn(A)`.
     Tolerance per quantity and per history entry: max(1e-10, k x the largest spread
-    of the oracle itself under the rounding-error model (3 seeds))."""
+    of the oracle itself under the rounding-error model (8 seeds: LSQR without
+    reorthogonalisation amplifies rounding chaotically, and at tomo64 the max over 3
+    seeds underestimates the max over 20 by up to 10x at late iterations))."""
     ref = fn(A)
     sx = 0.0
     sh = [np.zeros(np.size(r_)) for r_ in ref[1:1 + nhist]]
@@ -275,9 +277,12 @@ def test_pixel_order_invisible(gpu_ctx, order):
         assert rel(o2[0], o1[0]) < 1e-12, tag
         hist_ok(o2[1], o1[1], 1e-12)
         hist_ok(o2[2], o1[2], 1e-12)
-    l1 = hgmres.lsqr_solver(R_, b, xt, 0.0, 10, ctx=gpu_ctx)
-    l2 = hgmres.lsqr_solver(Tt, b, xt, 0.0, 10, ctx=gpu_ctx)
-    assert rel(l2[0], l1[0]) < 1e-9
+    # LSQR amplifies rounding ~1e6 here (oracle: 2.8e-10 from a 1e-16 perturbation of b),
+    # so both stored orders are held to the oracle's rounding envelope instead
+    A_ = R_.to_scipy()
+    for op in (R_, Tt):
+        _gkb_check(lambda AA: R.lsqr_solver(AA, b, xt, 0.0, 10), A_,
+                   hgmres.lsqr_solver(op, b, xt, 0.0, 10, ctx=gpu_ctx))
     with pytest.raises(ValueError):
         hgmres.hybrid_ba_gmres_rtp(Tt, R_.T, b, xt, 0.0, 3, 1e-2, ctx=gpu_ctx)   # mixed pixel orders
 
