@@ -59,8 +59,10 @@ hipEvent_t Timing::get() {
         pool.pop_back();
         return e;
     }
+    // timing-only events: no system-scope fence on record (no L2 writeback/invalidate
+    // around the timed kernels, which would slow them and the work after them)
     hipEvent_t e;
-    HGM_HIP(hipEventCreate(&e));
+    HGM_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     return e;
 }
 void Timing::clear() {
@@ -179,8 +181,31 @@ void pinned_ring(hgm_ctx* c, size_t bytes) {
     std::memset(c->hring, 0, bytes);
 }
 
+// Events the host waits on before reading the pinned ring.  Every scalar the kernels put
+// in the ring is a system-scope store (st_sys, device_common.h), so the event needs no
+// system-scope release of its own (an L2 writeback + invalidate per record, ~4% of the
+// C2 step).  HGM_SYNC_EVENT_FENCE=1 restores the fenced events.
+// With ranks the ring is a device buffer copied out by hipMemcpyAsync, so those events
+// keep the fence.
+static void sync_event(hgm_ctx* c, hipEvent_t& e, unsigned& have) {
+    static int v = -1;
+    if (v < 0) {
+        const char* env = std::getenv("HGM_SYNC_EVENT_FENCE");
+        v = env ? std::atoi(env) : 0;
+    }
+    const unsigned want = hipEventDisableTiming | ((v || c->world > 1) ? 0u : hipEventDisableSystemFence);
+    if (e && have != want) {
+        HGM_HIP(hipEventDestroy(e));
+        e = nullptr;
+    }
+    if (!e) {
+        HGM_HIP(hipEventCreateWithFlags(&e, want));
+        have = want;
+    }
+}
+
 void pipe_record(hgm_ctx* c) {
-    if (!c->ev_pipe) HGM_HIP(hipEventCreateWithFlags(&c->ev_pipe, hipEventDisableTiming));
+    sync_event(c, c->ev_pipe, c->ev_flags[8]);
     HGM_HIP(hipEventRecord(c->ev_pipe, c->stream));
 }
 
@@ -191,7 +216,7 @@ hipStream_t aux_stream(hgm_ctx* c) {
 
 void step_record(hgm_ctx* c, int k) {
     hipEvent_t& e = c->ev_step[k & 7];
-    if (!e) HGM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    sync_event(c, e, c->ev_flags[k & 7]);
     HGM_HIP(hipEventRecord(e, c->stream));
 }
 

@@ -80,6 +80,14 @@ __device__ __forceinline__ T group_sum(T acc) {
     return acc;
 }
 
+// Store of a result scalar that the host may read from pinned host memory (the
+// per-iteration ring): system scope, written through to memory, so the host needs no
+// system-scope fence on the event it waits for (capi.cpp sync_event_flags).
+template <typename T>
+__device__ __forceinline__ void st_sys(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Block (256 threads) sum, result broadcast to every thread.  Fixed order.  REUSE=false
 // drops the trailing barrier that protects `sh` for a later call (the caller then never
 // writes `sh` again in this launch).

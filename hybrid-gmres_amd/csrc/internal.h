@@ -83,6 +83,7 @@ struct hgm_ctx {
     // second stream: GMRES reconstruction/monitors overlap the next Arnoldi step (single GPU)
     hipStream_t aux = nullptr;
     hipEvent_t ev_step[8] = {};
+    unsigned ev_flags[9] = {};   // creation flags of ev_step[0..7], ev_pipe (capi.cpp sync_event)
     int pipe_depth = 2;                       // speculative Arnoldi steps in flight (HGM_PIPE_DEPTH)
     // prefix of workspace names while launching on `aux` (its scratch must not alias the
     // main stream's scratch: the two run concurrently)

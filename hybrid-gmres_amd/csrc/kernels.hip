@@ -43,7 +43,7 @@ template <typename T>
 __global__ __launch_bounds__(BS) void k_finalize(const T* __restrict__ parts, int np, T* out) {
     __shared__ T sh[4];
     const T r = reduce_parts(parts + (int64_t)blockIdx.x * np, np, sh);
-    if (threadIdx.x == 0) out[blockIdx.x] = r;
+    if (threadIdx.x == 0) st_sys(out + blockIdx.x, r);
 }
 
 // Single-launch reduction for short vectors (one 1024-thread block, fixed order).
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(1024) void k_reduce_single(int64_t n, const T* __re
     if (threadIdx.x == 0) {
         T r = 0;
         for (int w = 0; w < 16; ++w) r += sh[w];
-        *out = r;
+        st_sys(out, r);
     }
 }
 
@@ -238,7 +238,7 @@ template <typename T>
 __global__ __launch_bounds__(BS) void k_finalize2(const T* __restrict__ parts, int n0, int n1, T* out0, T* out1) {
     __shared__ T sh[4];
     const T r = blockIdx.x == 0 ? reduce_parts(parts, n0, sh) : reduce_parts(parts + n0, n1, sh);
-    if (threadIdx.x == 0) *(blockIdx.x == 0 ? out0 : out1) = r;
+    if (threadIdx.x == 0) st_sys(blockIdx.x == 0 ? out0 : out1, r);
 }
 
 static int gemv_blocks(int64_t n, int ppl = 1) {
@@ -332,7 +332,7 @@ __device__ __forceinline__ void mdot_side(const MdotStage<T>& S, int g, T* sh) {
         if (threadIdx.x == 0) S.parts[(int64_t)col * S.np + p] = tot;
     } else {
         const T r = reduce_parts(S.parts + (int64_t)g * S.np, S.np, sh);
-        if (threadIdx.x == 0) S.j.out[g] = r;
+        if (threadIdx.x == 0) st_sys(S.j.out + g, r);
     }
 }
 
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(BS) void k_mgs_pass(int64_t n, int nb, const T* __r
     T h = 0;
     if (MODE != 0) {
         h = (np_in > 0) ? reduce_parts<T, false>(pin, np_in, sh) : *hsrc;
-        if (hdst != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *hdst = h;
+        if (hdst != nullptr && blockIdx.x == 0 && threadIdx.x == 0) st_sys(hdst, h);
     }
     T acc0 = 0, acc1 = 0;
     while (i < n2) {
@@ -418,7 +418,7 @@ __global__ __launch_bounds__(BS) void k_mgs_normalize(int64_t n, T* __restrict__
     if (i < n2) vv = v2[i];                       // overlaps the partial re-reduction
     const T ss = (np_in > 0) ? reduce_parts<T, false>(pin, np_in, sh) : *ssrc;
     const T nrm = sqrt(ss);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *hdst = nrm;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st_sys(hdst, nrm);
     if (nrm == 0) return;
     while (i < n2) {
         vv.x = vv.x / nrm;
@@ -490,7 +490,7 @@ __global__ __launch_bounds__(MGS1_BS) void k_mgs_single(int n, const T* __restri
             a1 = __builtin_fma(q[j + 1], w[j + 1], a1);
         }
         const T h = bsum(a0 + a1, p & 1);
-        if (t == 0) Hcol[p] = h;
+        if (t == 0) st_sys(Hcol + p, h);
 #pragma unroll
         for (int j = 0; j < E; ++j) {
             const T s = h * q[j];
@@ -504,7 +504,7 @@ __global__ __launch_bounds__(MGS1_BS) void k_mgs_single(int n, const T* __restri
         a1 = __builtin_fma(w[j + 1], w[j + 1], a1);
     }
     const T nrm = sqrt(bsum(a0 + a1, (kk + 1) & 1));
-    if (t == 0) Hcol[kk + 1] = nrm;
+    if (t == 0) st_sys(Hcol + kk + 1, nrm);
     if (nrm != 0) {
 #pragma unroll
         for (int j = 0; j < E; ++j) w[j] = w[j] / nrm;
@@ -642,7 +642,7 @@ void gemv(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T* 
 template <typename T>
 __global__ __launch_bounds__(BS) void k_add_store(int k, const T* a, const T* b, T* out) {
     const int i = threadIdx.x;
-    if (i < k) out[i] = a[i] + b[i];
+    if (i < k) st_sys(out + i, a[i] + b[i]);
 }
 
 template <typename T>

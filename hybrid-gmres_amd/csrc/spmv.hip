@@ -114,7 +114,7 @@ __global__ __launch_bounds__(BS) void k_sum_parts(const T* __restrict__ parts, i
     T a = 0;
     for (int64_t i = threadIdx.x; i < np; i += BS) a += parts[i];
     const T r = block_sum_all(a, sh);
-    if (threadIdx.x == 0) *out = r;
+    if (threadIdx.x == 0) st_sys(out, r);
 }
 
 // Column-banded SpMV: work items (band b, block of RPB rows) in band-major order, grid-
