@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--orth", default="mgs", choices=["mgs", "cgs2"])
+    ap.add_argument("--tune-a", default="", help="experiment: SpMV variant:group for A (default: auto)")
+    ap.add_argument("--tune-b", default="", help="experiment: SpMV variant:group for B (default: auto)")
     ap.add_argument("--explicit-residual", action="store_true",
                     help="monitor norm(b - A*x) with an explicit SpMV (default: b - (A*Q) y)")
     ap.add_argument("--unmatched", action="store_true",
@@ -154,6 +156,10 @@ def main():
             B.close()
             B = hgmres.SparseOperator.pixel_backprojector(wl["N"], wl["angles"], ctx=ctx, dtype=A.dtype)
         lo, hi, full = 0, A.shape[1], A.shape
+    for M, t in ((A, args.tune_a), (B, args.tune_b)):
+        if t:
+            v, g = t.split(":")
+            M.tune(int(v), int(g))
     m, n = A.shape
     dev = torch.device("cuda", local)
     b_d = torch.from_numpy(b).to(dev)

@@ -174,8 +174,10 @@ void finalize_operator(hgm_ctx* c, hgm_mat* M) {
             M->variant = SPMV_STREAM | SPMV_NT;
             M->bsgroup = 4;
         } else {
+            // C2 A (460-entry rays, x L2-resident): 16 lanes per row beats 32 in the solve
+            // (33.0 vs 34.6 us, alternating runs, scripts/ab_compare.sh)
             M->variant = SPMV_VEC;
-            M->group = 32;
+            M->group = avg < 1024 ? 16 : 32;
         }
     } else {
         if (M->nnz >= 50000000) {

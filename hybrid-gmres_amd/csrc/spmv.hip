@@ -28,6 +28,9 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
 // value loads and 8-byte index loads (row heads/tails peeled to keep them aligned).
 // NT: nontemporal (streaming) loads for val/col so they do not evict x from L2/MALL.
 // Per-lane partial of the dot product of entries [s, e) with x, lane gl of a G-lane group.
+#ifndef HGM_SPMV_U
+#define HGM_SPMV_U 4   // pairs per lane per iteration of the VEC row loop (C2 A: 4 beats 2 and 8)
+#endif
 template <typename T, int G, bool VEC, bool NT>
 __device__ __forceinline__ T seg_partial(int64_t s, int64_t e, int gl, const int32_t* __restrict__ ci,
                                          const T* __restrict__ val, const T* __restrict__ x) {
@@ -54,6 +57,31 @@ __device__ __forceinline__ T seg_partial(int64_t s, int64_t e, int gl, const int
             if (gl == 0 && s < s2 && s < e) a0 += ld<NT>(val + s) * x[ld<NT>(ci + s)];
             if (gl == G - 1 && e2 < e && e2 >= s2) a1 += ld<NT>(val + e2) * x[ld<NT>(ci + e2)];
             int64_t i = s2 + 2 * gl;
+#if HGM_SPMV_U > 2
+            // U pairs per lane per iteration (all index/value loads, then all gathers)
+            for (; i + (HGM_SPMV_U - 1) * 2 * G < e2; i += HGM_SPMV_U * 2 * G) {
+                I2 cc[HGM_SPMV_U];
+                T2 vv[HGM_SPMV_U];
+#pragma unroll
+                for (int u = 0; u < HGM_SPMV_U; ++u) {
+                    cc[u] = ld<NT>(reinterpret_cast<const I2*>(ci + i + u * 2 * G));
+                    vv[u] = ld<NT>(reinterpret_cast<const T2*>(val + i + u * 2 * G));
+                }
+                T xx[2 * HGM_SPMV_U];
+#pragma unroll
+                for (int u = 0; u < HGM_SPMV_U; ++u) {
+                    xx[2 * u] = x[cc[u].x];
+                    xx[2 * u + 1] = x[cc[u].y];
+                }
+#pragma unroll
+                for (int u = 0; u < HGM_SPMV_U; u += 2) {
+                    a0 += vv[u].x * xx[2 * u];
+                    a1 += vv[u].y * xx[2 * u + 1];
+                    a2 += vv[u + 1].x * xx[2 * u + 2];
+                    a3 += vv[u + 1].y * xx[2 * u + 3];
+                }
+            }
+#endif
             for (; i + 2 * G < e2; i += 4 * G) {
                 const I2 c0 = ld<NT>(reinterpret_cast<const I2*>(ci + i));
                 const I2 c1 = ld<NT>(reinterpret_cast<const I2*>(ci + i + 2 * G));
