@@ -130,6 +130,7 @@ struct hgm_mat {
     int dtype = HGM_F64;
     int64_t* rp = nullptr;   // rows+1
     int32_t* ci = nullptr;   // nnz
+    uint16_t* ci16 = nullptr;  // narrow copy of ci when cols <= 65536 (row-kernel SpMV reads it)
     void* val = nullptr;     // nnz (double or float)
     int group = 64;          // lanes per row in the SpMV kernel
     int variant = 0;         // SpmvVariant bits

@@ -127,6 +127,7 @@ static void free_bands(hgm_mat* M) {
 void mat_free(hgm_mat* M) {
     if (!M) return;
     free_bands(M);
+    if (M->ci16) (void)hipFree(M->ci16);
     if (M->cfo) (void)hipFree(M->cfo);
     if (M->rp) (void)hipFree(M->rp);
     if (M->ci) (void)hipFree(M->ci);
@@ -161,8 +162,27 @@ __global__ void k_band_fill(int64_t rows, int64_t W, const int64_t* __restrict__
 //   long rows, x beyond L2                          -> 128 Ki-pixel column bands + streaming kernel
 //   short rows (pixel-major B), < 5e7 nnz           -> row kernel, 8 lanes/row, 8-B loads
 //   short rows, >= 5e7 nnz                          -> streaming kernel, nontemporal loads
+__global__ void k_narrow_ci(int64_t nnz, const int32_t* __restrict__ ci, uint16_t* __restrict__ o) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * BS)
+        o[i] = (uint16_t)ci[i];
+}
+
+// 16-bit column indices for operators with <= 65536 columns (the pixel-major B of C2/C3,
+// whose columns are rays): 10 instead of 12 bytes per fp64 entry for the row kernel.
+// HGM_CI16=0 disables.
+static void build_ci16(hgm_ctx* c, hgm_mat* M) {
+    if (M->ci16) (void)hipFree(M->ci16);
+    M->ci16 = nullptr;
+    const char* e = std::getenv("HGM_CI16");
+    if ((e && std::atoi(e) == 0) || M->nnz == 0 || M->cols > 65536) return;
+    HGM_HIP(hipMalloc(&M->ci16, sizeof(uint16_t) * M->nnz));
+    k_narrow_ci<<<grid_cap(M->nnz), BS, 0, c->stream>>>(M->nnz, M->ci, M->ci16);
+    HGM_HIP(hipGetLastError());
+}
+
 void finalize_operator(hgm_ctx* c, hgm_mat* M) {
     if (M->nnz > 0) build_stream_index(c, M);
+    build_ci16(c, M);
     const double avg = M->rows ? (double)M->nnz / (double)M->rows : 0.0;
     set_bands(c, M, auto_band_width(M));
     if (avg >= 64) {

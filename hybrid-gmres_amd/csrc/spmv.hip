@@ -31,12 +31,14 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
 #ifndef HGM_SPMV_U
 #define HGM_SPMV_U 4   // pairs per lane per iteration of the VEC row loop (C2 A: 4 beats 2 and 8)
 #endif
-template <typename T, int G, bool VEC, bool NT>
-__device__ __forceinline__ T seg_partial(int64_t s, int64_t e, int gl, const int32_t* __restrict__ ci,
+// IX: column index type (int32_t, or uint16_t for the narrow copy ci16; scalar path only).
+template <typename T, int G, bool VEC, bool NT, typename IX = int32_t>
+__device__ __forceinline__ T seg_partial(int64_t s, int64_t e, int gl, const IX* __restrict__ ci,
                                          const T* __restrict__ val, const T* __restrict__ x) {
+    static_assert(!VEC || sizeof(IX) == 4, "paired loads need 32-bit column indices");
     T a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     {
-        if (!VEC) {
+        if constexpr (!VEC) {
             int64_t i = s + gl;
             for (; i + 3 * G < e; i += 4 * G) {
                 const int32_t c0 = ld<NT>(ci + i), c1 = ld<NT>(ci + i + G), c2 = ld<NT>(ci + i + 2 * G),
@@ -52,6 +54,7 @@ __device__ __forceinline__ T seg_partial(int64_t s, int64_t e, int gl, const int
         } else {
             using T2 = typename NV2<T>::t;
             using I2 = ni2;
+            static_assert(sizeof(IX) == 4, "");
             const int64_t s2 = (s + 1) & ~int64_t(1);     // first even index >= s
             const int64_t e2 = e & ~int64_t(1);           // last even bound <= e
             if (gl == 0 && s < s2 && s < e) a0 += ld<NT>(val + s) * x[ld<NT>(ci + s)];
@@ -105,9 +108,9 @@ __device__ __forceinline__ T seg_partial(int64_t s, int64_t e, int gl, const int
 
 // NRM: also write the block's sum of y_r^2 (rows in increasing order) to nparts[blk] —
 // the residual monitor norm(b - A*x) (hybrid_*_rtp.m:32/35) without re-reading y.
-template <typename T, int G, int EPI, bool VEC, bool NT, bool NRM = false>
+template <typename T, int G, int EPI, bool VEC, bool NT, bool NRM = false, typename IX = int32_t>
 __global__ __launch_bounds__(BS) void k_spmv(int64_t rows, const int64_t* __restrict__ rp,
-                                             const int32_t* __restrict__ ci,
+                                             const IX* __restrict__ ci,
                                              const T* __restrict__ val, const T* __restrict__ x,
                                              T* __restrict__ y, T a, const T* __restrict__ z, int xcd,
                                              T* __restrict__ nparts) {
@@ -116,7 +119,7 @@ __global__ __launch_bounds__(BS) void k_spmv(int64_t rows, const int64_t* __rest
     const int64_t row = blk * RPB + threadIdx.x / G;
     const int gl = threadIdx.x & (G - 1);
     T acc = 0;
-    if (row < rows) acc = seg_partial<T, G, VEC, NT>(rp[row], rp[row + 1], gl, ci, val, x);
+    if (row < rows) acc = seg_partial<T, G, VEC, NT, IX>(rp[row], rp[row + 1], gl, ci, val, x);
     acc = group_sum<T, G>(acc);
     T r = 0;
     if (gl == 0 && row < rows) {
@@ -350,19 +353,20 @@ static void spmv_stream(hgm_ctx* c, bool last, const SegIndex& si, int G, bool n
 #undef HGM_SG
 }
 
-template <typename T, int G, bool VEC, bool NT>
+template <typename T, int G, bool VEC, bool NT, typename IX = int32_t>
 static void launch_spmv_v(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
     const int64_t nb = (M->rows + (BS / G) - 1) / (BS / G);
     if (nb == 0) return;
     const T* val = reinterpret_cast<const T*>(M->val);
+    const IX* ci = sizeof(IX) == 2 ? reinterpret_cast<const IX*>(M->ci16) : reinterpret_cast<const IX*>(M->ci);
     const int xcd = (M->variant & SPMV_XCD) ? 1 : 0;
     const dim3 g((unsigned)nb), b(BS);
     T* np_ = nullptr;
     switch (epi) {
-        case EPI_NONE: launch(c, true, k_spmv<T, G, EPI_NONE, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, np_); break;
-        case EPI_ADD: launch(c, true, k_spmv<T, G, EPI_ADD, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, np_); break;
-        case EPI_SUB: launch(c, true, k_spmv<T, G, EPI_SUB, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, np_); break;
-        default: launch(c, true, k_spmv<T, G, EPI_RSUB, VEC, NT>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, np_); break;
+        case EPI_NONE: launch(c, true, k_spmv<T, G, EPI_NONE, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_); break;
+        case EPI_ADD: launch(c, true, k_spmv<T, G, EPI_ADD, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_); break;
+        case EPI_SUB: launch(c, true, k_spmv<T, G, EPI_SUB, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_); break;
+        default: launch(c, true, k_spmv<T, G, EPI_RSUB, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_); break;
     }
 }
 
@@ -397,6 +401,8 @@ static void launch_spmv_g(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int ep
     }
     if (vec && nt) launch_spmv_v<T, G, true, true>(c, M, x, y, epi, a, z);
     else if (vec) launch_spmv_v<T, G, true, false>(c, M, x, y, epi, a, z);
+    else if (M->ci16 && nt) launch_spmv_v<T, G, false, true, uint16_t>(c, M, x, y, epi, a, z);
+    else if (M->ci16) launch_spmv_v<T, G, false, false, uint16_t>(c, M, x, y, epi, a, z);
     else if (nt) launch_spmv_v<T, G, false, true>(c, M, x, y, epi, a, z);
     else launch_spmv_v<T, G, false, false>(c, M, x, y, epi, a, z);
 }
@@ -489,7 +495,8 @@ void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T*
     HGM_HIP(hipGetLastError());
     // algorithmic bytes: nnz*(s+4) + 8(rows+1) + s*cols + s*rows (+ s*rows epilogue operand)
     const double s = sizeof(T);
-    double bytes = (double)M->nnz * (s + 4) + 8.0 * (M->rows + 1) + s * M->cols + s * M->rows;
+    const bool narrow = rowk && !nrm && M->ci16 && !(M->variant & SPMV_VEC);   // 16-bit indices read
+    double bytes = (double)M->nnz * (s + (narrow ? 2 : 4)) + 8.0 * (M->rows + 1) + s * M->cols + s * M->rows;
     if (epi != EPI_NONE) bytes += s * M->rows;
     timing_end(c, kclass, t0, bytes);
 }
