@@ -17,6 +17,8 @@ typedef float nf2 __attribute__((ext_vector_type(2)));
 typedef int ni2 __attribute__((ext_vector_type(2)));
 typedef int ni4 __attribute__((ext_vector_type(4)));
 typedef float nf4 __attribute__((ext_vector_type(4)));
+typedef unsigned short nus2 __attribute__((ext_vector_type(2)));
+typedef unsigned short nus4 __attribute__((ext_vector_type(4)));
 template <typename T> struct NV2;
 template <> struct NV2<double> { using t = nd2; };
 template <> struct NV2<float> { using t = nf2; };

@@ -181,13 +181,15 @@ __global__ __launch_bounds__(BS) void k_spmv_band(int64_t rows, int nbands, cons
 // partial in tail[k] and every later chunk's share in head[j]; k_stream_fixup adds them
 // in chunk order.  Fixed chunking => fixed summation order => bitwise reproducible.
 // ------------------------------------------------------------------------------
-template <typename T, int G, int EPI, bool NT>
+template <typename T, int G, int EPI, bool NT, typename IX = int32_t>
 __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, const int64_t* __restrict__ sp,
-                                                    const int32_t* __restrict__ fo, const int32_t* __restrict__ ci,
+                                                    const int32_t* __restrict__ fo, const IX* __restrict__ ci,
                                                     const T* __restrict__ val, const T* __restrict__ x,
                                                     T* __restrict__ out, T a, const T* __restrict__ z,
                                                     T* __restrict__ head, T* __restrict__ tail) {
     using T2 = typename NV2<T>::t;
+    using IV2 = std::conditional_t<sizeof(IX) == 2, nus2, ni2>;   // index pair / quad of the type
+    using IV4 = std::conditional_t<sizeof(IX) == 2, nus4, ni4>;
     __shared__ T prod[SCH];
     const int64_t k = blockIdx.x;
     const int64_t c0 = k * SCH;
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, c
 #pragma unroll
         for (int u = 0; u < SCH / (4 * BS); ++u) {
             const int j = 4 * threadIdx.x + u * 4 * BS;
-            const ni4 cc = ld<NT>(reinterpret_cast<const ni4*>(ci + c0 + j));
+            const IV4 cc = ld<NT>(reinterpret_cast<const IV4*>(ci + c0 + j));
             const nf4 v = ld<NT>(reinterpret_cast<const nf4*>(val + c0 + j));
             prod[j] = v.x * x[cc.x];
             prod[j + 1] = v.y * x[cc.y];
@@ -213,7 +215,7 @@ __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, c
         for (int u = 0; u < SCH / (2 * BS); ++u) {
             const int j = 2 * threadIdx.x + u * 2 * BS;
             const T2 v = ld<NT>(reinterpret_cast<const T2*>(val + c0 + j));
-            const ni2 cc = ld<NT>(reinterpret_cast<const ni2*>(ci + c0 + j));
+            const IV2 cc = ld<NT>(reinterpret_cast<const IV2*>(ci + c0 + j));
             prod[j] = v.x * x[cc.x];
             prod[j + 1] = v.y * x[cc.y];
         }
@@ -307,8 +309,8 @@ __global__ __launch_bounds__(BS) void k_epi(int64_t n, T* __restrict__ y, T a, c
 // launchers (every SpMV launch goes through hgm::launch so armed timing events ride
 // in the dispatch packets of the first / last kernel of the product)
 // ------------------------------------------------------------------------------
-template <typename T, int G, int EPI, bool NT>
-static void launch_stream_e(hgm_ctx* c, bool last, const SegIndex& si, const int32_t* ci, const T* val, const T* x,
+template <typename T, int G, int EPI, bool NT, typename IX>
+static void launch_stream_e(hgm_ctx* c, bool last, const SegIndex& si, const IX* ci, const T* val, const T* x,
                             T* out, T a, const T* z, T* head, T* tail) {
     if (si.nnz == 0) {
         int64_t g = (si.nseg + BS - 1) / BS;
@@ -316,7 +318,7 @@ static void launch_stream_e(hgm_ctx* c, bool last, const SegIndex& si, const int
         if (g > 0) launch(c, last, k_fill_epi<T, EPI>, dim3(g), dim3(BS), si.nseg, out, a, z);
         return;
     }
-    launch(c, false, k_spmv_stream<T, G, EPI, NT>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg, si.sp, si.fo, ci,
+    launch(c, false, k_spmv_stream<T, G, EPI, NT, IX>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg, si.sp, si.fo, ci,
            val, x, out, a, z, head, tail);
     int64_t g = (si.nchunks + BS - 1) / BS;
     if (g > 4096) g = 4096;
@@ -324,25 +326,25 @@ static void launch_stream_e(hgm_ctx* c, bool last, const SegIndex& si, const int
            (const T*)head, (const T*)tail);
 }
 
-template <typename T, int G, bool NT>
-static void launch_stream_g(hgm_ctx* c, bool last, const SegIndex& si, const int32_t* ci, const T* val, const T* x,
+template <typename T, int G, bool NT, typename IX>
+static void launch_stream_g(hgm_ctx* c, bool last, const SegIndex& si, const IX* ci, const T* val, const T* x,
                             T* out, int epi, T a, const T* z, T* head, T* tail) {
     switch (epi) {
-        case EPI_NONE: launch_stream_e<T, G, EPI_NONE, NT>(c, last, si, ci, val, x, out, a, z, head, tail); break;
-        case EPI_ADD: launch_stream_e<T, G, EPI_ADD, NT>(c, last, si, ci, val, x, out, a, z, head, tail); break;
-        case EPI_SUB: launch_stream_e<T, G, EPI_SUB, NT>(c, last, si, ci, val, x, out, a, z, head, tail); break;
-        default: launch_stream_e<T, G, EPI_RSUB, NT>(c, last, si, ci, val, x, out, a, z, head, tail); break;
+        case EPI_NONE: launch_stream_e<T, G, EPI_NONE, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail); break;
+        case EPI_ADD: launch_stream_e<T, G, EPI_ADD, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail); break;
+        case EPI_SUB: launch_stream_e<T, G, EPI_SUB, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail); break;
+        default: launch_stream_e<T, G, EPI_RSUB, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail); break;
     }
 }
 
-template <typename T>
-static void spmv_stream(hgm_ctx* c, bool last, const SegIndex& si, int G, bool nt, const int32_t* ci, const T* val,
+template <typename T, typename IX = int32_t>
+static void spmv_stream(hgm_ctx* c, bool last, const SegIndex& si, int G, bool nt, const IX* ci, const T* val,
                         const T* x, T* out, int epi, T a, const T* z) {
     T* head = c->buf<T>("stream_head", si.nchunks + 1);
     T* tail = c->buf<T>("stream_tail", si.nchunks + 1);
-#define HGM_SG(GG)                                                                              \
-    if (nt) launch_stream_g<T, GG, true>(c, last, si, ci, val, x, out, epi, a, z, head, tail);  \
-    else launch_stream_g<T, GG, false>(c, last, si, ci, val, x, out, epi, a, z, head, tail);
+#define HGM_SG(GG)                                                                                  \
+    if (nt) launch_stream_g<T, GG, true, IX>(c, last, si, ci, val, x, out, epi, a, z, head, tail);  \
+    else launch_stream_g<T, GG, false, IX>(c, last, si, ci, val, x, out, epi, a, z, head, tail);
     switch (G) {
         case 64: HGM_SG(64) break;
         case 32: HGM_SG(32) break;
@@ -466,7 +468,11 @@ static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int ep
         band_reduce<T>(c, M, yp, y, epi, a, z);
     } else {
         SegIndex si{M->nnz, M->rows, stream_chunks(M->nnz), M->rp, M->cfo};
-        spmv_stream<T>(c, true, si, M->sgroup, nt, M->ci, reinterpret_cast<const T*>(M->val), x, y, epi, a, z);
+        if (M->ci16)
+            spmv_stream<T, uint16_t>(c, true, si, M->sgroup, nt, M->ci16, reinterpret_cast<const T*>(M->val), x, y,
+                                     epi, a, z);
+        else
+            spmv_stream<T>(c, true, si, M->sgroup, nt, M->ci, reinterpret_cast<const T*>(M->val), x, y, epi, a, z);
     }
 }
 
@@ -495,7 +501,8 @@ void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T*
     HGM_HIP(hipGetLastError());
     // algorithmic bytes: nnz*(s+4) + 8(rows+1) + s*cols + s*rows (+ s*rows epilogue operand)
     const double s = sizeof(T);
-    const bool narrow = rowk && !nrm && M->ci16 && !(M->variant & SPMV_VEC);   // 16-bit indices read
+    // 16-bit indices read (row kernel without paired loads, or the unbanded streaming kernel)
+    const bool narrow = M->ci16 && ((rowk && !nrm && !(M->variant & SPMV_VEC)) || (stream && M->nbands <= 1));
     double bytes = (double)M->nnz * (s + (narrow ? 2 : 4)) + 8.0 * (M->rows + 1) + s * M->cols + s * M->rows;
     if (epi != EPI_NONE) bytes += s * M->rows;
     timing_end(c, kclass, t0, bytes);
