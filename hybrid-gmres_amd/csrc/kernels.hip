@@ -553,6 +553,241 @@ static bool mgs_single(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol
     return true;
 }
 
+// ------------------------------------------------------------------------------
+// MGS in one-reduction form (hybrid_*_rtp.m:20-26) for long vectors.  In exact
+// arithmetic the MGS coefficients satisfy h_j = q_j'w - sum_{i<j} h_i (q_j'q_i) for ANY
+// basis, orthonormal or not: (I + L) h = Q'w with L the strictly lower part of Q'Q (the
+// "inverse compact WY" form of MGS, Swirydowicz, Langou, Ananthan, Yang, Thomas, Numer.
+// Linear Algebra Appl. 28 (2021) e2343).  The sweep becomes four launches instead of k+3:
+//   1. k_mgs1_dots   : block partials of Q(:,0:k)'w and of the new Gram row q_k'Q(:,0:k-1)
+//   2. k_mgs1_solve  : one workgroup sums the partials in a fixed order and runs the
+//                      forward substitution for h (Gram triangle staged in LDS)
+//   3. k_mgs1_update : v = ((w - h_0 q_0) - h_1 q_1) - ... (MGS's own per-element order and
+//                      roundings) with the norm partials
+//   4. k_mgs_normalize (shared with the pass form)
+// The basis is read twice instead of in 2(k+1) vector passes.  Only the dot products round
+// differently from sequential MGS: |dH|/|H| = 8e-13 at k = 20 and 1.2e-11 at k = 80 on the
+// tomography operators, the size of MGS's own sensitivity to the order of its dot-product
+// sums.  Multi-GPU: the 2k+1 sums are one all-reduce (the pass form needs
+// k+1 all-reduces per step).
+// ------------------------------------------------------------------------------
+constexpr int MGS1_CG = 8;       // basis columns per workgroup of the dots pass
+constexpr int MGS1_MAXC = 120;   // k+1 <= 120: the Gram triangle fits 57 KiB of LDS
+
+static int mgs1_mode() {   // HGM_MGS_FORM: 1 = one-reduction (default), 0 = one launch per pass
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("HGM_MGS_FORM");
+        v = e ? std::atoi(e) : 1;
+    }
+    return v;
+}
+static int mgs1_ppl() {    // element pairs per lane of the dots pass (fewer partials to sum)
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("HGM_MGS1_PPL");
+        v = (e && std::atoi(e) > 0) ? std::atoi(e) : 2;
+    }
+    return v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* __restrict__ Q, int64_t ldq, int kk,
+                                                  const T* __restrict__ w, int npr, T* __restrict__ pr,
+                                                  T* __restrict__ pg, MdotStage<T> side) {
+    using T2 = typename V2<T>::t;
+    __shared__ T sh[4][2 * MGS1_CG];
+    const int ncg = (kk + MGS1_CG) / MGS1_CG;   // ceil((kk+1) / CG)
+    const int b = (int)blockIdx.x;
+    if (b >= npr * ncg) {   // extra workgroups: the side job
+        mdot_side(side, b - npr * ncg, &sh[0][0]);
+        return;
+    }
+    const int g = b / npr, rb = b - g * npr;
+    const int c0 = g * MGS1_CG;
+    const int nc = min(MGS1_CG, kk + 1 - c0);
+    const int64_t n2 = n >> 1, stride = (int64_t)npr * BS;
+    const T2* w2 = reinterpret_cast<const T2*>(w);
+    const T2* qk2 = reinterpret_cast<const T2*>(Q + (int64_t)kk * ldq);
+    const T* qc = Q + (int64_t)c0 * ldq;
+    T ar[MGS1_CG], ag[MGS1_CG];
+#pragma unroll
+    for (int c = 0; c < MGS1_CG; ++c) ar[c] = ag[c] = T(0);
+    for (int64_t i = (int64_t)rb * BS + threadIdx.x; i < n2; i += stride) {
+        const T2 ww = w2[i];
+        const T2 qk = qk2[i];
+        T2 q[MGS1_CG];
+#pragma unroll
+        for (int c = 0; c < MGS1_CG; ++c)
+            if (c < nc) q[c] = reinterpret_cast<const T2*>(qc + (int64_t)c * ldq)[i];
+#pragma unroll
+        for (int c = 0; c < MGS1_CG; ++c)
+            if (c < nc) {
+                ar[c] = __builtin_fma(q[c].y, ww.y, __builtin_fma(q[c].x, ww.x, ar[c]));
+                ag[c] = __builtin_fma(q[c].y, qk.y, __builtin_fma(q[c].x, qk.x, ag[c]));
+            }
+    }
+    if ((n & 1) && rb == npr - 1 && threadIdx.x == 0) {
+        const int64_t i = n - 1;
+        const T wi = w[i], qki = Q[(int64_t)kk * ldq + i];
+#pragma unroll
+        for (int c = 0; c < MGS1_CG; ++c)
+            if (c < nc) {
+                const T qi = qc[(int64_t)c * ldq + i];
+                ar[c] = __builtin_fma(qi, wi, ar[c]);
+                ag[c] = __builtin_fma(qi, qki, ag[c]);
+            }
+    }
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int c = 0; c < MGS1_CG; ++c)
+        if (c < nc) {
+            const T a = wave_sum_dpp(ar[c]);
+            const T e = wave_sum_dpp(ag[c]);
+            if (lane == 0) {
+                sh[wv][c] = a;
+                sh[wv][MGS1_CG + c] = e;
+            }
+        }
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < 2 * MGS1_CG) {
+        const int c = t < MGS1_CG ? t : t - MGS1_CG;
+        const T s = (sh[0][t] + sh[1][t]) + (sh[2][t] + sh[3][t]);
+        if (t < MGS1_CG) {
+            if (c < nc) pr[(int64_t)(c0 + c) * npr + rb] = s;
+        } else if (c < nc && c0 + c < kk) {
+            pg[(int64_t)(c0 + c) * npr + rb] = s;
+        }
+    }
+}
+
+// MODE 0: sum the partials and solve.  MODE 1: sum only (-> red[0, 2k+1): r_0..r_k then
+// the Gram row g_0..g_{k-1}; multi-GPU all-reduces it).  MODE 2: solve from red.
+// The packed strictly lower Gram triangle Gt (row j at j(j-1)/2) persists across the
+// steps of a solve: step k appends row k.  Dynamic LDS: k(k+1)/2 values.
+template <typename T, int MODE>
+__global__ __launch_bounds__(BS) void k_mgs1_solve(int kk, const T* __restrict__ pr, const T* __restrict__ pg,
+                                                   int npr, T* red, T* Gt, T* Hcol, T* hdev) {
+    extern __shared__ unsigned char mgs1_smem[];
+    T* sG = reinterpret_cast<T*>(mgs1_smem);
+    __shared__ T sr[MGS1_MAXC];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int64_t rowk = (int64_t)kk * (kk - 1) / 2;   // offset of Gram row kk
+    const int ncol = 2 * kk + 1;
+    auto put = [&](int col, T a) {
+        if (col <= kk) {
+            sr[col] = a;
+        } else {
+            sG[rowk + col - kk - 1] = a;
+            Gt[rowk + col - kk - 1] = a;
+        }
+    };
+    if (MODE != 2) {
+        // wave wv sums columns wv, wv+4, ...; lane-strided partials then the DPP wave sum
+        for (int col = wv; col < ncol; col += 4) {
+            const T* p = col <= kk ? pr + (int64_t)col * npr : pg + (int64_t)(col - kk - 1) * npr;
+            T a0 = 0, a1 = 0;
+            int i = lane;
+            for (; i + 64 < npr; i += 128) {
+                a0 += p[i];
+                a1 += p[i + 64];
+            }
+            if (i < npr) a0 += p[i];
+            const T a = wave_sum_dpp(a0 + a1);
+            if (lane == 0) {
+                if (MODE == 1) red[col] = a;
+                else put(col, a);
+            }
+        }
+        if (MODE == 1) return;
+    } else {
+        for (int col = t; col < ncol; col += BS) put(col, red[col]);
+    }
+    for (int64_t e = t; e < rowk; e += BS) sG[e] = Gt[e];   // rows 1..k-1 from earlier steps
+    __syncthreads();
+    if (wv != 0) return;
+    // forward substitution (I + L) h = r in wave 0, rows j = lane and lane + 64:
+    // s_j = ((r_j - h_0 G_j0) - h_1 G_j1) - ...,  h_i = s_i once rows < i are applied
+    const int j0 = lane, j1 = lane + 64;
+    T s0 = j0 <= kk ? sr[j0] : T(0);
+    T s1 = j1 <= kk ? sr[j1] : T(0);
+    const int64_t o0 = (int64_t)j0 * (j0 - 1) / 2, o1 = (int64_t)j1 * (j1 - 1) / 2;
+    for (int i = 0; i <= kk; ++i) {
+        const T h = i < 64 ? lane_bcast(s0, i) : lane_bcast(s1, i - 64);
+        if (lane == 0) {
+            st_sys(Hcol + i, h);
+            hdev[i] = h;
+        }
+        if (j0 > i && j0 <= kk) {
+            const T p = h * sG[o0 + i];
+            s0 = s0 - p;
+        }
+        if (j1 > i && j1 <= kk) {
+            const T p = h * sG[o1 + i];
+            s1 = s1 - p;
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, const T* __restrict__ Q, int64_t ldq, int kk,
+                                                    const T* w, T* v, const T* __restrict__ hdev,
+                                                    T* __restrict__ pout, MdotStage<T> side) {
+    using T2 = typename V2<T>::t;
+    __shared__ T hs[MGS1_MAXC];
+    __shared__ T sh[4];
+    if ((int)blockIdx.x >= nb) {
+        mdot_side(side, (int)blockIdx.x - nb, sh);
+        return;
+    }
+    for (int j = threadIdx.x; j <= kk; j += BS) hs[j] = hdev[j];
+    __syncthreads();
+    const int64_t n2 = n >> 1, stride = (int64_t)nb * BS;
+    const T2* w2 = reinterpret_cast<const T2*>(w);
+    T2* v2 = reinterpret_cast<T2*>(v);
+    T acc0 = 0, acc1 = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n2; i += stride) {
+        T2 vv = w2[i];
+        const T* q = Q;
+        int j = 0;
+        for (; j + 4 <= kk + 1; j += 4, q += 4 * ldq) {
+            T2 qq[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) qq[u] = reinterpret_cast<const T2*>(q + (int64_t)u * ldq)[i];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const T h = hs[j + u];
+                const T p0 = h * qq[u].x, p1 = h * qq[u].y;
+                vv.x = vv.x - p0;
+                vv.y = vv.y - p1;
+            }
+        }
+        for (; j <= kk; ++j, q += ldq) {
+            const T2 qq = reinterpret_cast<const T2*>(q)[i];
+            const T h = hs[j];
+            const T p0 = h * qq.x, p1 = h * qq.y;
+            vv.x = vv.x - p0;
+            vv.y = vv.y - p1;
+        }
+        v2[i] = vv;
+        acc0 += vv.x * vv.x;
+        acc1 += vv.y * vv.y;
+    }
+    if ((n & 1) && (int)blockIdx.x == nb - 1 && threadIdx.x == 0) {
+        const int64_t i = n - 1;
+        T vv = w[i];
+        for (int j = 0; j <= kk; ++j) {
+            const T p = hs[j] * Q[(int64_t)j * ldq + i];
+            vv = vv - p;
+        }
+        v[i] = vv;
+        acc0 += vv * vv;
+    }
+    const T tot = block_sum_all<T, false>(acc0 + acc1, sh);
+    if (threadIdx.x == 0) pout[blockIdx.x] = tot;
+}
+
 template <typename T>
 void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, const T* src,
          const MdotJob<T>* side) {
@@ -564,6 +799,50 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
     if (!dist && mgs_single<T>(c, n, Q, ldq, kk, Hcol, src)) {
         timing_end(c, KC_MGS, t0, s * n * (kk + 3.0));   // q_0..q_kk and v read once, v written once
         if (side) multidot<T>(c, side->n, side->ncols, side->Q, side->ldq, side->w, side->out, side->e);
+        return;
+    }
+    if (kk + 1 <= MGS1_MAXC && mgs1_mode() == 1) {
+        MdotStage<T> s1, s2;
+        if (side && !dist) {
+            s1.j = *side;
+            s1.np = parts_for(side->n);
+            s1.parts = c->buf<T>("mdot_parts", (size_t)s1.np * (side->ncols + 1));
+            s1.stage = 1;
+            s2 = s1;
+            s2.stage = 2;
+        }
+        hipStream_t st = c->stream;
+        const int npr = gemv_blocks(n, mgs1_ppl());
+        const int ncg = (kk + MGS1_CG) / MGS1_CG;
+        T* pr = c->buf<T>("mgs1_pr", (size_t)MGS1_MAXC * MAX_PARTS);
+        T* pg = c->buf<T>("mgs1_pg", (size_t)MGS1_MAXC * MAX_PARTS);
+        T* Gt = c->buf<T>("mgs1_G", (size_t)MGS1_MAXC * MGS1_MAXC / 2 + MGS1_MAXC);
+        T* hdev = c->buf<T>("mgs1_h", 2 * MGS1_MAXC + 2);
+        T* red = hdev + MGS1_MAXC;   // (unused in single-GPU mode)
+        const size_t lds = sizeof(T) * ((size_t)kk * (kk + 1) / 2 + 1);
+        k_mgs1_dots<T><<<npr * ncg + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1);
+        if (dist) {
+            T* redd = c->buf<T>("mgs1_red", 2 * MGS1_MAXC + 2);
+            k_mgs1_solve<T, 1><<<1, BS, 0, st>>>(kk, pr, pg, npr, redd, Gt, Hcol, hdev);
+            allreduce(c, redd, 2 * kk + 1);
+            k_mgs1_solve<T, 2><<<1, BS, lds, st>>>(kk, pr, pg, npr, redd, Gt, Hcol, hdev);
+        } else {
+            k_mgs1_solve<T, 0><<<1, BS, lds, st>>>(kk, pr, pg, npr, red, Gt, Hcol, hdev);
+        }
+        const int nb = gemv_blocks(n, mgs_ppl());
+        T* pout = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
+        k_mgs1_update<T><<<nb + s2.blocks(), BS, 0, st>>>(n, nb, Q, ldq, kk, src, v, hdev, pout, s2);
+        T* ss = c->buf<T>("mgs_ss", 4);
+        if (dist) {
+            k_finalize<T><<<1, BS, 0, st>>>(pout, nb, ss);
+            allreduce(c, ss, 1);
+        }
+        k_mgs_normalize<T><<<nb, BS, 0, st>>>(n, v, pout, dist ? 0 : nb, ss, Hcol + kk + 1);
+        HGM_HIP(hipGetLastError());
+        if (side && dist) multidot<T>(c, side->n, side->ncols, side->Q, side->ldq, side->w, side->out, side->e);
+        // dots read w and q_0..q_k (+ q_k per column group), the update reads w and
+        // q_0..q_k and writes v, the scale reads and writes v
+        timing_end(c, KC_MGS, t0, s * n * (2.0 * kk + 8.0));
         return;
     }
     // the side multidot rides on passes 0 and 1 (single GPU; with ranks it keeps its own

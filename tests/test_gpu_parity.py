@@ -436,6 +436,52 @@ def test_mgs_single_workgroup_matches_multiblock(tmp_path, N, na):
         assert rel(res["1"][side + "_x"], res["0"][side + "_x"]) < 1e-11
 
 
+_MGS_FORM_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + "/hybrid-gmres_amd")
+import hgmres
+from hgmres.problems import tomo_problem
+P = tomo_problem(int(sys.argv[3]), int(sys.argv[4]), noise=1e-2, seed=0)
+maxit = int(sys.argv[5])
+ctx = hgmres.Context(0)
+out = {}
+for tag, fn, lam in (("hab", hgmres.hybrid_ab_gmres_rtp, (1e-2,)), ("hba", hgmres.hybrid_ba_gmres_rtp, (1e-2,)),
+                     ("abn", hgmres.ABgmres_nonhybrid_bounds, ())):
+    o = fn(P.A, P.B, P.b, P.x_true, 0.0, maxit, *lam, ctx=ctx, return_H=True)
+    out[tag + "_x"], out[tag + "_H"], out[tag + "_r"], out[tag + "_e"] = o[0], o[-1], o[2], o[1]
+np.savez(sys.argv[2], **out)
+"""
+
+
+@pytest.mark.parametrize("N,na,maxit", [(64, 91, 80), (64, 90, 20)])
+def test_mgs_one_reduction_form(tmp_path, N, na, maxit):
+    """MGS in one-reduction form (default for multi-block sweeps: dots, forward
+    substitution with the kept Gram triangle, update, scale) against the one-launch-per-pass
+    form (HGM_MGS_FORM=0) and the oracle's sequential MGS.  HGM_MGS_SINGLE=0 forces the
+    multi-block path at this size.  64^2/91 has an odd m (m-space basis of ABgmres) and
+    80 iterations cover the 10 column groups of the dots pass and the second row per lane
+    of the substitution (k >= 64).  Bar: 1e-10 (north_star) against the oracle."""
+    res = {}
+    for form in ("1", "0"):
+        f = str(tmp_path / f"form{form}.npz")
+        env = dict(os.environ, HGM_MGS_SINGLE="0", HGM_MGS_FORM=form)
+        subprocess.run([sys.executable, "-c", _MGS_FORM_CHILD, ROOT, f, str(N), str(na), str(maxit)], env=env,
+                       check=True, timeout=600)
+        res[form] = np.load(f)
+    P = tomo_problem(N, na, noise=1e-2, seed=0)
+    refs = {"hab": R.hybrid_ab_gmres_rtp(P.A, P.B, P.b, P.x_true, 0.0, maxit, 1e-2, return_H=True),
+            "hba": R.hybrid_ba_gmres_rtp(P.A, P.B, P.b, P.x_true, 0.0, maxit, 1e-2, return_H=True),
+            "abn": R.ABgmres_nonhybrid_bounds(P.A, P.B, P.b, P.x_true, 0.0, maxit, return_H=True)}
+    for tag, ref in refs.items():
+        for form in ("1", "0"):
+            g = res[form]
+            H_ok(g[tag + "_H"], ref[-1])
+            assert rel(g[tag + "_x"], ref[0]) < TOL, (tag, form)
+            hist_ok(g[tag + "_r"], ref[2], TOL)
+            hist_ok(g[tag + "_e"], ref[1], TOL)
+        H_ok(res["1"][tag + "_H"], res["0"][tag + "_H"], 1e-10)
+
+
 def test_cgs2_matches_mgs(gpu_ctx, P64):
     o1 = hgmres.hybrid_ba_gmres_rtp(P64.A, P64.B, P64.b, P64.x_true, 0.0, 20, 1e-2, ctx=gpu_ctx, return_H=True)
     o2 = hgmres.hybrid_ba_gmres_rtp(P64.A, P64.B, P64.b, P64.x_true, 0.0, 20, 1e-2, ctx=gpu_ctx, return_H=True,
