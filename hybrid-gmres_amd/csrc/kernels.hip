@@ -560,27 +560,28 @@ static bool mgs_single(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol
 // "inverse compact WY" form of MGS, Swirydowicz, Langou, Ananthan, Yang, Thomas, Numer.
 // Linear Algebra Appl. 28 (2021) e2343).  The sweep becomes four launches instead of k+3:
 //   1. k_mgs1_dots   : block partials of Q(:,0:k)'w and of the new Gram row q_k'Q(:,0:k-1)
-//   2. k_mgs1_solve  : one workgroup sums the partials in a fixed order and runs the
-//                      forward substitution for h (Gram triangle staged in LDS)
+//   2. k_mgs1_solve  : one 1024-thread workgroup sums the 2k+1 partial rows (16 lanes per
+//                      row, all loads in flight at once) and runs the forward substitution
+//                      for h (Gram triangle in LDS)
 //   3. k_mgs1_update : v = ((w - h_0 q_0) - h_1 q_1) - ... (MGS's own per-element order and
 //                      roundings) with the norm partials
 //   4. k_mgs_normalize (shared with the pass form)
+// Summing the partials inside the dots kernel instead (last-arriving block per column
+// group, device-scope fences) measured 2.4x slower at C2: every fence writes back and
+// invalidates the XCD's L2.
 // The basis is read twice instead of in 2(k+1) vector passes.  Only the dot products round
 // differently from sequential MGS: |dH|/|H| = 8e-13 at k = 20 and 1.2e-11 at k = 80 on the
 // tomography operators, the size of MGS's own sensitivity to the order of its dot-product
-// sums.  Multi-GPU: the 2k+1 sums are one all-reduce (the pass form needs
-// k+1 all-reduces per step).
+// sums.  Every sum has a fixed order, so results are bitwise reproducible.
+// Multi-GPU: the 2k+1 sums are one all-reduce (the pass form needs k+1 all-reduces per
+// step) between the two halves of k_mgs1_solve.
 // ------------------------------------------------------------------------------
 constexpr int MGS1_CG = 8;       // basis columns per workgroup of the dots pass
 constexpr int MGS1_MAXC = 120;   // k+1 <= 120: the Gram triangle fits 57 KiB of LDS
 
 static int mgs1_mode() {   // HGM_MGS_FORM: 1 = one-reduction (default), 0 = one launch per pass
-    static int v = -1;
-    if (v < 0) {
-        const char* e = std::getenv("HGM_MGS_FORM");
-        v = e ? std::atoi(e) : 1;
-    }
-    return v;
+    const char* e = std::getenv("HGM_MGS_FORM");
+    return e ? std::atoi(e) : 1;
 }
 static int mgs1_ppl() {    // element pairs per lane of the dots pass (fewer partials to sum)
     static int v = -1;
@@ -589,6 +590,46 @@ static int mgs1_ppl() {    // element pairs per lane of the dots pass (fewer par
         v = (e && std::atoi(e) > 0) ? std::atoi(e) : 2;
     }
     return v;
+}
+
+// Forward substitution (I + L) h = r in wave 0 (rows j = lane, lane + 64):
+// s_j = ((r_j - h_0 G_j0) - h_1 G_j1) - ...;  h_i = s_i once rows < i are applied.
+// sr: r (LDS), sG: packed strictly lower Gram triangle (LDS, row j at j(j-1)/2).
+template <typename T>
+__device__ __forceinline__ void mgs1_substitute(int kk, const T* sr, const T* sG, T* Hcol, T* hdev) {
+    const int lane = threadIdx.x & 63;
+    const int j0 = lane, j1 = lane + 64;
+    T s0 = j0 <= kk ? sr[j0] : T(0);
+    T s1 = j1 <= kk ? sr[j1] : T(0);
+    const int o0 = j0 * (j0 - 1) / 2, o1 = j1 * (j1 - 1) / 2;
+    // four steps per round: the Gram loads of a round are issued before its dependent chain
+    for (int i0 = 0; i0 <= kk; i0 += 4) {
+        T g0[4], g1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u;
+            g0[u] = (j0 > i && j0 <= kk) ? sG[o0 + i] : T(0);
+            g1[u] = (j1 > i && j1 <= kk) ? sG[o1 + i] : T(0);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u;
+            if (i > kk) break;
+            const T h = i < 64 ? lane_bcast(s0, i) : lane_bcast(s1, i - 64);
+            if (lane == 0) {
+                st_sys(Hcol + i, h);
+                hdev[i] = h;
+            }
+            if (j0 > i && j0 <= kk) {
+                const T p = h * g0[u];
+                s0 = s0 - p;
+            }
+            if (j1 > i && j1 <= kk) {
+                const T p = h * g1[u];
+                s1 = s1 - p;
+            }
+        }
+    }
 }
 
 template <typename T>
@@ -638,7 +679,7 @@ __global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* __restrict
                 ag[c] = __builtin_fma(qi, qki, ag[c]);
             }
     }
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
 #pragma unroll
     for (int c = 0; c < MGS1_CG; ++c)
         if (c < nc) {
@@ -650,84 +691,67 @@ __global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* __restrict
             }
         }
     __syncthreads();
-    const int t = threadIdx.x;
-    if (t < 2 * MGS1_CG) {
-        const int c = t < MGS1_CG ? t : t - MGS1_CG;
-        const T s = (sh[0][t] + sh[1][t]) + (sh[2][t] + sh[3][t]);
-        if (t < MGS1_CG) {
-            if (c < nc) pr[(int64_t)(c0 + c) * npr + rb] = s;
-        } else if (c < nc && c0 + c < kk) {
-            pg[(int64_t)(c0 + c) * npr + rb] = s;
-        }
-    }
+    // rows of the group: 0..7 = r_{c0+row}, 8..15 = g_{c0+row-8} (g exists for columns < k)
+    auto row_ok = [&](int row) { return row < MGS1_CG ? row < nc : (row - MGS1_CG < nc && c0 + row - MGS1_CG < kk); };
+    auto row_ptr = [&](int row) -> T* {
+        return row < MGS1_CG ? pr + (int64_t)(c0 + row) * npr : pg + (int64_t)(c0 + row - MGS1_CG) * npr;
+    };
+    if (t < 2 * MGS1_CG && row_ok(t)) row_ptr(t)[rb] = (sh[0][t] + sh[1][t]) + (sh[2][t] + sh[3][t]);
 }
 
-// MODE 0: sum the partials and solve.  MODE 1: sum only (-> red[0, 2k+1): r_0..r_k then
-// the Gram row g_0..g_{k-1}; multi-GPU all-reduces it).  MODE 2: solve from red.
-// The packed strictly lower Gram triangle Gt (row j at j(j-1)/2) persists across the
-// steps of a solve: step k appends row k.  Dynamic LDS: k(k+1)/2 values.
+// One 1024-thread workgroup.  MODE 0: sum the partial rows and solve.  MODE 1: sum only,
+// red = [r_0..r_k | g_0..g_{k-1}] (multi-GPU all-reduces it).  MODE 2: solve from red.
+// Row c < k+1 is r_c (pr), row k+1+c is g_c (pg); 16 lanes (one DPP row) per partial row.
+// Gt: the packed strictly lower Gram triangle (row j at j(j-1)/2), kept across the steps
+// of a solve (step k appends row k); dynamic LDS holds its k(k+1)/2 values.
+constexpr int MGS1_SBS = 1024;
 template <typename T, int MODE>
-__global__ __launch_bounds__(BS) void k_mgs1_solve(int kk, const T* __restrict__ pr, const T* __restrict__ pg,
-                                                   int npr, T* red, T* Gt, T* Hcol, T* hdev) {
+__global__ __launch_bounds__(MGS1_SBS) void k_mgs1_solve(int kk, const T* __restrict__ pr, const T* __restrict__ pg,
+                                                         int npr, T* red, T* Gt, T* Hcol, T* hdev) {
     extern __shared__ unsigned char mgs1_smem[];
     T* sG = reinterpret_cast<T*>(mgs1_smem);
     __shared__ T sr[MGS1_MAXC];
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const int64_t rowk = (int64_t)kk * (kk - 1) / 2;   // offset of Gram row kk
-    const int ncol = 2 * kk + 1;
-    auto put = [&](int col, T a) {
-        if (col <= kk) {
-            sr[col] = a;
+    const int t = threadIdx.x;
+    const int rowk = kk * (kk - 1) / 2;   // offset of Gram row kk
+    const int nrow = 2 * kk + 1;
+    auto put = [&](int row, T a) {
+        if (row <= kk) {
+            sr[row] = a;
         } else {
-            sG[rowk + col - kk - 1] = a;
-            Gt[rowk + col - kk - 1] = a;
+            sG[rowk + row - kk - 1] = a;
+            Gt[rowk + row - kk - 1] = a;
         }
     };
     if (MODE != 2) {
-        // wave wv sums columns wv, wv+4, ...; lane-strided partials then the DPP wave sum
-        for (int col = wv; col < ncol; col += 4) {
-            const T* p = col <= kk ? pr + (int64_t)col * npr : pg + (int64_t)(col - kk - 1) * npr;
-            T a0 = 0, a1 = 0;
-            int i = lane;
-            for (; i + 64 < npr; i += 128) {
-                a0 += p[i];
-                a1 += p[i + 64];
+        const int sub = t & 15;
+        for (int row0 = 0; row0 < nrow; row0 += MGS1_SBS / 16) {
+            const int row = row0 + (t >> 4);
+            const bool ok = row < nrow;
+            const T* p = row <= kk ? pr + (int64_t)row * npr : pg + (int64_t)(row - kk - 1) * npr;
+            T acc = 0;
+            for (int base = 0; base < npr; base += 256) {
+                T pv[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int i = base + sub + 16 * u;
+                    pv[u] = (ok && i < npr) ? p[i] : T(0);
+                }
+#pragma unroll
+                for (int u = 0; u < 16; ++u) acc += pv[u];
             }
-            if (i < npr) a0 += p[i];
-            const T a = wave_sum_dpp(a0 + a1);
-            if (lane == 0) {
-                if (MODE == 1) red[col] = a;
-                else put(col, a);
+            acc = row16_sum(acc);
+            if (sub == 0 && ok) {
+                if (MODE == 1) red[row] = acc;
+                else put(row, acc);
             }
         }
         if (MODE == 1) return;
     } else {
-        for (int col = t; col < ncol; col += BS) put(col, red[col]);
+        for (int row = t; row < nrow; row += MGS1_SBS) put(row, red[row]);
     }
-    for (int64_t e = t; e < rowk; e += BS) sG[e] = Gt[e];   // rows 1..k-1 from earlier steps
+    for (int e = t; e < rowk; e += MGS1_SBS) sG[e] = Gt[e];   // rows 1..k-1 from earlier steps
     __syncthreads();
-    if (wv != 0) return;
-    // forward substitution (I + L) h = r in wave 0, rows j = lane and lane + 64:
-    // s_j = ((r_j - h_0 G_j0) - h_1 G_j1) - ...,  h_i = s_i once rows < i are applied
-    const int j0 = lane, j1 = lane + 64;
-    T s0 = j0 <= kk ? sr[j0] : T(0);
-    T s1 = j1 <= kk ? sr[j1] : T(0);
-    const int64_t o0 = (int64_t)j0 * (j0 - 1) / 2, o1 = (int64_t)j1 * (j1 - 1) / 2;
-    for (int i = 0; i <= kk; ++i) {
-        const T h = i < 64 ? lane_bcast(s0, i) : lane_bcast(s1, i - 64);
-        if (lane == 0) {
-            st_sys(Hcol + i, h);
-            hdev[i] = h;
-        }
-        if (j0 > i && j0 <= kk) {
-            const T p = h * sG[o0 + i];
-            s0 = s0 - p;
-        }
-        if (j1 > i && j1 <= kk) {
-            const T p = h * sG[o1 + i];
-            s1 = s1 - p;
-        }
-    }
+    if ((t >> 6) == 0) mgs1_substitute(kk, sr, sG, Hcol, hdev);
 }
 
 template <typename T>
@@ -817,17 +841,16 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
         T* pr = c->buf<T>("mgs1_pr", (size_t)MGS1_MAXC * MAX_PARTS);
         T* pg = c->buf<T>("mgs1_pg", (size_t)MGS1_MAXC * MAX_PARTS);
         T* Gt = c->buf<T>("mgs1_G", (size_t)MGS1_MAXC * MGS1_MAXC / 2 + MGS1_MAXC);
-        T* hdev = c->buf<T>("mgs1_h", 2 * MGS1_MAXC + 2);
-        T* red = hdev + MGS1_MAXC;   // (unused in single-GPU mode)
+        T* hdev = c->buf<T>("mgs1_h", MGS1_MAXC + 2);
         const size_t lds = sizeof(T) * ((size_t)kk * (kk + 1) / 2 + 1);
         k_mgs1_dots<T><<<npr * ncg + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1);
         if (dist) {
             T* redd = c->buf<T>("mgs1_red", 2 * MGS1_MAXC + 2);
-            k_mgs1_solve<T, 1><<<1, BS, 0, st>>>(kk, pr, pg, npr, redd, Gt, Hcol, hdev);
+            k_mgs1_solve<T, 1><<<1, MGS1_SBS, 0, st>>>(kk, pr, pg, npr, redd, Gt, Hcol, hdev);
             allreduce(c, redd, 2 * kk + 1);
-            k_mgs1_solve<T, 2><<<1, BS, lds, st>>>(kk, pr, pg, npr, redd, Gt, Hcol, hdev);
+            k_mgs1_solve<T, 2><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, redd, Gt, Hcol, hdev);
         } else {
-            k_mgs1_solve<T, 0><<<1, BS, lds, st>>>(kk, pr, pg, npr, red, Gt, Hcol, hdev);
+            k_mgs1_solve<T, 0><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, nullptr, Gt, Hcol, hdev);
         }
         const int nb = gemv_blocks(n, mgs_ppl());
         T* pout = c->buf<T>("mgs_parts", 2 * MAX_PARTS);

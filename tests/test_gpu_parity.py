@@ -449,6 +449,8 @@ for tag, fn, lam in (("hab", hgmres.hybrid_ab_gmres_rtp, (1e-2,)), ("hba", hgmre
                      ("abn", hgmres.ABgmres_nonhybrid_bounds, ())):
     o = fn(P.A, P.B, P.b, P.x_true, 0.0, maxit, *lam, ctx=ctx, return_H=True)
     out[tag + "_x"], out[tag + "_H"], out[tag + "_r"], out[tag + "_e"] = o[0], o[-1], o[2], o[1]
+o = hgmres.hybrid_ba_gmres_rtp(P.A, P.B, P.b, P.x_true, 0.0, maxit, 1e-2, ctx=ctx, return_H=True)
+out["hba_x2"], out["hba_H2"] = o[0], o[-1]
 np.savez(sys.argv[2], **out)
 """
 
@@ -480,6 +482,9 @@ def test_mgs_one_reduction_form(tmp_path, N, na, maxit):
             hist_ok(g[tag + "_r"], ref[2], TOL)
             hist_ok(g[tag + "_e"], ref[1], TOL)
         H_ok(res["1"][tag + "_H"], res["0"][tag + "_H"], 1e-10)
+    for form in ("1", "0"):   # fixed summation orders: repeated solves are bitwise equal
+        assert np.array_equal(res[form]["hba_x"], res[form]["hba_x2"])
+        assert np.array_equal(res[form]["hba_H"], res[form]["hba_H2"])
 
 
 def test_cgs2_matches_mgs(gpu_ctx, P64):
