@@ -595,8 +595,10 @@ static int mgs1_ppl() {    // element pairs per lane of the dots pass (fewer par
 // Forward substitution (I + L) h = r in wave 0 (rows j = lane, lane + 64):
 // s_j = ((r_j - h_0 G_j0) - h_1 G_j1) - ...;  h_i = s_i once rows < i are applied.
 // sr: r (LDS), sG: packed strictly lower Gram triangle (LDS, row j at j(j-1)/2).
+// h goes to device memory only: the update kernel's block 0 copies it to the host ring
+// (a one-block kernel would wait at its end for the host-memory stores to complete).
 template <typename T>
-__device__ __forceinline__ void mgs1_substitute(int kk, const T* sr, const T* sG, T* Hcol, T* hdev) {
+__device__ __forceinline__ void mgs1_substitute(int kk, const T* sr, const T* sG, T* hdev) {
     const int lane = threadIdx.x & 63;
     const int j0 = lane, j1 = lane + 64;
     T s0 = j0 <= kk ? sr[j0] : T(0);
@@ -616,10 +618,7 @@ __device__ __forceinline__ void mgs1_substitute(int kk, const T* sr, const T* sG
             const int i = i0 + u;
             if (i > kk) break;
             const T h = i < 64 ? lane_bcast(s0, i) : lane_bcast(s1, i - 64);
-            if (lane == 0) {
-                st_sys(Hcol + i, h);
-                hdev[i] = h;
-            }
+            if (lane == 0) hdev[i] = h;
             if (j0 > i && j0 <= kk) {
                 const T p = h * g0[u];
                 s0 = s0 - p;
@@ -707,7 +706,7 @@ __global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* __restrict
 constexpr int MGS1_SBS = 1024;
 template <typename T, int MODE>
 __global__ __launch_bounds__(MGS1_SBS) void k_mgs1_solve(int kk, const T* __restrict__ pr, const T* __restrict__ pg,
-                                                         int npr, T* red, T* Gt, T* Hcol, T* hdev) {
+                                                         int npr, T* red, T* Gt, T* hdev) {
     extern __shared__ unsigned char mgs1_smem[];
     T* sG = reinterpret_cast<T*>(mgs1_smem);
     __shared__ T sr[MGS1_MAXC];
@@ -722,6 +721,8 @@ __global__ __launch_bounds__(MGS1_SBS) void k_mgs1_solve(int kk, const T* __rest
             Gt[rowk + row - kk - 1] = a;
         }
     };
+    // rows 1..k-1 of the triangle (earlier steps): issued first, independent of the sums
+    for (int e = t; e < rowk; e += MGS1_SBS) sG[e] = Gt[e];
     if (MODE != 2) {
         const int sub = t & 15;
         for (int row0 = 0; row0 < nrow; row0 += MGS1_SBS / 16) {
@@ -749,14 +750,13 @@ __global__ __launch_bounds__(MGS1_SBS) void k_mgs1_solve(int kk, const T* __rest
     } else {
         for (int row = t; row < nrow; row += MGS1_SBS) put(row, red[row]);
     }
-    for (int e = t; e < rowk; e += MGS1_SBS) sG[e] = Gt[e];   // rows 1..k-1 from earlier steps
     __syncthreads();
-    if ((t >> 6) == 0) mgs1_substitute(kk, sr, sG, Hcol, hdev);
+    if ((t >> 6) == 0) mgs1_substitute(kk, sr, sG, hdev);
 }
 
 template <typename T>
 __global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, const T* __restrict__ Q, int64_t ldq, int kk,
-                                                    const T* w, T* v, const T* __restrict__ hdev,
+                                                    const T* w, T* v, const T* __restrict__ hdev, T* Hcol,
                                                     T* __restrict__ pout, MdotStage<T> side) {
     using T2 = typename V2<T>::t;
     __shared__ T hs[MGS1_MAXC];
@@ -765,7 +765,11 @@ __global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, const T* 
         mdot_side(side, (int)blockIdx.x - nb, sh);
         return;
     }
-    for (int j = threadIdx.x; j <= kk; j += BS) hs[j] = hdev[j];
+    for (int j = threadIdx.x; j <= kk; j += BS) {
+        const T h = hdev[j];
+        hs[j] = h;
+        if (blockIdx.x == 0) st_sys(Hcol + j, h);   // H(0:k, k) -> host ring
+    }
     __syncthreads();
     const int64_t n2 = n >> 1, stride = (int64_t)nb * BS;
     const T2* w2 = reinterpret_cast<const T2*>(w);
@@ -846,15 +850,15 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
         k_mgs1_dots<T><<<npr * ncg + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1);
         if (dist) {
             T* redd = c->buf<T>("mgs1_red", 2 * MGS1_MAXC + 2);
-            k_mgs1_solve<T, 1><<<1, MGS1_SBS, 0, st>>>(kk, pr, pg, npr, redd, Gt, Hcol, hdev);
+            k_mgs1_solve<T, 1><<<1, MGS1_SBS, 0, st>>>(kk, pr, pg, npr, redd, Gt, hdev);
             allreduce(c, redd, 2 * kk + 1);
-            k_mgs1_solve<T, 2><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, redd, Gt, Hcol, hdev);
+            k_mgs1_solve<T, 2><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, redd, Gt, hdev);
         } else {
-            k_mgs1_solve<T, 0><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, nullptr, Gt, Hcol, hdev);
+            k_mgs1_solve<T, 0><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, nullptr, Gt, hdev);
         }
         const int nb = gemv_blocks(n, mgs_ppl());
         T* pout = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
-        k_mgs1_update<T><<<nb + s2.blocks(), BS, 0, st>>>(n, nb, Q, ldq, kk, src, v, hdev, pout, s2);
+        k_mgs1_update<T><<<nb + s2.blocks(), BS, 0, st>>>(n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout, s2);
         T* ss = c->buf<T>("mgs_ss", 4);
         if (dist) {
             k_finalize<T><<<1, BS, 0, st>>>(pout, nb, ss);
