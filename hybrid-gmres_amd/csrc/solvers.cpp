@@ -177,6 +177,16 @@ struct GmresSpec {
     bool x_preassigned;   // hybrid_ba_gmres_rtp.m:4 initialises x = zeros
 };
 
+// n from which the GMRES reconstruction is serialised on the main stream (see gmres_family)
+static int64_t recon_serial_min_n() {
+    static int64_t v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("HGM_RECON_SERIAL_N");
+        v = e ? std::atoll(e) : (int64_t)(4 << 20);
+    }
+    return v;
+}
+
 int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_mat* A, const hgm_mat* B,
                  const double* b_in, const double* xt_in, double tol, int maxit, double lambda, double* x_out,
                  double* err_out, double* res_out, int* niters) {
@@ -232,9 +242,13 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     const bool zc = !dist_n(c);
     // single GPU: reconstructions run on the auxiliary stream, concurrently with the
     // Arnoldi steps (multi-GPU keeps one stream: the communicator's collectives must be
-    // issued in one order)
-    hipStream_t rs_stream = zc ? aux_stream(c) : st;
-    if (zc) HGM_HIP(hipStreamSynchronize(rs_stream));
+    // issued in one order).  For large n the concurrent GEMV over the kept columns evicts
+    // the SpMVs' L2-resident x-slices and costs the SpMVs more than it hides, so it is
+    // serialised behind the steps (HGM_RECON_SERIAL=0/1 overrides).
+    bool recon_serial = (int64_t)n >= recon_serial_min_n();
+    if (const char* e = std::getenv("HGM_RECON_SERIAL")) recon_serial = std::atoi(e) != 0;
+    hipStream_t rs_stream = (zc && !recon_serial) ? aux_stream(c) : st;
+    if (rs_stream != st) HGM_HIP(hipStreamSynchronize(rs_stream));
     pinned_ring(c, sizeof(double) * ring_n);
     const double* hr = c->hring;
     T* dr = zc ? c->hring_dev : c->buf<T>("ring_dev", ring_n);
