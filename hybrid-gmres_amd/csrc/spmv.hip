@@ -195,50 +195,86 @@ __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, c
     const int64_t c0 = k * SCH;
     const int64_t c1 = (c0 + SCH < nnz) ? c0 + SCH : nnz;
     const int n = (int)(c1 - c0);
+    // Segment bookkeeping of the reduction phase (the chunk's segment range, sp at its first
+    // segment for the head test and, per group, sp around its first task's segment) is
+    // loaded while the chunk's value/index loads are in flight, so its two dependent round
+    // trips (fo -> sp) overlap the product phase instead of following the barrier.  The
+    // scheduling barriers keep the compiler from hoisting its waits above those loads.
+    const int gid = threadIdx.x / G, gl = threadIdx.x & (G - 1);
+    int64_t s_begin, s_end, q, sp_b, pm, p0, p1;
+    auto bookkeeping = [&]() {
+        s_begin = fo[k];
+        s_end = fo[k + 1];
+        q = s_begin + gid;
+        sp_b = s_begin <= nseg ? sp[s_begin] : 0;
+        pm = (q >= 1 && q - 1 <= nseg) ? sp[q - 1] : 0;
+        p0 = q <= nseg ? sp[q] : 0;
+        p1 = q + 1 <= nseg ? sp[q + 1] : 0;
+    };
     if (n == SCH && sizeof(T) == 4) {
         // fp32: four entries per lane per step (16-B value and 16-B index loads, both fully
         // coalesced across the wave)
+        constexpr int U = SCH / (4 * BS);
+        IV4 cc[U];
+        nf4 vv[U];
 #pragma unroll
-        for (int u = 0; u < SCH / (4 * BS); ++u) {
+        for (int u = 0; u < U; ++u) {
             const int j = 4 * threadIdx.x + u * 4 * BS;
-            const IV4 cc = ld<NT>(reinterpret_cast<const IV4*>(ci + c0 + j));
-            const nf4 v = ld<NT>(reinterpret_cast<const nf4*>(val + c0 + j));
-            prod[j] = v.x * x[cc.x];
-            prod[j + 1] = v.y * x[cc.y];
-            prod[j + 2] = v.z * x[cc.z];
-            prod[j + 3] = v.w * x[cc.w];
+            cc[u] = ld<NT>(reinterpret_cast<const IV4*>(ci + c0 + j));
+            vv[u] = ld<NT>(reinterpret_cast<const nf4*>(val + c0 + j));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        bookkeeping();
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = 4 * threadIdx.x + u * 4 * BS;
+            prod[j] = vv[u].x * x[cc[u].x];
+            prod[j + 1] = vv[u].y * x[cc[u].y];
+            prod[j + 2] = vv[u].z * x[cc[u].z];
+            prod[j + 3] = vv[u].w * x[cc[u].w];
         }
     } else if (n == SCH) {
         // fp64: a pair per lane per step (16-B value loads; four entries per lane would leave
         // every 16-B wave load half-coalesced: measured 17% slower at C4)
+        constexpr int U = SCH / (2 * BS);
+        IV2 cc[U];
+        T2 vv[U];
 #pragma unroll
-        for (int u = 0; u < SCH / (2 * BS); ++u) {
+        for (int u = 0; u < U; ++u) {
             const int j = 2 * threadIdx.x + u * 2 * BS;
-            const T2 v = ld<NT>(reinterpret_cast<const T2*>(val + c0 + j));
-            const IV2 cc = ld<NT>(reinterpret_cast<const IV2*>(ci + c0 + j));
-            prod[j] = v.x * x[cc.x];
-            prod[j + 1] = v.y * x[cc.y];
+            vv[u] = ld<NT>(reinterpret_cast<const T2*>(val + c0 + j));
+            cc[u] = ld<NT>(reinterpret_cast<const IV2*>(ci + c0 + j));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        bookkeeping();
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = 2 * threadIdx.x + u * 2 * BS;
+            prod[j] = vv[u].x * x[cc[u].x];
+            prod[j + 1] = vv[u].y * x[cc[u].y];
         }
     } else {
+        bookkeeping();
         for (int j = threadIdx.x; j < n; j += BS) prod[j] = val[c0 + j] * x[ci[c0 + j]];
     }
     __syncthreads();
-    const int64_t s_begin = fo[k], s_end = fo[k + 1];
-    const int has_head = (s_begin > 0 && sp[s_begin] > c0) ? 1 : 0;
+    const int has_head = (s_begin > 0 && sp_b > c0) ? 1 : 0;
     const int64_t ntasks = (s_end - s_begin) + has_head;
-    const int gid = threadIdx.x / G, gl = threadIdx.x & (G - 1);
     constexpr int NG = BS / G;
     for (int64_t t = gid; t < ntasks; t += NG) {
-        int64_t s, lo, hi;
-        if (has_head && t == 0) {
-            s = s_begin - 1;
-            lo = c0;
+        int64_t s, lo, send;
+        if (t == gid) {             // first task: prefetched bounds
+            s = q - has_head;
+            lo = (has_head && t == 0) ? c0 : (has_head ? pm : p0);
+            send = has_head ? p0 : p1;
         } else {
             s = s_begin + t - has_head;
             lo = sp[s];
+            send = sp[s + 1];
         }
-        const int64_t send = sp[s + 1];
-        hi = send < c1 ? send : c1;
+        const int64_t hi = send < c1 ? send : c1;
         T acc = 0;
         for (int64_t i = lo + gl; i < hi; i += G) acc += prod[i - c0];
         acc = group_sum<T, G>(acc);
