@@ -80,7 +80,7 @@ void Timing::clear() {
 // (first launch: start, last launch: stop); other classes use stream markers.
 void timing_begin(hgm_ctx* c, int cls, hipEvent_t* start) {
     *start = nullptr;
-    if (!c->timing.on || cls < 0 || cls >= KC_N || !((c->timing.mask >> cls) & 1u)) return;
+    if (!c->timing.on || c->timing.paused || cls < 0 || cls >= KC_N || !((c->timing.mask >> cls) & 1u)) return;
     *start = c->timing.get();
     if (cls == KC_SPMV_A || cls == KC_SPMV_B) {
         c->arm_start = *start;
@@ -824,8 +824,15 @@ HGM_API int hgm_kernel_timing(hgm_ctx* c, int enable) {
         sync(c);
         c->timing.clear();
         c->timing.on = enable != 0;
+        c->timing.paused = false;
         c->timing.mask = (enable & 0x100) ? (unsigned)(enable & 0xff) : 0xffu;
     });
+    return HGM_OK;
+}
+
+HGM_API int hgm_kernel_timing_pause(hgm_ctx* c, int paused) {
+    if (!c) return HGM_E_ARG;
+    c->timing.paused = paused != 0;
     return HGM_OK;
 }
 

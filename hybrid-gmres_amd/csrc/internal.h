@@ -49,6 +49,7 @@ enum KClass { KC_SPMV_A = 0, KC_SPMV_B = 1, KC_MGS = 2, KC_N = 3 };
 
 struct Timing {
     bool on = false;
+    bool paused = false;   // hgm_kernel_timing_pause: armed but not recording
     unsigned mask = 0xffu;   // timed classes
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[KC_N];
     double bytes[KC_N] = {0, 0, 0};

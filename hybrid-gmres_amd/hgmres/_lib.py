@@ -88,6 +88,7 @@ _SIGS = {
     "hgm_gcv_fminbnd": (c_int, [dp, c_int, c_double, c_double, c_double, c_double, c_double, dp, dp]),
     "hgm_kernel_timing": (c_int, [c_void_p, c_int]),
     "hgm_kernel_timing_read": (c_int, [c_void_p, c_int, dp, ip64, dp]),
+    "hgm_kernel_timing_pause": (c_int, [c_void_p, c_int]),
 }
 
 _lib = None

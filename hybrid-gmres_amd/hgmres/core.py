@@ -108,6 +108,9 @@ class Context:
     def kernel_timing(self, enable=True):
         _check(L.load().hgm_kernel_timing(self._h, int(enable)), self)
 
+    def kernel_timing_pause(self, paused=True):
+        _check(L.load().hgm_kernel_timing_pause(self._h, int(paused)), self)
+
     def kernel_timing_read(self, cls):
         ms, calls, by = C.c_double(), C.c_int64(), C.c_double()
         _check(L.load().hgm_kernel_timing_read(self._h, cls, C.byref(ms), C.byref(calls), C.byref(by)), self)

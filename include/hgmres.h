@@ -241,6 +241,9 @@ HGM_API int hgm_gcv_fminbnd(const double* H, int k, double beta, double trace_m,
 HGM_API int hgm_kernel_timing(hgm_ctx* ctx, int enable);
 HGM_API int hgm_kernel_timing_read(hgm_ctx* ctx, int cls, double* total_ms, int64_t* calls,
                                    double* bytes);
+/* Pause (1) / resume (0) the armed timing without a sync or a reset: launches enqueued
+ * while paused carry no events (bench.py times a sample of the solves in its timed region). */
+HGM_API int hgm_kernel_timing_pause(hgm_ctx* ctx, int paused);
 
 #ifdef __cplusplus
 }
