@@ -122,6 +122,70 @@ __device__ __forceinline__ T apply_epi(T t, T a, const T* __restrict__ z, int64_
     return t;
 }
 
+// Epilogues with the pending normalisation (internal.h PendNorm); h from pn_pre / pn_fin.
+template <typename T, int EPI>
+__device__ __forceinline__ T apply_epi_pn(T t, T a, const T* __restrict__ z, int64_t i, const PendNorm<T>& pn, T h) {
+    if constexpr (EPI == EPI_DIVH) {
+        return h != T(0) ? t / h : t;
+    } else if constexpr (EPI == EPI_ADDQ) {
+        const T v = z[i];
+        const T q = h != T(0) ? v / h : v;   // a zero norm (breakdown) leaves v as k_mgs_normalize does
+        if (pn.q) pn.q[i] = q;
+        const T s = a * q;
+        return t + s;
+    } else {
+        return apply_epi<T, EPI>(t, a, z, i);
+    }
+}
+
+// The same epilogues with the operand z_i already loaded (zi; the row kernel issues that
+// load at kernel start so it overlaps the product instead of following it).
+template <typename T, int EPI>
+__device__ __forceinline__ T apply_epi_zv(T t, T a, T zi, int64_t i, const PendNorm<T>& pn, T h) {
+    if constexpr (EPI == EPI_ADD) { T s = a * zi; return t + s; }
+    if constexpr (EPI == EPI_SUB) { T s = a * zi; return t - s; }
+    if constexpr (EPI == EPI_RSUB) return zi - t;
+    if constexpr (EPI == EPI_DIVH) return h != T(0) ? t / h : t;
+    if constexpr (EPI == EPI_ADDQ) {
+        const T q = h != T(0) ? zi / h : zi;
+        if (pn.q) pn.q[i] = q;
+        const T s = a * q;
+        return t + s;
+    }
+    return t;
+}
+
+// h of the pending normalisation, in two halves so that its loads are issued at kernel
+// start and overlap the product: pn_pre returns this thread's share (EPI_DIVH: its
+// strided partial sum, the order of reduce_parts; EPI_ADDQ: h itself), pn_fin the value.
+// EPI_DIVH: every thread of the block must call pn_fin (block sum, same bits as
+// k_mgs_normalize's sqrt(sum)); block 0 publishes h to hdev and the host ring.
+template <typename T, int EPI>
+__device__ __forceinline__ T pn_pre(const PendNorm<T>& pn) {
+    if constexpr (EPI == EPI_DIVH) {
+        T a = 0;
+        for (int i = threadIdx.x; i < pn.np; i += BS) a += pn.parts[i];
+        return a;
+    } else if constexpr (EPI == EPI_ADDQ) {
+        return *pn.hdev;
+    } else {
+        return T(1);
+    }
+}
+template <typename T, int EPI>
+__device__ __forceinline__ T pn_fin(const PendNorm<T>& pn, T pre, T* sh) {
+    if constexpr (EPI == EPI_DIVH) {
+        const T h = sqrt(block_sum_all<T, true>(pre, sh));
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            pn.hdev[0] = h;
+            st_sys(pn.hring, h);
+        }
+        return h;
+    } else {
+        return pre;
+    }
+}
+
 // Raw buffer access (gfx9 resource word 3 = 0x00020000): the range check against
 // `bytes` returns 0 for loads and drops stores past the end, and one 32-bit lane
 // offset serves every resource, so unrolled strided loops keep one address VGPR.

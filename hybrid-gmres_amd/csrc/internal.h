@@ -173,14 +173,32 @@ inline int64_t stream_chunks(int64_t nnz) { return (nnz + SCH - 1) / SCH; }
 namespace hgm {
 
 // ---------------- kernels (kernels.hip) ----------------
-enum Epi { EPI_NONE = 0, EPI_ADD = 1, EPI_SUB = 2, EPI_RSUB = 3 };
+enum Epi { EPI_NONE = 0, EPI_ADD = 1, EPI_SUB = 2, EPI_RSUB = 3, EPI_DIVH = 4, EPI_ADDQ = 5 };
+
+// Pending normalisation of the Krylov vector (gmres_family): Q(:,k) holds
+// v_k before its division by h = H(k,k-1) = sqrt(sum parts), and the step's two SpMVs apply
+// it in their epilogues instead of a separate scale pass:
+//   EPI_DIVH (A): y = (A v) / h; every block sums `parts` in the fixed order of
+//                 k_mgs_normalize, block 0 stores h to hdev and to the host ring (hring);
+//   EPI_ADDQ (B): y = t + a (v_r / h), h from hdev (q written back over v when q != nullptr;
+//                 the GMRES step leaves that to the MGS dots kernel).
+template <typename T>
+struct PendNorm {
+    const T* parts = nullptr;
+    int np = 0;
+    T* hdev = nullptr;
+    T* hring = nullptr;
+    T* q = nullptr;
+};
 
 int pick_group(int64_t rows, int64_t nnz);
 // y = epi(M x): EPI_ADD: t + a*z ; EPI_SUB: t - a*z ; EPI_RSUB: z - t  (two roundings, no FMA)
 // sumsq_out (optional, device): also *sumsq_out = sum_r y_r^2 (fused into the row kernel)
 template <typename T>
 void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, int kclass,
-          T* sumsq_out = nullptr);
+          T* sumsq_out = nullptr, const PendNorm<T>* pn = nullptr);
+// whether spmv() can apply EPI_DIVH / EPI_ADDQ for this operator's kernel choice
+bool spmv_pn_ok(const hgm_mat* M, int epi);
 template <typename T>
 void epilogue(hgm_ctx* c, int64_t n, T* y, int epi, T a, const T* z);
 
@@ -228,7 +246,11 @@ bool krylov_padded(int64_t ldq);
 // side (optional): a multidot enqueued with the sweep (see MdotJob).
 template <typename T>
 void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, const T* src = nullptr,
-         const MdotJob<T>* side = nullptr);
+         const MdotJob<T>* side = nullptr, PendNorm<T>* defer = nullptr, const T* pend_h = nullptr);
+// defer (single GPU, one-reduction form only): leave v = Q(:,kk+1) unnormalised and return
+// its norm partials in *defer (np > 0) for the next step's SpMV epilogues (EPI_DIVH / EPI_ADDQ);
+// np == 0 on return means the sweep normalised v itself.  pend_h (device h): Q(:,kk) still
+// holds v_kk from the previous step's deferral; the dots kernel divides it and writes q_kk.
 template <typename T>
 void cgs2(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist);
 

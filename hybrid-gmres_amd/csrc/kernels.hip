@@ -631,10 +631,12 @@ __device__ __forceinline__ void mgs1_substitute(int kk, const T* sr, const T* sG
     }
 }
 
+// hpend (pending normalisation, internal.h PendNorm): Q(:,k) still holds v_k; every block
+// uses q_k = v_k / *hpend (k_mgs1_update writes q_k back once this kernel is done).
 template <typename T>
-__global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* __restrict__ Q, int64_t ldq, int kk,
+__global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* Q, int64_t ldq, int kk,
                                                   const T* __restrict__ w, int npr, T* __restrict__ pr,
-                                                  T* __restrict__ pg, MdotStage<T> side) {
+                                                  T* __restrict__ pg, MdotStage<T> side, const T* hpend) {
     using T2 = typename V2<T>::t;
     __shared__ T sh[4][2 * MGS1_CG];
     const int ncg = (kk + MGS1_CG) / MGS1_CG;   // ceil((kk+1) / CG)
@@ -650,16 +652,22 @@ __global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* __restrict
     const T2* w2 = reinterpret_cast<const T2*>(w);
     const T2* qk2 = reinterpret_cast<const T2*>(Q + (int64_t)kk * ldq);
     const T* qc = Q + (int64_t)c0 * ldq;
+    const T hp = hpend ? *hpend : T(0);
+    auto scale = [&](T v) -> T { return hp != T(0) ? v / hp : v; };   // as k_mgs_normalize
     T ar[MGS1_CG], ag[MGS1_CG];
 #pragma unroll
     for (int c = 0; c < MGS1_CG; ++c) ar[c] = ag[c] = T(0);
     for (int64_t i = (int64_t)rb * BS + threadIdx.x; i < n2; i += stride) {
         const T2 ww = w2[i];
-        const T2 qk = qk2[i];
+        T2 qk = qk2[i];
+        if (hpend) {
+            qk.x = scale(qk.x);
+            qk.y = scale(qk.y);
+        }
         T2 q[MGS1_CG];
 #pragma unroll
         for (int c = 0; c < MGS1_CG; ++c)
-            if (c < nc) q[c] = reinterpret_cast<const T2*>(qc + (int64_t)c * ldq)[i];
+            if (c < nc) q[c] = (hpend && c0 + c == kk) ? qk : reinterpret_cast<const T2*>(qc + (int64_t)c * ldq)[i];
 #pragma unroll
         for (int c = 0; c < MGS1_CG; ++c)
             if (c < nc) {
@@ -669,11 +677,12 @@ __global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* __restrict
     }
     if ((n & 1) && rb == npr - 1 && threadIdx.x == 0) {
         const int64_t i = n - 1;
-        const T wi = w[i], qki = Q[(int64_t)kk * ldq + i];
+        const T wi = w[i];
+        const T qki = hpend ? scale(Q[(int64_t)kk * ldq + i]) : Q[(int64_t)kk * ldq + i];
 #pragma unroll
         for (int c = 0; c < MGS1_CG; ++c)
             if (c < nc) {
-                const T qi = qc[(int64_t)c * ldq + i];
+                const T qi = (hpend && c0 + c == kk) ? qki : qc[(int64_t)c * ldq + i];
                 ar[c] = __builtin_fma(qi, wi, ar[c]);
                 ag[c] = __builtin_fma(qi, qki, ag[c]);
             }
@@ -755,9 +764,11 @@ __global__ __launch_bounds__(MGS1_SBS) void k_mgs1_solve(int kk, const T* __rest
 }
 
 template <typename T>
-__global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, const T* __restrict__ Q, int64_t ldq, int kk,
+// hpend: Q(:,k) still holds v_k (pending normalisation): q_k = v_k / *hpend is used for the
+// last term and written back (each element by the one thread that updates it).
+__global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, T* Q, int64_t ldq, int kk,
                                                     const T* w, T* v, const T* __restrict__ hdev, T* Hcol,
-                                                    T* __restrict__ pout, MdotStage<T> side) {
+                                                    T* __restrict__ pout, MdotStage<T> side, const T* hpend) {
     using T2 = typename V2<T>::t;
     __shared__ T hs[MGS1_MAXC];
     __shared__ T sh[4];
@@ -774,12 +785,23 @@ __global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, const T* 
     const int64_t n2 = n >> 1, stride = (int64_t)nb * BS;
     const T2* w2 = reinterpret_cast<const T2*>(w);
     T2* v2 = reinterpret_cast<T2*>(v);
+    const T hp = hpend ? *hpend : T(0);
+    auto scale = [&](T x) -> T { return hp != T(0) ? x / hp : x; };   // as k_mgs_normalize
+    const int jn = hpend ? kk : kk + 1;                               // columns read as stored
+    T2* qk2 = reinterpret_cast<T2*>(Q + (int64_t)kk * ldq);
     T acc0 = 0, acc1 = 0;
     for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n2; i += stride) {
         T2 vv = w2[i];
+        T2 qkk{0, 0};
+        if (hpend) {
+            qkk = qk2[i];
+            qkk.x = scale(qkk.x);
+            qkk.y = scale(qkk.y);
+            qk2[i] = qkk;
+        }
         const T* q = Q;
         int j = 0;
-        for (; j + 4 <= kk + 1; j += 4, q += 4 * ldq) {
+        for (; j + 4 <= jn; j += 4, q += 4 * ldq) {
             T2 qq[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) qq[u] = reinterpret_cast<const T2*>(q + (int64_t)u * ldq)[i];
@@ -792,7 +814,7 @@ __global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, const T* 
             }
         }
         for (; j <= kk; ++j, q += ldq) {
-            const T2 qq = reinterpret_cast<const T2*>(q)[i];
+            const T2 qq = (j == kk && hpend) ? qkk : reinterpret_cast<const T2*>(q)[i];
             const T h = hs[j];
             const T p0 = h * qq.x, p1 = h * qq.y;
             vv.x = vv.x - p0;
@@ -805,8 +827,13 @@ __global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, const T* 
     if ((n & 1) && (int)blockIdx.x == nb - 1 && threadIdx.x == 0) {
         const int64_t i = n - 1;
         T vv = w[i];
+        T qkk = 0;
+        if (hpend) {
+            qkk = scale(Q[(int64_t)kk * ldq + i]);
+            Q[(int64_t)kk * ldq + i] = qkk;
+        }
         for (int j = 0; j <= kk; ++j) {
-            const T p = hs[j] * Q[(int64_t)j * ldq + i];
+            const T p = hs[j] * ((j == kk && hpend) ? qkk : Q[(int64_t)j * ldq + i]);
             vv = vv - p;
         }
         v[i] = vv;
@@ -818,7 +845,10 @@ __global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, const T* 
 
 template <typename T>
 void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, const T* src,
-         const MdotJob<T>* side) {
+         const MdotJob<T>* side, PendNorm<T>* defer, const T* pend_h) {
+    if (defer) defer->np = 0;
+    HGM_REQUIRE(!pend_h || (!dist && kk + 1 <= MGS1_MAXC && mgs1_mode() == 1 && !krylov_padded(ldq)),
+                "mgs: pending normalisation needs the one-reduction form");
     hipEvent_t t0 = nullptr;
     timing_begin(c, KC_MGS, &t0);
     const double s = sizeof(T);
@@ -847,7 +877,7 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
         T* Gt = c->buf<T>("mgs1_G", (size_t)MGS1_MAXC * MGS1_MAXC / 2 + MGS1_MAXC);
         T* hdev = c->buf<T>("mgs1_h", MGS1_MAXC + 2);
         const size_t lds = sizeof(T) * ((size_t)kk * (kk + 1) / 2 + 1);
-        k_mgs1_dots<T><<<npr * ncg + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1);
+        k_mgs1_dots<T><<<npr * ncg + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1, pend_h);
         if (dist) {
             T* redd = c->buf<T>("mgs1_red", 2 * MGS1_MAXC + 2);
             k_mgs1_solve<T, 1><<<1, MGS1_SBS, 0, st>>>(kk, pr, pg, npr, redd, Gt, hdev);
@@ -858,7 +888,15 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
         }
         const int nb = gemv_blocks(n, mgs_ppl());
         T* pout = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
-        k_mgs1_update<T><<<nb + s2.blocks(), BS, 0, st>>>(n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout, s2);
+        k_mgs1_update<T><<<nb + s2.blocks(), BS, 0, st>>>(n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout, s2, pend_h);
+        if (defer && !dist && kk + 2 <= MGS1_MAXC) {   // the next step must be one-reduction too
+            // the next step's SpMVs divide by H(kk+1,kk) in their epilogues
+            HGM_HIP(hipGetLastError());
+            defer->parts = pout;
+            defer->np = nb;
+            timing_end(c, KC_MGS, t0, s * n * (2.0 * kk + 6.0));
+            return;
+        }
         T* ss = c->buf<T>("mgs_ss", 4);
         if (dist) {
             k_finalize<T><<<1, BS, 0, st>>>(pout, nb, ss);
@@ -1120,7 +1158,8 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
     template void gemv_err<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, const T*, T*); \
     template void recon<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, const T*, T*, int64_t, \
                            const T*, int64_t, const T*, T*);                                   \
-    template void mgs<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool, const T*, const MdotJob<T>*);                       \
+    template void mgs<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool, const T*, const MdotJob<T>*, PendNorm<T>*,   \
+                         const T*);                       \
     template void cgs2<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool);                      \
     template void gemv<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, int);       \
     template void div_scalar<T>(hgm_ctx*, int64_t, const T*, T*, T);                           \

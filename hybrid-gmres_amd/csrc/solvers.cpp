@@ -177,6 +177,48 @@ struct GmresSpec {
     bool x_preassigned;   // hybrid_ba_gmres_rtp.m:4 initialises x = zeros
 };
 
+// Ring polling (single GPU): the host waits for step k by watching the entries of ring
+// slot k turn from a NaN sentinel into values instead of an event recorded after the step.
+// A recorded event (a marker packet, or a completion signal on the step's last dispatch)
+// makes the next kernel wait for an end-of-kernel release: ~4.5 us per step on the main
+// stream (rocprofv3 trace).  Every ring entry is written exactly once per
+// solve by a system-scope store (st_sys), so a non-sentinel value is final.
+constexpr uint64_t RING_SENTINEL = 0x7FF4DEADBEEF0001ull;   // a NaN no kernel produces
+static bool ring_poll_on() {
+    const char* e = std::getenv("HGM_RING_POLL");
+    return !e || std::atoi(e) != 0;
+}
+// Spin until ring[i] for i in idx are all non-sentinel.  Checks the stream for errors (and
+// for going idle with an entry never written, a bug) once per ms so a fault cannot hang.
+static void ring_wait(hgm_ctx* c, const double* ring, const std::vector<size_t>& idx) {
+    const volatile uint64_t* r = reinterpret_cast<const volatile uint64_t*>(ring);
+    const auto t0 = std::chrono::steady_clock::now();
+    auto last = t0;
+    bool idle_seen = false;
+    for (;;) {
+        bool all = true;
+        for (size_t i : idx)
+            if (r[i] == RING_SENTINEL) {
+                all = false;
+                break;
+            }
+        if (all) break;
+        const auto now = std::chrono::steady_clock::now();
+        if (now - last > std::chrono::milliseconds(1)) {
+            last = now;
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q != hipSuccess && q != hipErrorNotReady) HGM_HIP(q);
+            if (q == hipSuccess) {
+                if (idle_seen) throw Error{HGM_E_HIP, "ring poll: stream idle with a ring entry never written"};
+                idle_seen = true;   // one more round: the last stores may still be in flight
+            }
+        }
+    }
+    if (c->host_stats) {
+        c->wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+}
+
 // n from which the GMRES reconstruction is serialised on the main stream (see gmres_family)
 static int64_t recon_serial_min_n() {
     static int64_t v = -1;
@@ -251,6 +293,11 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     if (rs_stream != st) HGM_HIP(hipStreamSynchronize(rs_stream));
     pinned_ring(c, sizeof(double) * ring_n);
     const double* hr = c->hring;
+    const bool poll = zc && ring_poll_on();
+    if (poll) {
+        uint64_t* r = reinterpret_cast<uint64_t*>(c->hring);
+        for (size_t i = 0; i < (size_t)maxit * LH; ++i) r[i] = RING_SENTINEL;
+    }
     T* dr = zc ? c->hring_dev : c->buf<T>("ring_dev", ring_n);
     auto publish = [&](size_t off, size_t cnt) {
         if (!zc)
@@ -285,12 +332,34 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     int k = 0;
     std::vector<double> y, rhs, M;
     std::vector<double> G((size_t)maxit * maxit, 0.0), cvec(maxit, 0.0);
+    // Pending normalisation (single GPU, n-space, one-reduction MGS): step k
+    // leaves v_{k+1} = Q(:,k+1) undivided and step k+1 applies q = v / H(k+1,k) where it reads
+    // it — A: (A*v)/h, which also publishes h = H(k+1,k); B: B*(A*q) + lambda*q; the MGS dots
+    // kernel writes q back over v — so the sweep needs no scale pass.  Step k's event is then
+    // recorded at the end of step k+1.  HGM_PEND_NORM=0 keeps the scale pass.
+    const char* pn_env = std::getenv("HGM_PEND_NORM");
+    const bool pn_ok = nspace && !dist && orth == HGM_MGS && (!pn_env || std::atoi(pn_env) != 0) &&
+                       spmv_pn_ok(A, EPI_DIVH) && spmv_pn_ok(B, EPI_ADDQ);
+    PendNorm<T> pend;                                  // np > 0: Q(:,next step) awaits its division
+    T* pn_h = c->buf<T>("pn_h", 2);
     // Enqueue Arnoldi step kq: operator application + orthogonalisation (+ Gram column).
     auto enqueue_step = [&](int kq) {
         T* qk = Q + (int64_t)kq * ldq;
         T* v = Q + (int64_t)(kq + 1) * ldq;
+        const bool pending_in = pend.np > 0;
         // ---- operator (hybrid_*_rtp.m:19 ; *_bounds.m:25) ----
-        if (nspace) {
+        if (nspace && pending_in) {
+            T* Aq = AQ ? AQ + (int64_t)kq * ldaq : t;
+            PendNorm<T> pa = pend;
+            pa.hdev = pn_h;
+            pa.hring = dr + (size_t)(kq - 1) * LH + kq;    // H(kq, kq-1) of step kq-1
+            spmv<T>(c, A, qk, Aq, EPI_DIVH, T(0), nullptr, KC_SPMV_A, nullptr, &pa);   // A*q = (A*v)/h
+            PendNorm<T> pb;
+            pb.hdev = pn_h;
+            // B*(A*q) + lambda*q with q = v/h (lambda = 0: B*(A*q) + 0*q); the MGS dots kernel
+            // writes q back over v
+            spmv<T>(c, B, Aq, v, EPI_ADDQ, T(sp.lambda_in_op ? lambda : 0.0), qk, KC_SPMV_B, nullptr, &pb);
+        } else if (nspace) {
             T* Aq = AQ ? AQ + (int64_t)kq * ldaq : t;
             apply_A<T>(c, A, qk, Aq, EPI_NONE, T(0), nullptr);
             if (sp.lambda_in_op) apply_B<T>(c, B, Aq, v, EPI_ADD, T(lambda), qk);   // B*(A*v) + lambda*v
@@ -329,10 +398,22 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             cgs2<T>(c, dim, Q, ldq, kq, Hcol, dist);
             if (side) multidot<T>(c, m, gram.ncols, AQ, ldaq, gram.w, gram.out, b);
         } else {
-            mgs<T>(c, dim, Q, ldq, kq, Hcol, dist, (!nspace && ABQ) ? ABQ + (int64_t)kq * ldaq : nullptr, side);
+            PendNorm<T>* defer = (pn_ok && kq + 1 < maxit) ? &pend : nullptr;
+            if (!defer) pend.np = 0;
+            mgs<T>(c, dim, Q, ldq, kq, Hcol, dist, (!nspace && ABQ) ? ABQ + (int64_t)kq * ldaq : nullptr, side,
+                   defer, pending_in ? (const T*)pn_h : nullptr);
         }
-        publish((size_t)kq * LH, LH);
-        step_record(c, kq);
+        // Step kq-1's column is complete (H(kq,kq-1) came from this step's A product).  The
+        // event goes at the end of the step: a marker between two kernels costs a bubble.
+        if (poll) return;                                 // the host polls the ring instead
+        if (nspace && pending_in) {
+            publish((size_t)(kq - 1) * LH, LH);
+            step_record(c, kq - 1);
+        }
+        if (pend.np == 0) {                               // else: recorded at the end of step kq+1
+            publish((size_t)kq * LH, LH);
+            step_record(c, kq);
+        }
     };
     // Reconstruction + monitors of iteration kq from y_kq (in the ring) on the auxiliary
     // stream, then the event the host waits on.  Everything it reads (Q(:,0..kq), y_kq)
@@ -396,7 +477,19 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     bool done = false;
     for (k = 0; k < maxit; ++k) {
         if (k >= 1) pipe_wait(c);                        // R_{k-1}
-        step_wait(c, k);                                 // S_k: H(:,k) (+ Gram column k)
+        if (poll) {
+            // S_k: H(0:k+1,k) (+ Gram column k).  H(k+1,k) is written by a kernel that starts
+            // after every kernel of step k has finished (the scale pass of step k, or with the
+            // pending normalisation the A product of step k+1), so once it is visible Q(:,0:k)
+            // and the kept products of step k, which R_k reads, are complete.
+            std::vector<size_t> idx;
+            for (int i = 0; i < k + 2; ++i) idx.push_back((size_t)k * LH + i);
+            if (sp.proj == PROJ_ABRTP)
+                for (int i = 0; i < k + 2; ++i) idx.push_back((size_t)k * LH + (maxit + 2) + i);
+            ring_wait(c, hr, idx);
+        } else {
+            step_wait(c, k);                             // S_k: H(:,k) (+ Gram column k)
+        }
         if (k >= 1) {
             const double* mk = hr + offM + 2 * (size_t)(k - 1);
             res[k - 1] = std::sqrt(mk[0]) / nb;

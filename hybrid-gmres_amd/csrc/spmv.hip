@@ -113,17 +113,24 @@ __global__ __launch_bounds__(BS) void k_spmv(int64_t rows, const int64_t* __rest
                                              const IX* __restrict__ ci,
                                              const T* __restrict__ val, const T* __restrict__ x,
                                              T* __restrict__ y, T a, const T* __restrict__ z, int xcd,
-                                             T* __restrict__ nparts) {
+                                             T* __restrict__ nparts, PendNorm<T> pn) {
     constexpr int RPB = BS / G;
     const int64_t blk = xcd ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
     const int64_t row = blk * RPB + threadIdx.x / G;
     const int gl = threadIdx.x & (G - 1);
+    const T hpre = pn_pre<T, EPI>(pn);
+    T zr = T(0);   // epilogue operand, loaded up front
+    if constexpr (EPI != EPI_NONE && EPI != EPI_DIVH) {
+        if (gl == 0 && row < rows) zr = z[row];
+    }
     T acc = 0;
     if (row < rows) acc = seg_partial<T, G, VEC, NT, IX>(rp[row], rp[row + 1], gl, ci, val, x);
     acc = group_sum<T, G>(acc);
+    __shared__ T hsh[4];
+    const T h = pn_fin<T, EPI>(pn, hpre, hsh);
     T r = 0;
     if (gl == 0 && row < rows) {
-        r = apply_epi<T, EPI>(acc, a, z, row);
+        r = apply_epi_zv<T, EPI>(acc, a, zr, row, pn, h);
         y[row] = r;
     }
     if (NRM) {
@@ -186,7 +193,8 @@ __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, c
                                                     const int32_t* __restrict__ fo, const IX* __restrict__ ci,
                                                     const T* __restrict__ val, const T* __restrict__ x,
                                                     T* __restrict__ out, T a, const T* __restrict__ z,
-                                                    T* __restrict__ head, T* __restrict__ tail) {
+                                                    T* __restrict__ head, T* __restrict__ tail, PendNorm<T> pn) {
+    static_assert(EPI != EPI_DIVH, "EPI_DIVH is applied by the band reduction or the row kernel");
     using T2 = typename NV2<T>::t;
     using IV2 = std::conditional_t<sizeof(IX) == 2, nus2, ni2>;   // index pair / quad of the type
     using IV4 = std::conditional_t<sizeof(IX) == 2, nus4, ni4>;
@@ -202,7 +210,9 @@ __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, c
     // scheduling barriers keep the compiler from hoisting its waits above those loads.
     const int gid = threadIdx.x / G, gl = threadIdx.x & (G - 1);
     int64_t s_begin, s_end, q, sp_b, pm, p0, p1;
+    T h = T(1);
     auto bookkeeping = [&]() {
+        h = pn_pre<T, EPI>(pn);
         s_begin = fo[k];
         s_end = fo[k + 1];
         q = s_begin + gid;
@@ -281,7 +291,7 @@ __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, c
         if (gl == 0) {
             if (has_head && t == 0) head[k] = acc;
             else if (send > c1) tail[k] = acc;
-            else out[s] = apply_epi<T, EPI>(acc, a, z, s);
+            else out[s] = apply_epi_pn<T, EPI>(acc, a, z, s, pn, h);
         }
     }
 }
@@ -290,7 +300,9 @@ template <typename T, int EPI>
 __global__ __launch_bounds__(BS) void k_stream_fixup(int64_t nnz, int64_t nchunks, const int64_t* __restrict__ sp,
                                                      const int32_t* __restrict__ fo, T* __restrict__ out, T a,
                                                      const T* __restrict__ z, const T* __restrict__ head,
-                                                     const T* __restrict__ tail) {
+                                                     const T* __restrict__ tail, PendNorm<T> pn) {
+    static_assert(EPI != EPI_DIVH, "EPI_DIVH is applied by the band reduction or the row kernel");
+    const T h = pn_pre<T, EPI>(pn);
     for (int64_t k = (int64_t)blockIdx.x * BS + threadIdx.x; k < nchunks; k += (int64_t)gridDim.x * BS) {
         const int64_t s_begin = fo[k], s_end = fo[k + 1];
         if (s_end <= s_begin) continue;
@@ -303,7 +315,7 @@ __global__ __launch_bounds__(BS) void k_stream_fixup(int64_t nnz, int64_t nchunk
             const int64_t cj1 = (j + 1) * SCH < nnz ? (j + 1) * SCH : nnz;
             if (sp[s + 1] <= cj1) break;
         }
-        out[s] = apply_epi<T, EPI>(sum, a, z, s);
+        out[s] = apply_epi_pn<T, EPI>(sum, a, z, s, pn, h);
     }
 }
 
@@ -316,11 +328,14 @@ __global__ __launch_bounds__(BS) void k_fill_epi(int64_t n, T* __restrict__ out,
 // y[r] = epi( sum_b ypart[b*rows + r] ), bands summed in increasing b (deterministic)
 template <typename T, int EPI>
 __global__ __launch_bounds__(BS) void k_band_reduce(int64_t rows, int nbands, const T* __restrict__ ypart,
-                                                    T* __restrict__ y, T a, const T* __restrict__ z) {
+                                                    T* __restrict__ y, T a, const T* __restrict__ z,
+                                                    PendNorm<T> pn) {
+    __shared__ T hsh[4];
+    const T h = pn_fin<T, EPI>(pn, pn_pre<T, EPI>(pn), hsh);
     for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BS) {
         T s = 0;
         for (int b = 0; b < nbands; ++b) s += ypart[(int64_t)b * rows + r];
-        y[r] = apply_epi<T, EPI>(s, a, z, r);
+        y[r] = apply_epi_pn<T, EPI>(s, a, z, r, pn, h);
     }
 }
 
@@ -347,7 +362,7 @@ __global__ __launch_bounds__(BS) void k_epi(int64_t n, T* __restrict__ y, T a, c
 // ------------------------------------------------------------------------------
 template <typename T, int G, int EPI, bool NT, typename IX>
 static void launch_stream_e(hgm_ctx* c, bool last, const SegIndex& si, const IX* ci, const T* val, const T* x,
-                            T* out, T a, const T* z, T* head, T* tail) {
+                            T* out, T a, const T* z, T* head, T* tail, const PendNorm<T>& pn) {
     if (si.nnz == 0) {
         int64_t g = (si.nseg + BS - 1) / BS;
         if (g > 4096) g = 4096;
@@ -355,32 +370,33 @@ static void launch_stream_e(hgm_ctx* c, bool last, const SegIndex& si, const IX*
         return;
     }
     launch(c, false, k_spmv_stream<T, G, EPI, NT, IX>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg, si.sp, si.fo, ci,
-           val, x, out, a, z, head, tail);
+           val, x, out, a, z, head, tail, pn);
     int64_t g = (si.nchunks + BS - 1) / BS;
     if (g > 4096) g = 4096;
     launch(c, last, k_stream_fixup<T, EPI>, dim3(g), dim3(BS), si.nnz, si.nchunks, si.sp, si.fo, out, a, z,
-           (const T*)head, (const T*)tail);
+           (const T*)head, (const T*)tail, pn);
 }
 
 template <typename T, int G, bool NT, typename IX>
 static void launch_stream_g(hgm_ctx* c, bool last, const SegIndex& si, const IX* ci, const T* val, const T* x,
-                            T* out, int epi, T a, const T* z, T* head, T* tail) {
+                            T* out, int epi, T a, const T* z, T* head, T* tail, const PendNorm<T>& pn) {
     switch (epi) {
-        case EPI_NONE: launch_stream_e<T, G, EPI_NONE, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail); break;
-        case EPI_ADD: launch_stream_e<T, G, EPI_ADD, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail); break;
-        case EPI_SUB: launch_stream_e<T, G, EPI_SUB, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail); break;
-        default: launch_stream_e<T, G, EPI_RSUB, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail); break;
+        case EPI_NONE: launch_stream_e<T, G, EPI_NONE, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn); break;
+        case EPI_ADD: launch_stream_e<T, G, EPI_ADD, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn); break;
+        case EPI_SUB: launch_stream_e<T, G, EPI_SUB, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn); break;
+        case EPI_ADDQ: launch_stream_e<T, G, EPI_ADDQ, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn); break;
+        default: launch_stream_e<T, G, EPI_RSUB, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn); break;
     }
 }
 
 template <typename T, typename IX = int32_t>
 static void spmv_stream(hgm_ctx* c, bool last, const SegIndex& si, int G, bool nt, const IX* ci, const T* val,
-                        const T* x, T* out, int epi, T a, const T* z) {
+                        const T* x, T* out, int epi, T a, const T* z, const PendNorm<T>& pn = PendNorm<T>{}) {
     T* head = c->buf<T>("stream_head", si.nchunks + 1);
     T* tail = c->buf<T>("stream_tail", si.nchunks + 1);
 #define HGM_SG(GG)                                                                                  \
-    if (nt) launch_stream_g<T, GG, true, IX>(c, last, si, ci, val, x, out, epi, a, z, head, tail);  \
-    else launch_stream_g<T, GG, false, IX>(c, last, si, ci, val, x, out, epi, a, z, head, tail);
+    if (nt) launch_stream_g<T, GG, true, IX>(c, last, si, ci, val, x, out, epi, a, z, head, tail, pn);  \
+    else launch_stream_g<T, GG, false, IX>(c, last, si, ci, val, x, out, epi, a, z, head, tail, pn);
     switch (G) {
         case 64: HGM_SG(64) break;
         case 32: HGM_SG(32) break;
@@ -392,7 +408,8 @@ static void spmv_stream(hgm_ctx* c, bool last, const SegIndex& si, int G, bool n
 }
 
 template <typename T, int G, bool VEC, bool NT, typename IX = int32_t>
-static void launch_spmv_v(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
+static void launch_spmv_v(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z,
+                          const PendNorm<T>& pn) {
     const int64_t nb = (M->rows + (BS / G) - 1) / (BS / G);
     if (nb == 0) return;
     const T* val = reinterpret_cast<const T*>(M->val);
@@ -401,10 +418,12 @@ static void launch_spmv_v(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int ep
     const dim3 g((unsigned)nb), b(BS);
     T* np_ = nullptr;
     switch (epi) {
-        case EPI_NONE: launch(c, true, k_spmv<T, G, EPI_NONE, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_); break;
-        case EPI_ADD: launch(c, true, k_spmv<T, G, EPI_ADD, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_); break;
-        case EPI_SUB: launch(c, true, k_spmv<T, G, EPI_SUB, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_); break;
-        default: launch(c, true, k_spmv<T, G, EPI_RSUB, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_); break;
+        case EPI_NONE: launch(c, true, k_spmv<T, G, EPI_NONE, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_, pn); break;
+        case EPI_ADD: launch(c, true, k_spmv<T, G, EPI_ADD, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_, pn); break;
+        case EPI_SUB: launch(c, true, k_spmv<T, G, EPI_SUB, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_, pn); break;
+        case EPI_DIVH: launch(c, true, k_spmv<T, G, EPI_DIVH, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_, pn); break;
+        case EPI_ADDQ: launch(c, true, k_spmv<T, G, EPI_ADDQ, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_, pn); break;
+        default: launch(c, true, k_spmv<T, G, EPI_RSUB, VEC, NT, false, IX>, g, b, M->rows, M->rp, ci, val, x, y, a, z, xcd, np_, pn); break;
     }
 }
 
@@ -421,14 +440,17 @@ static void launch_spmv_nrm_v(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, in
     T* parts = c->buf<T>("spmv_nparts", nb + 1);
     const dim3 g((unsigned)nb), b(BS);
     if (epi == EPI_SUB)
-        launch(c, true, k_spmv<T, G, EPI_SUB, VEC, NT, true>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, parts);
+        launch(c, true, k_spmv<T, G, EPI_SUB, VEC, NT, true>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, parts,
+               PendNorm<T>{});
     else
-        launch(c, true, k_spmv<T, G, EPI_RSUB, VEC, NT, true>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, parts);
+        launch(c, true, k_spmv<T, G, EPI_RSUB, VEC, NT, true>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z, xcd, parts,
+               PendNorm<T>{});
     hipLaunchKernelGGL(k_sum_parts<T>, dim3(1), dim3(BS), 0, c->stream, (const T*)parts, nb, out);
 }
 
 template <typename T, int G>
-static void launch_spmv_g(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, T* nrm = nullptr) {
+static void launch_spmv_g(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, T* nrm,
+                          const PendNorm<T>& pn) {
     const bool vec = M->variant & SPMV_VEC, nt = M->variant & SPMV_NT;
     if (nrm) {
         if (vec && nt) launch_spmv_nrm_v<T, G, true, true>(c, M, x, y, epi, a, z, nrm);
@@ -437,12 +459,12 @@ static void launch_spmv_g(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int ep
         else launch_spmv_nrm_v<T, G, false, false>(c, M, x, y, epi, a, z, nrm);
         return;
     }
-    if (vec && nt) launch_spmv_v<T, G, true, true>(c, M, x, y, epi, a, z);
-    else if (vec) launch_spmv_v<T, G, true, false>(c, M, x, y, epi, a, z);
-    else if (M->ci16 && nt) launch_spmv_v<T, G, false, true, uint16_t>(c, M, x, y, epi, a, z);
-    else if (M->ci16) launch_spmv_v<T, G, false, false, uint16_t>(c, M, x, y, epi, a, z);
-    else if (nt) launch_spmv_v<T, G, false, true>(c, M, x, y, epi, a, z);
-    else launch_spmv_v<T, G, false, false>(c, M, x, y, epi, a, z);
+    if (vec && nt) launch_spmv_v<T, G, true, true>(c, M, x, y, epi, a, z, pn);
+    else if (vec) launch_spmv_v<T, G, true, false>(c, M, x, y, epi, a, z, pn);
+    else if (M->ci16 && nt) launch_spmv_v<T, G, false, true, uint16_t>(c, M, x, y, epi, a, z, pn);
+    else if (M->ci16) launch_spmv_v<T, G, false, false, uint16_t>(c, M, x, y, epi, a, z, pn);
+    else if (nt) launch_spmv_v<T, G, false, true>(c, M, x, y, epi, a, z, pn);
+    else launch_spmv_v<T, G, false, false>(c, M, x, y, epi, a, z, pn);
 }
 
 template <typename T, int G, bool VEC, bool NT>
@@ -466,22 +488,27 @@ static void launch_band_g(hgm_ctx* c, const hgm_mat* M, const T* x, T* yp) {
 }
 
 template <typename T, int EPI>
-static void launch_band_reduce(hgm_ctx* c, const hgm_mat* M, const T* yp, T* y, T a, const T* z) {
-    launch(c, true, k_band_reduce<T, EPI>, dim3(grid_for(M->rows)), dim3(BS), M->rows, M->nbands, yp, y, a, z);
+static void launch_band_reduce(hgm_ctx* c, const hgm_mat* M, const T* yp, T* y, T a, const T* z,
+                               const PendNorm<T>& pn) {
+    launch(c, true, k_band_reduce<T, EPI>, dim3(grid_for(M->rows)), dim3(BS), M->rows, M->nbands, yp, y, a, z, pn);
 }
 
 template <typename T>
-static void band_reduce(hgm_ctx* c, const hgm_mat* M, const T* yp, T* y, int epi, T a, const T* z) {
+static void band_reduce(hgm_ctx* c, const hgm_mat* M, const T* yp, T* y, int epi, T a, const T* z,
+                        const PendNorm<T>& pn) {
     switch (epi) {
-        case EPI_NONE: launch_band_reduce<T, EPI_NONE>(c, M, yp, y, a, z); break;
-        case EPI_ADD: launch_band_reduce<T, EPI_ADD>(c, M, yp, y, a, z); break;
-        case EPI_SUB: launch_band_reduce<T, EPI_SUB>(c, M, yp, y, a, z); break;
-        default: launch_band_reduce<T, EPI_RSUB>(c, M, yp, y, a, z); break;
+        case EPI_NONE: launch_band_reduce<T, EPI_NONE>(c, M, yp, y, a, z, pn); break;
+        case EPI_ADD: launch_band_reduce<T, EPI_ADD>(c, M, yp, y, a, z, pn); break;
+        case EPI_SUB: launch_band_reduce<T, EPI_SUB>(c, M, yp, y, a, z, pn); break;
+        case EPI_DIVH: launch_band_reduce<T, EPI_DIVH>(c, M, yp, y, a, z, pn); break;
+        case EPI_ADDQ: launch_band_reduce<T, EPI_ADDQ>(c, M, yp, y, a, z, pn); break;
+        default: launch_band_reduce<T, EPI_RSUB>(c, M, yp, y, a, z, pn); break;
     }
 }
 
 template <typename T>
-static void spmv_banded(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
+static void spmv_banded(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z,
+                        const PendNorm<T>& pn) {
     T* yp = c->buf<T>("band_part", (size_t)M->nbands * M->rows + 1);
     switch (M->bgroup) {
         case 64: launch_band_g<T, 64>(c, M, x, yp); break;
@@ -490,46 +517,57 @@ static void spmv_banded(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi,
         case 8: launch_band_g<T, 8>(c, M, x, yp); break;
         default: launch_band_g<T, 4>(c, M, x, yp); break;
     }
-    band_reduce<T>(c, M, yp, y, epi, a, z);
+    band_reduce<T>(c, M, yp, y, epi, a, z, pn);
 }
 
 template <typename T>
-static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
+static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z,
+                          const PendNorm<T>& pn) {
     const bool nt = M->variant & SPMV_NT;
     if (M->nbands > 1) {
         T* yp = c->buf<T>("band_part", (size_t)M->nbands * M->rows + 1);
         SegIndex si{M->nnz, (int64_t)M->nbands * M->rows, stream_chunks(M->nnz), M->brp, M->bcfo};
         spmv_stream<T>(c, false, si, M->bsgroup, nt, M->bci, reinterpret_cast<const T*>(M->bval), x, yp, EPI_NONE,
                        T(0), nullptr);
-        band_reduce<T>(c, M, yp, y, epi, a, z);
+        band_reduce<T>(c, M, yp, y, epi, a, z, pn);
     } else {
         SegIndex si{M->nnz, M->rows, stream_chunks(M->nnz), M->rp, M->cfo};
         if (M->ci16)
             spmv_stream<T, uint16_t>(c, true, si, M->sgroup, nt, M->ci16, reinterpret_cast<const T*>(M->val), x, y,
-                                     epi, a, z);
+                                     epi, a, z, pn);
         else
-            spmv_stream<T>(c, true, si, M->sgroup, nt, M->ci, reinterpret_cast<const T*>(M->val), x, y, epi, a, z);
+            spmv_stream<T>(c, true, si, M->sgroup, nt, M->ci, reinterpret_cast<const T*>(M->val), x, y, epi, a, z, pn);
     }
 }
 
+bool spmv_pn_ok(const hgm_mat* M, int epi) {
+    if (M->nnz == 0) return false;
+    const bool stream = (M->variant & SPMV_STREAM) && (M->nbands > 1 ? M->bcfo != nullptr : M->cfo != nullptr);
+    if (epi == EPI_DIVH) return !(stream && M->nbands <= 1);   // row kernel or band reduction
+    return epi == EPI_ADDQ;
+}
+
 template <typename T>
-void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, int kclass, T* sumsq_out) {
+void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z, int kclass, T* sumsq_out,
+          const PendNorm<T>* pnp) {
+    const PendNorm<T> pn = pnp ? *pnp : PendNorm<T>{};
+    HGM_REQUIRE((epi != EPI_DIVH && epi != EPI_ADDQ) || (pnp && spmv_pn_ok(M, epi)), "spmv: pending-norm epilogue");
     hipEvent_t t0 = nullptr;
     timing_begin(c, kclass, &t0);
     const bool stream = (M->variant & SPMV_STREAM) && (M->nbands > 1 ? M->bcfo != nullptr : M->cfo != nullptr);
     const bool rowk = !stream && M->nbands <= 1;
     T* nrm = (rowk && (epi == EPI_SUB || epi == EPI_RSUB)) ? sumsq_out : nullptr;
     if (stream) {
-        spmv_streamed<T>(c, M, x, y, epi, a, z);
+        spmv_streamed<T>(c, M, x, y, epi, a, z, pn);
     } else if (M->nbands > 1) {
-        spmv_banded<T>(c, M, x, y, epi, a, z);
+        spmv_banded<T>(c, M, x, y, epi, a, z, pn);
     } else {
         switch (M->group) {
-            case 64: launch_spmv_g<T, 64>(c, M, x, y, epi, a, z, nrm); break;
-            case 32: launch_spmv_g<T, 32>(c, M, x, y, epi, a, z, nrm); break;
-            case 16: launch_spmv_g<T, 16>(c, M, x, y, epi, a, z, nrm); break;
-            case 8: launch_spmv_g<T, 8>(c, M, x, y, epi, a, z, nrm); break;
-            default: launch_spmv_g<T, 4>(c, M, x, y, epi, a, z, nrm); break;
+            case 64: launch_spmv_g<T, 64>(c, M, x, y, epi, a, z, nrm, pn); break;
+            case 32: launch_spmv_g<T, 32>(c, M, x, y, epi, a, z, nrm, pn); break;
+            case 16: launch_spmv_g<T, 16>(c, M, x, y, epi, a, z, nrm, pn); break;
+            case 8: launch_spmv_g<T, 8>(c, M, x, y, epi, a, z, nrm, pn); break;
+            default: launch_spmv_g<T, 4>(c, M, x, y, epi, a, z, nrm, pn); break;
         }
     }
     // other kernels: separate fixed-order reduction of the output
@@ -540,7 +578,8 @@ void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T*
     // 16-bit indices read (row kernel without paired loads, or the unbanded streaming kernel)
     const bool narrow = M->ci16 && ((rowk && !nrm && !(M->variant & SPMV_VEC)) || (stream && M->nbands <= 1));
     double bytes = (double)M->nnz * (s + (narrow ? 2 : 4)) + 8.0 * (M->rows + 1) + s * M->cols + s * M->rows;
-    if (epi != EPI_NONE) bytes += s * M->rows;
+    if (epi != EPI_NONE && epi != EPI_DIVH) bytes += s * M->rows;   // epilogue operand read
+    if (epi == EPI_ADDQ) bytes += s * M->rows;                       // ... and the normalised q written back
     timing_end(c, kclass, t0, bytes);
 }
 
@@ -578,8 +617,10 @@ void epilogue_to(hgm_ctx* c, int64_t n, const T* in, T* out, int epi, T a, const
 template void epilogue_to<double>(hgm_ctx*, int64_t, const double*, double*, int, double, const double*);
 template void epilogue_to<float>(hgm_ctx*, int64_t, const float*, float*, int, float, const float*);
 
-template void spmv<double>(hgm_ctx*, const hgm_mat*, const double*, double*, int, double, const double*, int, double*);
-template void spmv<float>(hgm_ctx*, const hgm_mat*, const float*, float*, int, float, const float*, int, float*);
+template void spmv<double>(hgm_ctx*, const hgm_mat*, const double*, double*, int, double, const double*, int, double*,
+                           const PendNorm<double>*);
+template void spmv<float>(hgm_ctx*, const hgm_mat*, const float*, float*, int, float, const float*, int, float*,
+                          const PendNorm<float>*);
 template void epilogue<double>(hgm_ctx*, int64_t, double*, int, double, const double*);
 template void epilogue<float>(hgm_ctx*, int64_t, float*, int, float, const float*);
 
