@@ -258,6 +258,8 @@ void cgs2(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist);
 template <typename T>
 void gemv(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y_dev, T* x, int mode);
 template <typename T> void div_scalar(hgm_ctx* c, int64_t n, const T* in, T* out, T s);
+// v = v / norm(v) on the device, *nrm_out = norm(v) (system-scope store, e.g. the host ring)
+template <typename T> void normalize_to(hgm_ctx* c, int64_t n, T* v, T* nrm_out);
 template <typename T> void lsqr_update(hgm_ctx* c, int64_t n, T* x, T* w, const T* v, T a, T b);
 template <typename T>
 void lsmr_update(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, const T* v, T c_hbar, T c_x, T c_h,

@@ -1026,6 +1026,25 @@ template <typename T> void div_scalar(hgm_ctx* c, int64_t n, const T* in, T* out
     HGM_HIP(hipGetLastError());
 }
 
+// v = v / sqrt(sum parts) (every block re-reduces the partials in the fixed order of
+// k_finalize); block 0 stores the norm to *nrm_out with a system-scope store.  Divides even by
+// a zero norm, as MATLAB's r0 / beta does.
+template <typename T>
+__global__ __launch_bounds__(BS) void k_vnorm(int64_t n, T* __restrict__ v, const T* __restrict__ parts, int np,
+                                              T* nrm_out) {
+    __shared__ T sh[4];
+    const T nrm = sqrt(reduce_parts<T, false>(parts, np, sh));
+    if (blockIdx.x == 0 && threadIdx.x == 0) st_sys(nrm_out, nrm);
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) v[i] = v[i] / nrm;
+}
+template <typename T> void normalize_to(hgm_ctx* c, int64_t n, T* v, T* nrm_out) {
+    const int np = parts_for(n);
+    T* parts = c->buf<T>("red_parts", MAX_PARTS);
+    k_reduce_partial<T, 1><<<np, BS, 0, c->stream>>>(n, v, v, parts);
+    k_vnorm<T><<<grid_for(n), BS, 0, c->stream>>>(n, v, parts, np, nrm_out);
+    HGM_HIP(hipGetLastError());
+}
+
 // lsqr_solver.m:40-41:  x = x + (phi/rho) w ;  w = v - (theta/rho) w
 template <typename T>
 __global__ __launch_bounds__(BS) void k_lsqr_update(int64_t n, T* __restrict__ x, T* __restrict__ w,
@@ -1158,6 +1177,7 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
     template void gemv_err<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, const T*, T*); \
     template void recon<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, const T*, T*, int64_t, \
                            const T*, int64_t, const T*, T*);                                   \
+    template void normalize_to<T>(hgm_ctx*, int64_t, T*, T*);                                                        \
     template void mgs<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool, const T*, const MdotJob<T>*, PendNorm<T>*,   \
                          const T*);                       \
     template void cgs2<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool);                      \

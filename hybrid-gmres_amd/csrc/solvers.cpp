@@ -149,6 +149,11 @@ void stage_out_n(hgm_ctx* c, double* out, const T* d, int64_t n, bool dev, const
         stage_out<T>(c, out, d, n, dev);
         return;
     }
+    if (dev && std::is_same<T, double>::value) {   // straight into the caller's device buffer
+        pix_permute<T>(c, o, d, reinterpret_cast<T*>(out), 1);
+        HGM_HIP(hipStreamSynchronize(c->stream));
+        return;
+    }
     T* q = c->buf<T>("out_pix", n);
     pix_permute<T>(c, o, d, q, 1);
     stage_out<T>(c, out, q, n, dev);
@@ -280,7 +285,8 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // all-reduced scalars live in a device mirror and each slot is copied out once.
     const size_t LH = 2 * (size_t)(maxit + 2);
     const size_t offM = (size_t)maxit * LH, offY = offM + 2 * (size_t)maxit;
-    const size_t ring_n = offY + (size_t)maxit * maxit;
+    const size_t offS = offY + (size_t)maxit * maxit;   // [beta, ||b||^2, ||x_true||^2] (polling)
+    const size_t ring_n = offS + 4;
     const bool zc = !dist_n(c);
     // single GPU: reconstructions run on the auxiliary stream, concurrently with the
     // Arnoldi steps (multi-GPU keeps one stream: the communicator's collectives must be
@@ -297,6 +303,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     if (poll) {
         uint64_t* r = reinterpret_cast<uint64_t*>(c->hring);
         for (size_t i = 0; i < (size_t)maxit * LH; ++i) r[i] = RING_SENTINEL;
+        for (size_t i = offS; i < offS + 3; ++i) r[i] = RING_SENTINEL;
     }
     T* dr = zc ? c->hring_dev : c->buf<T>("ring_dev", ring_n);
     auto publish = [&](size_t off, size_t cnt) {
@@ -311,22 +318,34 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
 
     // ||b|| (m, replicated) and ||x_true|| (n, sharded) — MATLAB recomputes them every
     // iteration (hybrid_*_rtp.m:32-33); the values are loop-invariant.
-    sumsq<T>(c, m, b, dslot<T>(c, S_NB));
-    nsumsq_diff<T>(c, n, xt, x, dslot<T>(c, S_NXT));   // ||x_true - 0||^2
-    // r0
+    double nb = 0, nxt = 0, beta = 0;
     T* q0 = Q;
+    if (poll) {
+        // no host round trip before the first step: the norms land in the ring (read at
+        // iteration 0) and r0 is divided on the device
+        sumsq<T>(c, m, b, dr + offS + 1);
+        sumsq<T>(c, n, xt, dr + offS + 2);                   // ||x_true - 0||^2
+    } else {
+        sumsq<T>(c, m, b, dslot<T>(c, S_NB));
+        nsumsq_diff<T>(c, n, xt, x, dslot<T>(c, S_NXT));   // ||x_true - 0||^2
+    }
+    // r0
     if (nspace) {
         apply_B<T>(c, B, b, q0, EPI_NONE, T(0), nullptr);   // d = B*b   (hybrid_*_rtp.m:7,9; *_bounds r0 = B*(b - A*0))
     } else {
         HGM_HIP(hipMemcpyAsync(q0, b, sizeof(T) * m, hipMemcpyDeviceToDevice, st));   // r0 = b - A*(B*0) = b
     }
-    if (nspace) nsumsq<T>(c, dim, q0, dslot<T>(c, S_BETA));
-    else sumsq<T>(c, dim, q0, dslot<T>(c, S_BETA));
-    read_scalars(c, 0, 3);
-    const double nb = std::sqrt(c->hscal[S_NB]);
-    const double nxt = std::sqrt(c->hscal[S_NXT]);
-    const double beta = std::sqrt(c->hscal[S_BETA]);      // :10  beta = norm(r0)
-    div_scalar<T>(c, dim, q0, q0, beta);                  // :13  Q(:,1) = r0 / beta
+    if (poll) {
+        normalize_to<T>(c, dim, q0, dr + offS);           // :10,:13  beta = norm(r0); Q(:,1) = r0 / beta
+    } else {
+        if (nspace) nsumsq<T>(c, dim, q0, dslot<T>(c, S_BETA));
+        else sumsq<T>(c, dim, q0, dslot<T>(c, S_BETA));
+        read_scalars(c, 0, 3);
+        nb = std::sqrt(c->hscal[S_NB]);
+        nxt = std::sqrt(c->hscal[S_NXT]);
+        beta = std::sqrt(c->hscal[S_BETA]);               // :10  beta = norm(r0)
+        div_scalar<T>(c, dim, q0, q0, (T)beta);           // :13  Q(:,1) = r0 / beta
+    }
 
     bool x_assigned = sp.x_preassigned;
     int k = 0;
@@ -487,6 +506,12 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             if (sp.proj == PROJ_ABRTP)
                 for (int i = 0; i < k + 2; ++i) idx.push_back((size_t)k * LH + (maxit + 2) + i);
             ring_wait(c, hr, idx);
+            if (k == 0) {                                // the setup norms (written before step 0)
+                ring_wait(c, hr, {offS, offS + 1, offS + 2});
+                beta = hr[offS];
+                nb = std::sqrt(hr[offS + 1]);
+                nxt = std::sqrt(hr[offS + 2]);
+            }
         } else {
             step_wait(c, k);                             // S_k: H(:,k) (+ Gram column k)
         }
