@@ -256,8 +256,6 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     const int64_t ldq = krylov_ld(dim, dist);
     hipStream_t st = c->stream;
 
-    const T* b = stage_in<T>(c, "in_b", b_in, m, dev);
-    const T* xt = stage_in_n<T>(c, "in_xt", xt_in, n, dev, po);
     T* Q = c->buf<T>("Q", (size_t)ldq * (maxit + 1));
     if (krylov_padded(ldq)) HGM_HIP(hipMemsetAsync(Q, 0, sizeof(T) * ldq * (maxit + 1), st));
     T* x = c->buf<T>("x", n > 0 ? n : 1);
@@ -310,6 +308,9 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         if (!zc)
             HGM_HIP(hipMemcpyAsync(c->hring + off, dr + off, sizeof(T) * cnt, hipMemcpyDeviceToHost, c->stream));
     };
+    // inputs staged after the ring reset (its stream sync then finds the GPU idle)
+    const T* b = stage_in<T>(c, "in_b", b_in, m, dev);
+    const T* xt = stage_in_n<T>(c, "in_xt", xt_in, n, dev, po);
     fill<T>(c, n, x, T(0));
 
     std::vector<double> H((size_t)(maxit + 1) * maxit, 0.0);
@@ -320,9 +321,14 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // iteration (hybrid_*_rtp.m:32-33); the values are loop-invariant.
     double nb = 0, nxt = 0, beta = 0;
     T* q0 = Q;
-    if (poll) {
+    if (poll && dev && rs_stream != st) {
         // no host round trip before the first step: the norms land in the ring (read at
-        // iteration 0) and r0 is divided on the device
+        // iteration 0) and r0 is divided on the device.  With device inputs the two norms
+        // run on the aux stream, beside B*b (x_true in the caller's order: same norm).
+        StreamScope scope(c, rs_stream, "aux:");
+        sumsq<T>(c, m, b, dr + offS + 1);
+        sumsq<T>(c, n, reinterpret_cast<const T*>(xt_in), dr + offS + 2);   // ||x_true - 0||^2
+    } else if (poll) {
         sumsq<T>(c, m, b, dr + offS + 1);
         sumsq<T>(c, n, xt, dr + offS + 2);                   // ||x_true - 0||^2
     } else {
@@ -574,9 +580,18 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         x_assigned = true;
         if (k + L + 1 < maxit) enqueue_step(k + L + 1);  // speculative, see above
     }
+    bool staged = false;
     if (!done) {
-        // all maxit iterations ran: the last monitors are still outstanding
-        pipe_wait(c);
+        // all maxit iterations ran: the last monitors are still outstanding.  With the
+        // reconstruction on the aux stream, x is staged out behind it there (one sync, no
+        // host wake-up in between).
+        if (rs_stream != st && x_assigned) {
+            StreamScope scope(c, rs_stream, "aux:");
+            stage_out_n<T>(c, x_out, x, n, dev, po);     // ends with a sync of the aux stream
+            staged = true;
+        } else {
+            pipe_wait(c);
+        }
         k = maxit - 1;
         const double* mk = hr + offM + 2 * (size_t)k;
         res[k] = std::sqrt(mk[0]) / nb;
@@ -586,7 +601,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     const int nit = k + 1;                               // niters = k
     if (rs_stream != st) HGM_HIP(hipStreamSynchronize(rs_stream));
     if (!x_assigned) throw Error{HGM_E_NOT_ASSIGNED, "Output argument \"x\" not assigned during call (breakdown at k = 1)"};
-    stage_out_n<T>(c, x_out, x, n, dev, po);
+    if (!staged) stage_out_n<T>(c, x_out, x, n, dev, po);
     if (c->host_stats) {
         const double tot = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
         std::fprintf(stderr, "hgm gmres: %d iters, %.1f us total, %.1f us blocked in %ld waits\n", nit, tot * 1e6,
