@@ -246,7 +246,13 @@ bool krylov_padded(int64_t ldq);
 // side (optional): a multidot enqueued with the sweep (see MdotJob).
 template <typename T>
 void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, const T* src = nullptr,
-         const MdotJob<T>* side = nullptr, PendNorm<T>* defer = nullptr, const T* pend_h = nullptr);
+         const MdotJob<T>* side = nullptr, PendNorm<T>* defer = nullptr, const T* pend_h = nullptr,
+         const T* xe = nullptr, T* qg = nullptr);
+// Gram error monitor (one-reduction form only, mgs_gram_ok): with xe = x_true the sweep of
+// step kk also writes qg[0..kk+1] = [q_kk'q_0 .. q_kk'q_{kk-1}, q_kk'q_kk, q_kk'x_true] (host
+// ring, system-scope stores), so ||Q y - x_true||^2 = xt'xt - 2 y'(Q'xt) + y'(Q'Q)y needs no
+// pass over the basis.
+bool mgs_gram_ok(int64_t ldq, int maxit, bool dist);
 // defer (single GPU, one-reduction form only): leave v = Q(:,kk+1) unnormalised and return
 // its norm partials in *defer (np > 0) for the next step's SpMV epilogues (EPI_DIVH / EPI_ADDQ);
 // np == 0 on return means the sweep normalised v itself.  pend_h (device h): Q(:,kk) still

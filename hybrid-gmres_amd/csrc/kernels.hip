@@ -273,8 +273,10 @@ template <typename T>
 void recon(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T* x, const T* xt, T* err_out,
            int64_t m, const T* AQ, int64_t ldaq, const T* b, T* res_out) {
     HGM_REQUIRE(k <= GEMV_KMAX && ldq % 2 == 0 && ldaq % 2 == 0, "recon: k too large");
-    const int nbx = gemv_blocks(n), nbr = gemv_blocks(m);
+    // x == nullptr: the residual monitor only (the error comes from the Gram error monitor)
+    const int nbx = x ? gemv_blocks(n) : 0, nbr = gemv_blocks(m);
     T* parts = c->buf<T>("recon_parts", 2 * MAX_PARTS);
+    if (!x) err_out = c->buf<T>("recon_noerr", 2);
     k_recon<T><<<nbx + nbr, BS, sizeof(T) * (k > 0 ? k : 1), c->stream>>>(n, k, Q, ldq, y, x, xt, m, AQ, ldaq, b,
                                                                           parts, nbx);
     k_finalize2<T><<<2, BS, 0, c->stream>>>(parts, nbx, nbr, err_out, res_out);
@@ -583,6 +585,9 @@ static int mgs1_mode() {   // HGM_MGS_FORM: 1 = one-reduction (default), 0 = one
     const char* e = std::getenv("HGM_MGS_FORM");
     return e ? std::atoi(e) : 1;
 }
+bool mgs_gram_ok(int64_t ldq, int maxit, bool dist) {
+    return !dist && maxit <= MGS1_MAXC && mgs1_mode() == 1 && !krylov_padded(ldq);
+}
 static int mgs1_ppl() {    // element pairs per lane of the dots pass (fewer partials to sum)
     static int v = -1;
     if (v < 0) {
@@ -636,9 +641,10 @@ __device__ __forceinline__ void mgs1_substitute(int kk, const T* sr, const T* sG
 template <typename T>
 __global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* Q, int64_t ldq, int kk,
                                                   const T* __restrict__ w, int npr, T* __restrict__ pr,
-                                                  T* __restrict__ pg, MdotStage<T> side, const T* hpend) {
+                                                  T* __restrict__ pg, MdotStage<T> side, const T* hpend,
+                                                  const T* __restrict__ xe) {
     using T2 = typename V2<T>::t;
-    __shared__ T sh[4][2 * MGS1_CG];
+    __shared__ T sh[4][2 * MGS1_CG + 1];
     const int ncg = (kk + MGS1_CG) / MGS1_CG;   // ceil((kk+1) / CG)
     const int b = (int)blockIdx.x;
     if (b >= npr * ncg) {   // extra workgroups: the side job
@@ -652,6 +658,11 @@ __global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* Q, int64_t
     const T2* w2 = reinterpret_cast<const T2*>(w);
     const T2* qk2 = reinterpret_cast<const T2*>(Q + (int64_t)kk * ldq);
     const T* qc = Q + (int64_t)c0 * ldq;
+    // Gram error monitor (xe = x_true): the group holding column kk also sums q_kk'x_true
+    // (to pg row kk+1); its ag[kk - c0] = q_kk'q_kk goes to pg row kk
+    const bool gx = xe != nullptr && g == ncg - 1;
+    const T2* xe2 = reinterpret_cast<const T2*>(xe);
+    T ax = 0;
     const T hp = hpend ? *hpend : T(0);
     auto scale = [&](T v) -> T { return hp != T(0) ? v / hp : v; };   // as k_mgs_normalize
     T ar[MGS1_CG], ag[MGS1_CG];
@@ -674,6 +685,10 @@ __global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* Q, int64_t
                 ar[c] = __builtin_fma(q[c].y, ww.y, __builtin_fma(q[c].x, ww.x, ar[c]));
                 ag[c] = __builtin_fma(q[c].y, qk.y, __builtin_fma(q[c].x, qk.x, ag[c]));
             }
+        if (gx) {
+            const T2 xx = xe2[i];
+            ax = __builtin_fma(qk.y, xx.y, __builtin_fma(qk.x, xx.x, ax));
+        }
     }
     if ((n & 1) && rb == npr - 1 && threadIdx.x == 0) {
         const int64_t i = n - 1;
@@ -686,6 +701,7 @@ __global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* Q, int64_t
                 ar[c] = __builtin_fma(qi, wi, ar[c]);
                 ag[c] = __builtin_fma(qi, qki, ag[c]);
             }
+        if (gx) ax = __builtin_fma(qki, xe[i], ax);
     }
     const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
 #pragma unroll
@@ -698,13 +714,24 @@ __global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* Q, int64_t
                 sh[wv][MGS1_CG + c] = e;
             }
         }
+    if (gx) {
+        const T a = wave_sum_dpp(ax);
+        if (lane == 0) sh[wv][2 * MGS1_CG] = a;
+    }
     __syncthreads();
     // rows of the group: 0..7 = r_{c0+row}, 8..15 = g_{c0+row-8} (g exists for columns < k)
-    auto row_ok = [&](int row) { return row < MGS1_CG ? row < nc : (row - MGS1_CG < nc && c0 + row - MGS1_CG < kk); };
+    // (with xe also g_kk = q_kk'q_kk, and row 16 = q_kk'x_true to pg row kk+1)
+    auto row_ok = [&](int row) {
+        if (row == 2 * MGS1_CG) return gx;
+        return row < MGS1_CG
+                   ? row < nc
+                   : (row - MGS1_CG < nc && (c0 + row - MGS1_CG < kk || (gx && c0 + row - MGS1_CG == kk)));
+    };
     auto row_ptr = [&](int row) -> T* {
+        if (row == 2 * MGS1_CG) return pg + (int64_t)(kk + 1) * npr;
         return row < MGS1_CG ? pr + (int64_t)(c0 + row) * npr : pg + (int64_t)(c0 + row - MGS1_CG) * npr;
     };
-    if (t < 2 * MGS1_CG && row_ok(t)) row_ptr(t)[rb] = (sh[0][t] + sh[1][t]) + (sh[2][t] + sh[3][t]);
+    if (t <= 2 * MGS1_CG && row_ok(t)) row_ptr(t)[rb] = (sh[0][t] + sh[1][t]) + (sh[2][t] + sh[3][t]);
 }
 
 // One 1024-thread workgroup.  MODE 0: sum the partial rows and solve.  MODE 1: sum only,
@@ -715,16 +742,19 @@ __global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* Q, int64_t
 constexpr int MGS1_SBS = 1024;
 template <typename T, int MODE>
 __global__ __launch_bounds__(MGS1_SBS) void k_mgs1_solve(int kk, const T* __restrict__ pr, const T* __restrict__ pg,
-                                                         int npr, T* red, T* Gt, T* hdev) {
+                                                         int npr, T* red, T* Gt, T* hdev, T* gx) {
     extern __shared__ unsigned char mgs1_smem[];
     T* sG = reinterpret_cast<T*>(mgs1_smem);
     __shared__ T sr[MGS1_MAXC];
     const int t = threadIdx.x;
     const int rowk = kk * (kk - 1) / 2;   // offset of Gram row kk
-    const int nrow = 2 * kk + 1;
+    // gx (MODE 0, Gram error monitor): rows 2k+1, 2k+2 = q_k'q_k, q_k'x_true (pg rows k, k+1)
+    const int nrow = 2 * kk + 1 + (MODE == 0 && gx ? 2 : 0);
     auto put = [&](int row, T a) {
         if (row <= kk) {
             sr[row] = a;
+        } else if (row > 2 * kk) {
+            gx[row - 2 * kk - 1] = a;
         } else {
             sG[rowk + row - kk - 1] = a;
             Gt[rowk + row - kk - 1] = a;
@@ -768,7 +798,8 @@ template <typename T>
 // last term and written back (each element by the one thread that updates it).
 __global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, T* Q, int64_t ldq, int kk,
                                                     const T* w, T* v, const T* __restrict__ hdev, T* Hcol,
-                                                    T* __restrict__ pout, MdotStage<T> side, const T* hpend) {
+                                                    T* __restrict__ pout, MdotStage<T> side, const T* hpend,
+                                                    const T* __restrict__ grow, const T* __restrict__ gx, T* qg) {
     using T2 = typename V2<T>::t;
     __shared__ T hs[MGS1_MAXC];
     __shared__ T sh[4];
@@ -781,6 +812,8 @@ __global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, T* Q, int
         hs[j] = h;
         if (blockIdx.x == 0) st_sys(Hcol + j, h);   // H(0:k, k) -> host ring
     }
+    if (qg && blockIdx.x == 0)                      // Gram error monitor row -> host ring
+        for (int j = threadIdx.x; j <= kk + 1; j += BS) st_sys(qg + j, j < kk ? grow[j] : gx[j - kk]);
     __syncthreads();
     const int64_t n2 = n >> 1, stride = (int64_t)nb * BS;
     const T2* w2 = reinterpret_cast<const T2*>(w);
@@ -845,8 +878,10 @@ __global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, T* Q, int
 
 template <typename T>
 void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, const T* src,
-         const MdotJob<T>* side, PendNorm<T>* defer, const T* pend_h) {
+         const MdotJob<T>* side, PendNorm<T>* defer, const T* pend_h, const T* xe, T* qg) {
     if (defer) defer->np = 0;
+    HGM_REQUIRE(!xe || (qg && !dist && kk + 1 <= MGS1_MAXC && mgs1_mode() == 1 && !krylov_padded(ldq)),
+                "mgs: the Gram error monitor needs the one-reduction form");
     HGM_REQUIRE(!pend_h || (!dist && kk + 1 <= MGS1_MAXC && mgs1_mode() == 1 && !krylov_padded(ldq)),
                 "mgs: pending normalisation needs the one-reduction form");
     hipEvent_t t0 = nullptr;
@@ -873,22 +908,24 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
         const int npr = gemv_blocks(n, mgs1_ppl());
         const int ncg = (kk + MGS1_CG) / MGS1_CG;
         T* pr = c->buf<T>("mgs1_pr", (size_t)MGS1_MAXC * MAX_PARTS);
-        T* pg = c->buf<T>("mgs1_pg", (size_t)MGS1_MAXC * MAX_PARTS);
+        T* pg = c->buf<T>("mgs1_pg", (size_t)(MGS1_MAXC + 2) * MAX_PARTS);
+        T* gx = xe ? c->buf<T>("mgs1_gx", 2) : nullptr;
         T* Gt = c->buf<T>("mgs1_G", (size_t)MGS1_MAXC * MGS1_MAXC / 2 + MGS1_MAXC);
         T* hdev = c->buf<T>("mgs1_h", MGS1_MAXC + 2);
         const size_t lds = sizeof(T) * ((size_t)kk * (kk + 1) / 2 + 1);
-        k_mgs1_dots<T><<<npr * ncg + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1, pend_h);
+        k_mgs1_dots<T><<<npr * ncg + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1, pend_h, xe);
         if (dist) {
             T* redd = c->buf<T>("mgs1_red", 2 * MGS1_MAXC + 2);
-            k_mgs1_solve<T, 1><<<1, MGS1_SBS, 0, st>>>(kk, pr, pg, npr, redd, Gt, hdev);
+            k_mgs1_solve<T, 1><<<1, MGS1_SBS, 0, st>>>(kk, pr, pg, npr, redd, Gt, hdev, nullptr);
             allreduce(c, redd, 2 * kk + 1);
-            k_mgs1_solve<T, 2><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, redd, Gt, hdev);
+            k_mgs1_solve<T, 2><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, redd, Gt, hdev, nullptr);
         } else {
-            k_mgs1_solve<T, 0><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, nullptr, Gt, hdev);
+            k_mgs1_solve<T, 0><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, nullptr, Gt, hdev, gx);
         }
         const int nb = gemv_blocks(n, mgs_ppl());
         T* pout = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
-        k_mgs1_update<T><<<nb + s2.blocks(), BS, 0, st>>>(n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout, s2, pend_h);
+        k_mgs1_update<T><<<nb + s2.blocks(), BS, 0, st>>>(n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout, s2, pend_h,
+                                                        Gt + (size_t)kk * (kk - 1) / 2, gx, xe ? qg : nullptr);
         if (defer && !dist && kk + 2 <= MGS1_MAXC) {   // the next step must be one-reduction too
             // the next step's SpMVs divide by H(kk+1,kk) in their epilogues
             HGM_HIP(hipGetLastError());
@@ -1179,7 +1216,7 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
                            const T*, int64_t, const T*, T*);                                   \
     template void normalize_to<T>(hgm_ctx*, int64_t, T*, T*);                                                        \
     template void mgs<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool, const T*, const MdotJob<T>*, PendNorm<T>*,   \
-                         const T*);                       \
+                         const T*, const T*, T*);                                              \
     template void cgs2<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool);                      \
     template void gemv<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, int);       \
     template void div_scalar<T>(hgm_ctx*, int64_t, const T*, T*, T);                           \

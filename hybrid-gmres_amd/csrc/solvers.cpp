@@ -193,6 +193,16 @@ static bool ring_poll_on() {
     const char* e = std::getenv("HGM_RING_POLL");
     return !e || std::atoi(e) != 0;
 }
+// Gram error monitor (HGM_GRAM_ERR=0 disables).  HGM_GRAM_ERR_MIN: the smallest
+// ||x - x_true||^2 / ||x_true||^2 it is used for (default 0.01; below, x is formed per iteration).
+static bool gram_err_on() {
+    const char* e = std::getenv("HGM_GRAM_ERR");
+    return !e || std::atoi(e) != 0;
+}
+static double gram_err_min() {
+    const char* e = std::getenv("HGM_GRAM_ERR_MIN");
+    return e ? std::atof(e) : 0.01;
+}
 // Spin until ring[i] for i in idx are all non-sentinel.  Checks the stream for errors (and
 // for going idle with an entry never written, a bug) once per ms so a fault cannot hang.
 static void ring_wait(hgm_ctx* c, const double* ring, const std::vector<size_t>& idx) {
@@ -284,8 +294,15 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     const size_t LH = 2 * (size_t)(maxit + 2);
     const size_t offM = (size_t)maxit * LH, offY = offM + 2 * (size_t)maxit;
     const size_t offS = offY + (size_t)maxit * maxit;   // [beta, ||b||^2, ||x_true||^2] (polling)
-    const size_t ring_n = offS + 4;
     const bool zc = !dist_n(c);
+    // Gram error monitor: step k's MGS sweep appends [Q(:,k)'Q(:,0:k-1),
+    // Q(:,k)'Q(:,k), Q(:,k)'x_true] to the ring (LQ doubles) and the host evaluates
+    // ||Q y_k - x_true||^2 from them, so an iteration's reconstruction reads only the kept A*Q.
+    const bool gem = aq_res && zc && ring_poll_on() && orth == HGM_MGS && mgs_gram_ok(ldq, maxit, dist) &&
+                     gram_err_on();
+    const double gem_min = gram_err_min();
+    const size_t LQ = (size_t)maxit + 2, offQG = offS + 4;
+    const size_t ring_n = offQG + (gem ? (size_t)maxit * LQ : 0);
     // single GPU: reconstructions run on the auxiliary stream, concurrently with the
     // Arnoldi steps (multi-GPU keeps one stream: the communicator's collectives must be
     // issued in one order).  For large n the concurrent GEMV over the kept columns evicts
@@ -302,6 +319,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         uint64_t* r = reinterpret_cast<uint64_t*>(c->hring);
         for (size_t i = 0; i < (size_t)maxit * LH; ++i) r[i] = RING_SENTINEL;
         for (size_t i = offS; i < offS + 3; ++i) r[i] = RING_SENTINEL;
+        for (size_t i = offQG; i < ring_n; ++i) r[i] = RING_SENTINEL;
     }
     T* dr = zc ? c->hring_dev : c->buf<T>("ring_dev", ring_n);
     auto publish = [&](size_t off, size_t cnt) {
@@ -319,7 +337,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
 
     // ||b|| (m, replicated) and ||x_true|| (n, sharded) — MATLAB recomputes them every
     // iteration (hybrid_*_rtp.m:32-33); the values are loop-invariant.
-    double nb = 0, nxt = 0, beta = 0;
+    double nb = 0, nxt = 0, beta = 0, xt2 = 0;
     T* q0 = Q;
     if (poll && dev && rs_stream != st) {
         // no host round trip before the first step: the norms land in the ring (read at
@@ -357,6 +375,8 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     int k = 0;
     std::vector<double> y, rhs, M;
     std::vector<double> G((size_t)maxit * maxit, 0.0), cvec(maxit, 0.0);
+    // Gram error monitor: Q'Q, Q'x_true and the errors it produced (-1: formed explicitly)
+    std::vector<double> GQ(gem ? (size_t)maxit * maxit : 0), cq(maxit, 0.0), gerr(maxit, -1.0);
     // Pending normalisation (single GPU, n-space, one-reduction MGS): step k
     // leaves v_{k+1} = Q(:,k+1) undivided and step k+1 applies q = v / H(k+1,k) where it reads
     // it — A: (A*v)/h, which also publishes h = H(k+1,k); B: B*(A*q) + lambda*q; the MGS dots
@@ -426,7 +446,8 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             PendNorm<T>* defer = (pn_ok && kq + 1 < maxit) ? &pend : nullptr;
             if (!defer) pend.np = 0;
             mgs<T>(c, dim, Q, ldq, kq, Hcol, dist, (!nspace && ABQ) ? ABQ + (int64_t)kq * ldaq : nullptr, side,
-                   defer, pending_in ? (const T*)pn_h : nullptr);
+                   defer, pending_in ? (const T*)pn_h : nullptr, gem ? xt : nullptr,
+                   gem ? dr + offQG + (size_t)kq * LQ : nullptr);
         }
         // Step kq-1's column is complete (H(kq,kq-1) came from this step's A product).  The
         // event goes at the end of the step: a marker between two kernels costs a bubble.
@@ -444,7 +465,8 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // stream, then the event the host waits on.  Everything it reads (Q(:,0..kq), y_kq)
     // is complete when it is enqueued (the host has seen step kq finish), so it needs no
     // stream dependency; it writes only x, its own scratch and ring slot kq.
-    auto enqueue_recon = [&](int kq) {
+    int x_pending = -1;   // the last reconstruction, when it left x unformed (Gram error monitor)
+    auto enqueue_recon = [&](int kq, bool want_x) {
         StreamScope scope(c, rs_stream, "aux:");
         const int kk = kq + 1;
         const T* yk = c->hring_dev + offY + (size_t)kq * maxit;
@@ -454,7 +476,9 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         if (aq_res) {
             // x = Q(:,1:k)*yk with ||x - x_true||^2 (:33/:36) and ||b - A*x||^2 (:32/:35)
             // evaluated as ||b - (A*Q(:,1:k))*yk||^2, all in one launch (+ finalize)
-            recon<T>(c, n, kk, Q, ldq, yk, x, xt, eslot, m, AQ, ldaq, b, rslot);
+            // (want_x false: the Gram error monitor has the error, x is formed at the end)
+            recon<T>(c, n, kk, Q, ldq, yk, want_x ? x : nullptr, xt, eslot, m, AQ, ldaq, b, rslot);
+            x_pending = want_x ? -1 : kq;
             if (dist_n(c)) allreduce(c, eslot, 1);
             publish(offM + 2 * (size_t)kq, 2);
             pipe_record(c);
@@ -511,12 +535,15 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             for (int i = 0; i < k + 2; ++i) idx.push_back((size_t)k * LH + i);
             if (sp.proj == PROJ_ABRTP)
                 for (int i = 0; i < k + 2; ++i) idx.push_back((size_t)k * LH + (maxit + 2) + i);
+            if (gem)
+                for (int i = 0; i < k + 2; ++i) idx.push_back(offQG + (size_t)k * LQ + i);
             ring_wait(c, hr, idx);
             if (k == 0) {                                // the setup norms (written before step 0)
                 ring_wait(c, hr, {offS, offS + 1, offS + 2});
                 beta = hr[offS];
                 nb = std::sqrt(hr[offS + 1]);
                 nxt = std::sqrt(hr[offS + 2]);
+                xt2 = hr[offS + 2];
             }
         } else {
             step_wait(c, k);                             // S_k: H(:,k) (+ Gram column k)
@@ -524,7 +551,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         if (k >= 1) {
             const double* mk = hr + offM + 2 * (size_t)(k - 1);
             res[k - 1] = std::sqrt(mk[0]) / nb;
-            err[k - 1] = std::sqrt(mk[1]) / nxt;
+            err[k - 1] = gerr[k - 1] >= 0 ? gerr[k - 1] : std::sqrt(mk[1]) / nxt;
             if (res[k - 1] <= tol) {                     // :35 / :38 / *_bounds :79-83
                 k = k - 1;
                 done = true;
@@ -536,6 +563,12 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         if (sp.proj == PROJ_ABRTP) {
             for (int i = 0; i <= k; ++i) G[(size_t)k * maxit + i] = hk[(maxit + 2) + i];
             cvec[k] = hk[(maxit + 2) + k + 1];
+        }
+        if (gem) {
+            const double* gk = hr + offQG + (size_t)k * LQ;
+            for (int i = 0; i < k; ++i) GQ[(size_t)k * maxit + i] = GQ[(size_t)i * maxit + k] = gk[i];
+            GQ[(size_t)k * maxit + k] = gk[k];
+            cq[k] = gk[k + 1];
         }
         if (Hh(k + 1, k) == 0) {                         // :25  if H(k+1,k) == 0, break
             done = true;
@@ -576,9 +609,32 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             dense::mldivide_square(kk, M.data(), cvec.data(), y.data());
         }
         std::memcpy(c->hring + offY + (size_t)k * maxit, y.data(), sizeof(double) * kk);
-        enqueue_recon(k);
+        bool want_x = true;
+        if (gem) {
+            // ||Q y - x_true||^2 = x_true'x_true - 2 y'(Q'x_true) + y'(Q'Q) y (hybrid_*_rtp.m:33/:36
+            // with x = Q y), used when it is at least gem_min ||x_true||^2 (the cancellation then
+            // costs at most a factor 1/gem_min of the terms' rounding)
+            long double e2 = xt2;
+            for (int i = 0; i < kk; ++i) {
+                long double gy = 0;
+                for (int j = 0; j < kk; ++j) gy += (long double)GQ[(size_t)i * maxit + j] * y[j];
+                e2 += (long double)y[i] * (gy - 2.0L * cq[i]);
+            }
+            if (xt2 > 0 && e2 >= (long double)gem_min * xt2) {
+                gerr[k] = std::sqrt((double)e2) / nxt;
+                want_x = false;
+            }
+        }
+        enqueue_recon(k, want_x);
         x_assigned = true;
         if (k + L + 1 < maxit) enqueue_step(k + L + 1);  // speculative, see above
+    }
+    if (x_pending >= 0) {
+        // the last reconstruction left x unformed (Gram error monitor): x = Q(:,0:k) y_k
+        // behind it, on the same stream
+        StreamScope scope(c, rs_stream, "aux:");
+        gemv<T>(c, n, x_pending + 1, Q, ldq, c->hring_dev + offY + (size_t)x_pending * maxit, x, 0);
+        x_pending = -1;
     }
     bool staged = false;
     if (!done) {
@@ -595,7 +651,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         k = maxit - 1;
         const double* mk = hr + offM + 2 * (size_t)k;
         res[k] = std::sqrt(mk[0]) / nb;
-        err[k] = std::sqrt(mk[1]) / nxt;
+        err[k] = gerr[k] >= 0 ? gerr[k] : std::sqrt(mk[1]) / nxt;
     }
     if (k == maxit) k = maxit - 1;
     const int nit = k + 1;                               // niters = k

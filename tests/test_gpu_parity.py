@@ -487,6 +487,63 @@ def test_mgs_one_reduction_form(tmp_path, N, na, maxit):
         assert np.array_equal(res[form]["hba_H"], res[form]["hba_H2"])
 
 
+_GEM_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + "/hybrid-gmres_amd")
+import hgmres
+from hgmres.problems import tomo_problem
+P = tomo_problem(int(sys.argv[3]), int(sys.argv[4]), noise=1e-2, seed=0)
+maxit = int(sys.argv[5])
+tols = {"hab": float(sys.argv[6]), "hba": float(sys.argv[7])}
+ctx = hgmres.Context(0)
+out = {}
+for tag, fn in (("hab", hgmres.hybrid_ab_gmres_rtp), ("hba", hgmres.hybrid_ba_gmres_rtp)):
+    x, e, r, k, H = fn(P.A, P.B, P.b, P.x_true, tols[tag], maxit, 1e-2, ctx=ctx, return_H=True)
+    out[tag + "_x"], out[tag + "_e"], out[tag + "_r"], out[tag + "_H"] = x, e, r, H
+np.savez(sys.argv[2], **out)
+"""
+
+
+@pytest.mark.parametrize("N,na,maxit,stop", [(64, 90, 20, False), (64, 91, 80, False), (64, 90, 20, True)])
+def test_gram_error_monitor(tmp_path, N, na, maxit, stop):
+    """Gram error monitor: the error history as x_true'x_true - 2y'(Q'x_true)
+    + y'(Q'Q)y, with Q'Q and Q'x_true from the one-reduction MGS sweep, and x formed once
+    after the loop.  Variants: off (HGM_GRAM_ERR=0), on (default threshold) and mixed
+    (threshold at the median error: later iterations form x explicitly).  x, H and the
+    residual history are bitwise the explicit path's (same kernels); the error history agrees
+    with it to 1e-12 and with the oracle to 1e-10.  `stop` ends both solves by `tol` at k = 5
+    (hybrid_*_rtp.m:35), so x is that of an iteration before the last Arnoldi step."""
+    P = tomo_problem(N, na, noise=1e-2, seed=0)
+    fns = {"hab": R.hybrid_ab_gmres_rtp, "hba": R.hybrid_ba_gmres_rtp}
+    tols = {t: 0.0 for t in fns}
+    if stop:
+        tols = {t: float(f(P.A, P.B, P.b, P.x_true, 0.0, maxit, 1e-2)[2][4]) * (1 + 1e-9) for t, f in fns.items()}
+    refs = {t: f(P.A, P.B, P.b, P.x_true, tols[t], maxit, 1e-2, return_H=True) for t, f in fns.items()}
+    thr = float(np.median(refs["hab"][1])) ** 2
+    variants = {"off": {"HGM_GRAM_ERR": "0"}, "on": {"HGM_GRAM_ERR": "1"},
+                "mix": {"HGM_GRAM_ERR": "1", "HGM_GRAM_ERR_MIN": repr(thr)}}
+    res = {}
+    for v, extra in variants.items():
+        f = str(tmp_path / f"gem_{v}.npz")
+        env = dict(os.environ, HGM_MGS_SINGLE="0", **extra)
+        subprocess.run([sys.executable, "-c", _GEM_CHILD, ROOT, f, str(N), str(na), str(maxit),
+                        repr(tols["hab"]), repr(tols["hba"])], env=env, check=True, timeout=600)
+        res[v] = np.load(f)
+    off = res["off"]
+    for tag, ref in refs.items():
+        if stop:
+            assert ref[3] == 5 and off[tag + "_r"].shape == (5,)
+        hist_ok(off[tag + "_e"], ref[1], TOL)
+        for v in ("on", "mix"):
+            g = res[v]
+            assert np.array_equal(g[tag + "_H"], off[tag + "_H"]), (tag, v)
+            assert np.array_equal(g[tag + "_x"], off[tag + "_x"]), (tag, v)
+            assert np.array_equal(g[tag + "_r"], off[tag + "_r"]), (tag, v)
+            hist_ok(g[tag + "_e"], off[tag + "_e"], 1e-12)
+            hist_ok(g[tag + "_e"], ref[1], TOL)
+            assert rel(g[tag + "_x"], ref[0]) < TOL
+
+
 def test_cgs2_matches_mgs(gpu_ctx, P64):
     o1 = hgmres.hybrid_ba_gmres_rtp(P64.A, P64.B, P64.b, P64.x_true, 0.0, 20, 1e-2, ctx=gpu_ctx, return_H=True)
     o2 = hgmres.hybrid_ba_gmres_rtp(P64.A, P64.B, P64.b, P64.x_true, 0.0, 20, 1e-2, ctx=gpu_ctx, return_H=True,
@@ -602,12 +659,15 @@ def test_c2_hybrid_ab_gmres_rtp_properties(gpu_ctx):
     assert np.max(np.abs(np.triu(H, 2))) < 1e-9 * np.max(np.abs(H))
     # residual from the returned x agrees with the reported history (size-independent check)
     assert abs(np.linalg.norm(P.b - P.A @ x) / np.linalg.norm(P.b) - r[-1]) < 1e-12
+    # the error history (Gram error monitor at this size) against the returned x
+    assert abs(np.linalg.norm(x - P.x_true) / np.linalg.norm(P.x_true) - e[-1]) < 1e-11
     # short oracle comparison at full size
     xr, er, rr, kr, Hr = R.hybrid_ab_gmres_rtp(P.A, P.B, P.b, P.x_true, 0.0, 6, 1e-2, return_H=True)
     x6, e6, r6, k6, H6 = hgmres.hybrid_ab_gmres_rtp(Ao, Bo, P.b, P.x_true, 0.0, 6, 1e-2, ctx=gpu_ctx, return_H=True)
     H_ok(H6, Hr)
     assert rel(x6, xr) < TOL
     hist_ok(r6, rr, TOL)
+    hist_ok(e6, er, TOL)
 
 
 # ---------------------------------------------------------------------------------------
