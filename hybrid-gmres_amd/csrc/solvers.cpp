@@ -1091,6 +1091,9 @@ int arnoldi(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b_in, 
     div_scalar<T>(c, dim, Q, Q, beta);                                         // :15
     std::vector<double> H((size_t)(kg + 1) * kg, 0.0);
     int done = 0;
+    // The steps are enqueued back to back, with no host round trip per step: the breakdown
+    // test H(k+1,k) < btol runs on the host afterwards, and the steps past a breakdown (which
+    // wrote only Q(:,>k+1) and H(:,>k) on the device) are discarded.
     for (int k = 0; k < kg; ++k) {
         T* qk = Q + (int64_t)k * ldq;
         T* v = Q + (int64_t)(k + 1) * ldq;
@@ -1104,9 +1107,13 @@ int arnoldi(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b_in, 
         T* Hcol = Hd + (int64_t)k * (kg + 1);
         if (orth == HGM_CGS2) cgs2<T>(c, dim, Q, ldq, k, Hcol, dist);
         else mgs<T>(c, dim, Q, ldq, k, Hcol, dist);                            // :25-31
-        Reader rd(c);
-        rd.add(&H[(size_t)k * (kg + 1)], Hcol, sizeof(T) * (k + 2));
-        rd.go();
+    }
+    std::vector<double> Hall((size_t)(kg + 1) * kg);
+    Reader rd(c);
+    rd.add(Hall.data(), Hd, sizeof(T) * Hall.size());
+    rd.go();
+    for (int k = 0; k < kg; ++k) {
+        std::memcpy(&H[(size_t)k * (kg + 1)], &Hall[(size_t)k * (kg + 1)], sizeof(double) * (k + 2));
         done = k + 1;
         if (H[(size_t)k * (kg + 1) + k + 1] < btol) {                          // :30  H(k+1,k) < 1e-12 -> break
             // the reference breaks before Q(:,k+1) = v/H(k+1,k); H(k+1,k) keeps its value

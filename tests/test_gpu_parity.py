@@ -635,6 +635,19 @@ def test_gcv(gpu_ctx, name):
         hist_ok(vals, g[f"gcv_{typ}_vals"], 1e-9)
 
 
+def test_gcv_arnoldi_breakdown(gpu_ctx):
+    """gcv_function.m:30 breaks at H(k+1,k) < 1e-12 (the steps are enqueued without a host
+    round trip; the ones past the break are discarded): H keeps zero columns after it."""
+    A = sp.csr_matrix(np.diag([1.0, 2.0, 3.0, 4.0, 5.0, 6.0]))
+    b = np.array([1.0, 1.0, 0.0, 0.0, 0.0, 0.0])
+    for typ in ("ab", "ba"):
+        H, beta, kd = hgmres.arnoldi(A, A.T, b, 5, typ, ctx=gpu_ctx)
+        Hr, br = R.arnoldi(A, A.T.tocsr(), b, 5, typ)
+        assert kd == 2, (typ, kd)
+        H_ok(H, Hr)
+        assert np.all(H[:, kd:] == 0) and abs(beta - br) <= TOL * br
+
+
 def test_gcv_fminbnd_matches_scipy(gpu_ctx):
     import scipy.optimize as so
     A, B, b, xt, g = golden_problem("tomo24_pixel.npz")
