@@ -719,6 +719,9 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     div_scalar<T>(c, n, v, v, (T)alpha);                                       // :12
     HGM_HIP(hipMemcpyAsync(w, v, sizeof(T) * n, hipMemcpyDeviceToDevice, c->stream));   // :14 w = v
     double phi_bar = beta, rho_bar = alpha;                                    // :15-16
+    // non-hybrid: the stop test uses phi_bar (host), so the error history (:43) stays on the
+    // device and is read once after the loop instead of once per iteration
+    T* errh = hybrid ? nullptr : c->buf<T>("lsqr_errh", maxit);
     int k = 0;
     for (k = 0; k < maxit; ++k) {
         // :22-24  u_hat = A*v - alpha*u ; beta = norm(u_hat) ; u = u_hat / beta
@@ -761,7 +764,7 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         const double phi = cs * phi_bar;
         phi_bar = sn * phi_bar;
         lsqr_update<T>(c, n, x, w, v, (T)(phi / rho), (T)(theta / rho));     // :40-41
-        nsumsq_diff<T>(c, n, x, xt, sl + S_ERR);
+        nsumsq_diff<T>(c, n, x, xt, hybrid ? sl + S_ERR : errh + k);
         if (hybrid) {
             apply_A<T>(c, A, x, t, EPI_RSUB, T(0), b);                        // hybrid :43  b - A*x
             sumsq<T>(c, m, t, sl + S_RES);
@@ -773,14 +776,18 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
             res[k] = std::sqrt((double)hs[1]) / nb;
             if (res[k] < tol) break;                                           // hybrid :45 (<)
         } else {
-            err[k] = std::sqrt((double)read1<T>(c, sl + S_ERR)) / nxt;         // :43
-            res[k] = std::fabs(phi_bar) / nb;                                  // :44
+            res[k] = std::fabs(phi_bar) / nb;                                  // :44 (:43 below)
             if (res[k] <= tol) break;                                          // :46 (<=)
         }
     }
     if (k == maxit) k = maxit - 1;
     const int nit = k + 1;
     if (!hybrid) {
+        std::vector<T> eh(nit);
+        Reader re(c);
+        re.add(eh.data(), errh, sizeof(T) * nit);
+        re.go();
+        for (int i = 0; i < nit; ++i) err[i] = std::sqrt((double)eh[i]) / nxt;   // :43
         apply_A<T>(c, A, x, t, EPI_RSUB, T(0), b);                            // :52 exact final residual
         sumsq<T>(c, m, t, sl + S_RES);
         res[nit - 1] = std::sqrt((double)read1<T>(c, sl + S_RES)) / nb;
@@ -879,6 +886,17 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     double zetabar = alpha * beta, alphabar = alpha, rho = 1, rhobar = 1, cbar = 1, sbar = 0;   // :19-23
     HGM_HIP(hipMemcpyAsync(h, v, sizeof(T) * n, hipMemcpyDeviceToDevice, c->stream));   // :25
     double prev_ch = 0.0;                                                      // (theta/rho) of the previous :67
+    // tol <= 0: `res < tol` (:76) can never hold, so the monitors stay on the device and are
+    // read once after the loop instead of once per iteration
+    const bool defer_mon = kept && !(tol > 0);
+    double* dmonh = defer_mon ? c->buf<double>("lsmr_monh", 2 * (size_t)maxit) : nullptr;
+    T* errh = defer_mon ? c->buf<T>("lsmr_errh", maxit) : nullptr;
+    auto monitors = [&](int kk, double m0, double m1, double e2) {
+        const double nr = std::sqrt(m0);
+        res[kk] = nr / (nb + EPSD);                                            // :70
+        ar[kk] = std::sqrt(m1) / (normA * std::max(nr, EPSD));                 // :71
+        if (xt) err[kk] = std::sqrt(e2) / nxt;                                 // :72-73
+    };
     int k = 0;
     for (k = 0; k < maxit; ++k) {
         const double alpha_k = alpha;
@@ -921,12 +939,13 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         Reader rr(c);
         if (kept) {
             // :69 ||b - A*x||^2 and :71 ||A'b - A'A*x||^2 from the kept images
-            lsmr_monitor<T>(c, m, Av, nullptr, 1.0, 0.0, Ihm, Ihbm, Ixm, b, prev_ch, c_hbar, c_x, k == 0, dmon);
+            double* dm = defer_mon ? dmonh + 2 * (size_t)k : dmon;
+            lsmr_monitor<T>(c, m, Av, nullptr, 1.0, 0.0, Ihm, Ihbm, Ixm, b, prev_ch, c_hbar, c_x, k == 0, dm);
             lsmr_monitor<T>(c, n, Atu1, Atu0, beta, alpha_k, Ihn, Ihbn, Ixn, Atb, prev_ch, c_hbar, c_x, k == 0,
-                            dmon + 1);
-            if (dist_n(c)) allreduce(c, dmon + 1, 1);
+                            dm + 1);
+            if (dist_n(c)) allreduce(c, dm + 1, 1);
             std::swap(Atu0, Atu1);
-            rr.add(mon, dmon, sizeof(double) * 2);
+            if (!defer_mon) rr.add(mon, dmon, sizeof(double) * 2);
         } else {
             apply_A<T>(c, A, x, r, EPI_RSUB, T(0), b);                         // :69 r = b - A*x
             sumsq<T>(c, m, r, sl + S_RES);
@@ -936,21 +955,28 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
             rr.add(&hs[1], sl + S_AR, sizeof(T));
         }
         prev_ch = c_h;
-        if (xt) nsumsq_diff<T>(c, n, x, xt, sl + S_ERR);
+        if (xt) nsumsq_diff<T>(c, n, x, xt, defer_mon ? errh + k : sl + S_ERR);
+        if (defer_mon) continue;
         if (xt) rr.add(&hs[2], sl + S_ERR, sizeof(T));
         rr.go();
         if (!kept) {
             mon[0] = (double)hs[0];
             mon[1] = (double)hs[1];
         }
-        const double nr = std::sqrt(mon[0]);
-        res[k] = nr / (nb + EPSD);                                             // :70
-        ar[k] = std::sqrt(mon[1]) / (normA * std::max(nr, EPSD));              // :71
-        if (xt) err[k] = std::sqrt((double)hs[2]) / nxt;                       // :72-73
+        monitors(k, mon[0], mon[1], xt ? (double)hs[2] : 0.0);
         if (res[k] < tol) break;                                               // :76 (<)
     }
     if (k == maxit) k = maxit - 1;
     const int nit = k + 1;
+    if (defer_mon) {
+        std::vector<double> mh(2 * (size_t)nit);
+        std::vector<T> eh(nit, T(0));
+        Reader re(c);
+        re.add(mh.data(), dmonh, sizeof(double) * mh.size());
+        if (xt) re.add(eh.data(), errh, sizeof(T) * nit);
+        re.go();
+        for (int i = 0; i < nit; ++i) monitors(i, mh[2 * i], mh[2 * i + 1], (double)eh[i]);
+    }
     stage_out_n<T>(c, x_out, x, n, dev, po);
     if (err_out) std::memcpy(err_out, err.data(), sizeof(double) * nit);
     if (res_out) std::memcpy(res_out, res.data(), sizeof(double) * nit);

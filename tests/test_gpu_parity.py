@@ -602,6 +602,16 @@ def test_lsmr_monitor_forms_agree(gpu_ctx, P64, dtype):
     hist_ok(o1[3], o2[3], 1e-8 if dtype == 0 else 1e-3)
 
 
+def test_lsmr_deferred_monitors(gpu_ctx, P64):
+    """tol <= 0: `res < tol` (lsmr_solver.m:76) cannot fire, so the monitors are read once
+    after the loop; tol > 0 reads them every iteration for the stop test.  Same bits."""
+    o1 = hgmres.lsmr_solver(P64.A, P64.b, P64.x_true, 0.0, 15, ctx=gpu_ctx)
+    o2 = hgmres.lsmr_solver(P64.A, P64.b, P64.x_true, 1e-300, 15, ctx=gpu_ctx)
+    assert o1[-1] == o2[-1] == 15
+    for a, b in zip(o1[:-1], o2[:-1]):
+        assert np.array_equal(a, b)
+
+
 def test_lsqr_fp32(gpu_ctx, P64):
     """BASELINE configs[4]: LSQR / LSMR in fp32 sharing the SpMV kernels.  fp32 GKB
     departs from fp64 by ~1e-5 at k = 4 and by ~5e-2 at k = 8 on this operator
