@@ -1,24 +1,27 @@
 #!/usr/bin/env python3
 """Benchmark: GMRES iterations/s + SpMV GB/s (% HBM roofline) on a synthetic 2-D phantom.
 
-Workload (BASELINE.json configs[1], the metric's single-GPU configuration):
-  hybrid_ab_gmres_rtp, fp64, 512x512 Shepp-Logan phantom, parallel-beam Siddon A
-  (30 angles, 725 detectors: m = 21,750 rays, n = 262,144 pixels, nnz = 1.0e7),
-  matched back-projector B = A', lambda = 1e-2, maxit = 20, tol = 0 (all 20
-  iterations run).  One "step" = one complete 20-iteration solve.  Inputs (A, B,
-  b, x_true) are resident in HBM before the timed region.
+Default workload = BASELINE.json configs[3], the configuration the metric's
+"1/2/4/8 GPU" and north_star's ">= 60 % ... at nnz ~ 1e9" are quoted on, which fits
+one MI355X:  AB-GMRES (ABgmres_nonhybrid_bounds.m, m-space Arnoldi on A*B), fp64,
+4096x4096 Shepp-Logan phantom, parallel-beam Siddon A (47 angles, 5793 detectors:
+m = 272,271 rays, n = 16,777,216 pixels, nnz(A) = 1.0e9), matched B = A', maxit = 20,
+tol = 0 (all 20 iterations run).  One "step" = one complete 20-iteration solve.
+Inputs (A, B, b, x_true) are resident in HBM before the timed region.
+`--workload c2|c3|c3gcv|c5|c5m` runs the other BASELINE configs as side lines.
 
-Multi-GPU (torchrun, one process per GPU): weak scaling over independent
-slices — rank r reconstructs its own slice (same geometry, noise seed r); there
-is no data-path collective (the 512^2 operator is below the size where pixel
-sharding amortises its all-reduce, north_star; the RCCL-sharded operator path
-is `--workload c4 --shard`).  value = total GMRES iterations of all ranks / max
-rank time.
+Multi-GPU (torchrun, one process per GPU): by default ONE global solve of the same
+operator, pixel-sharded by nnz across the ranks: rank g holds
+A(:,P_g) and B(P_g,:), and the only data-path collective is an RCCL all-reduce of
+the m-vector partial A_g*(B_g*q) per Arnoldi step (strong scaling; value = GMRES
+iterations of the global solve / max rank time).  `--replicas` instead runs one
+independent solve per GPU (weak scaling, no collective).
 
 Extra fields: "roofline" for the dominant SpMV kernel (algorithmic bytes per
 launch / average launch duration from HIP events recorded on the library's
 stream during the timed region), "kernels" (both SpMV classes and MGS),
-"cpu_baseline" (the oracle restatement timed on host cores, rank 0, N=1).
+"cpu_baseline" (the oracle restatement timed on the host cores, rank 0, N=1: all cores
+through oracle/spmv_omp.c, plus a one-core scipy leg; nproc and CPU model stated).
 """
 import argparse
 import json
@@ -41,10 +44,13 @@ WORKLOADS = {
     # cached H: analyze_regularization.m:39-46) + the BA-GMRES solve at the chosen lambda
     "c3gcv": dict(N=2048, angles=19, solver="hybrid_ba_gmres_rtp", maxit=20, lam=1e-2, cpu_iters=3,
                   gcv=dict(k=20, lo=1e-8, hi=1.0, tolx=1e-10)),
-    "c4": dict(N=4096, angles=47, solver="ABgmres_nonhybrid_bounds", maxit=20, lam=0.0, cpu_iters=1),
+    "c4": dict(N=4096, angles=47, solver="ABgmres_nonhybrid_bounds", maxit=20, lam=0.0, cpu_iters=2,
+               cpu_iters_single=1),
     # BASELINE configs[4]: the Golub-Kahan path on the 4096^2 operator in fp32
-    "c5": dict(N=4096, angles=47, solver="lsqr_solver", maxit=20, lam=0.0, f32=True, cpu_iters=1),
-    "c5m": dict(N=4096, angles=47, solver="lsmr_solver", maxit=20, lam=0.0, f32=True, cpu_iters=1),
+    "c5": dict(N=4096, angles=47, solver="lsqr_solver", maxit=20, lam=0.0, f32=True, cpu_iters=2,
+               cpu_iters_single=1),
+    "c5m": dict(N=4096, angles=47, solver="lsmr_solver", maxit=20, lam=0.0, f32=True, cpu_iters=2,
+                cpu_iters_single=1),
 }
 UNITS = {"lsqr_solver": "LSQR iters/s", "lsmr_solver": "LSMR iters/s"}
 
@@ -54,7 +60,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     ap.add_argument("--orth", default="mgs", choices=["mgs", "cgs2"])
     ap.add_argument("--tune-a", default="", help="experiment: SpMV variant:group for A (default: auto)")
     ap.add_argument("--tune-b", default="", help="experiment: SpMV variant:group for B (default: auto)")
@@ -62,17 +68,19 @@ def parse():
                     help="monitor norm(b - A*x) with an explicit SpMV (default: b - (A*Q) y)")
     ap.add_argument("--unmatched", action="store_true",
                     help="GMRES workloads: B = the unmatched pixel-driven back-projector instead of A'")
-    ap.add_argument("--shard", action="store_true",
-                    help="N>1: one pixel-sharded solve over RCCL (strong scaling) instead of N replicas")
+    ap.add_argument("--replicas", action="store_true",
+                    help="N>1: one independent solve per GPU (weak scaling) instead of one pixel-sharded solve")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
-                    help="--shard transport: RCCL, or the host all-reduce hook (single-device emulation)")
+                    help="sharded-solve transport: RCCL, or the host all-reduce hook (single-device emulation)")
     ap.add_argument("--same-device", action="store_true", help="run every rank on GPU 0 (shard emulation)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP-event timing")
     # default A: the roofline kernel; timing both classes costs ~11% of the C2 step, A alone ~4%
     ap.add_argument("--time-classes", default="A", choices=["A", "B", "AB", "MGS", "ALL"],
                     help="kernel classes timed with HIP events in the timed region (roofline: A)")
-    ap.add_argument("--cpu-iters", type=int, default=0, help="oracle iterations for cpu_baseline (0 = maxit)")
+    ap.add_argument("--cpu-iters", type=int, default=0, help="oracle iterations of the all-core cpu_baseline leg "
+                                                             "(0 = the workload's default)")
+    ap.add_argument("--no-cpu-single", action="store_true", help="skip the one-core cpu_baseline leg")
     ap.add_argument("--time-every", type=int, default=4,
                     help="HIP-event timing on every Nth timed step (all its launches of the timed classes); "
                          "events ride in the dispatch packets and cost ~3%% of a C2 step when on every step")
@@ -145,7 +153,7 @@ def main():
     from hgmres.core import _check
 
     wl = WORKLOADS[args.workload]
-    shard = args.shard and world > 1
+    shard = world > 1 and not args.replicas
     if shard:
         # one global problem, pixel-sharded: RCCL context (or the host
         # all-reduce hook for the single-device emulation)
@@ -195,7 +203,8 @@ def main():
         if gcv:
             _check(lib.hgm_arnoldi(ctx.handle, A._h, B._h, b.ctypes.data_as(L.dp), kg, L.HGM_SIDE_BA, 1e-12, o_orth,
                                    Hg.ctypes.data_as(L.dp), C.byref(beta_g), C.byref(kdone)), ctx)
-            rc = lib.hgm_gcv_fminbnd(Hg.ctypes.data_as(L.dp), kdone.value, beta_g.value, float(n), gcv["lo"],
+            # k = size(H,2) = k_gcv (gcv_function.m:33): the columns past a breakdown are zero
+            rc = lib.hgm_gcv_fminbnd(Hg.ctypes.data_as(L.dp), kg, beta_g.value, float(n), gcv["lo"],
                                      gcv["hi"], gcv["tolx"], C.byref(lam_c), C.byref(g_c))
             if rc != 0:
                 raise RuntimeError(f"hgm_gcv_fminbnd failed ({rc})")
@@ -278,7 +287,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(A, B, b, x_true, wl, args.cpu_iters or wl["cpu_iters"])
+        cpu = cpu_baseline(A, B, b, x_true, wl, args.cpu_iters or wl["cpu_iters"],
+                           0 if args.no_cpu_single else wl.get("cpu_iters_single", wl["cpu_iters"]))
 
     if rank == 0:
         line = {
@@ -322,32 +332,71 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(A, B, b, x_true, wl, iters):
-    """The oracle restatement (reference algorithm, scipy SpMV) on one host core."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _host_cores():
+    """CPUs this process may run on (the box's share, not the machine's count)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:   # pragma: no cover
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(A, B, b, x_true, wl, iters, iters_single):
+    """The oracle restatement (the reference algorithm) on the same operator, timed on the
+    host: all cores (oracle/spmv_omp.c row-block SpMV, BLAS unrestricted; the products are
+    bitwise those of the one-core scipy leg) and, if iters_single > 0, one core (scipy CSR
+    SpMV, BLAS limited to one thread).  A timed solve includes the reference's setup
+    (r0, norms), so iters/s understates the CPU's steady rate by that share (stated)."""
+    from oracle import parallel as OP
     from oracle import restatement as R
     try:
         from threadpoolctl import threadpool_limits
     except ImportError:   # pragma: no cover
         threadpool_limits = None
-    maxit = iters or wl["maxit"]
+    import contextlib
     fn = getattr(R, wl["solver"])
     gkb = wl["solver"] in UNITS
-    As = A.to_scipy()
-    if gkb:   # the restatement forms A' itself (lsqr_solver.m:10); fp64 arithmetic, fp32-rounded values
-        args = (As, b, x_true, 0.0, maxit)
-    else:
-        args = (As, B.to_scipy(), b, x_true, 0.0, maxit) + \
-            ((wl["lam"],) if wl["solver"] != "ABgmres_nonhybrid_bounds" else ())
-    import contextlib
-    with (threadpool_limits(limits=1) if threadpool_limits else contextlib.nullcontext()):
+    unit = UNITS.get(wl["solver"], "GMRES iters/s")
+    As, Bs = A.to_scipy(), B.to_scipy()     # fp64 arithmetic on the fp32-rounded values for C5
+
+    def run(Aop, Bop, k):
+        if gkb:   # the restatement applies A' itself (lsqr_solver.m:10); here B = A' (device transpose)
+            args = (Aop, b, x_true, 0.0, k)
+        else:
+            args = (Aop, Bop, b, x_true, 0.0, k) + ((wl["lam"],) if wl["solver"] != "ABgmres_nonhybrid_bounds" else ())
         t0 = time.perf_counter()
         out = fn(*args)
         dt = time.perf_counter() - t0
-    k = out[-1] if wl["solver"] == "lsmr_solver" else out[3]
-    return {"value": round(k / dt, 4), "unit": UNITS.get(wl["solver"], "GMRES iters/s"), "cores": 1,
-            "kind": "port",
-            "sample": f"oracle/restatement.py {wl['solver']} on the same {wl['N']}^2 operator, {k} iterations "
-                      f"({dt:.1f} s, scipy CSR SpMV + numpy, 1 thread)"}
+        kk = out[-1] if wl["solver"] == "lsmr_solver" else out[3]
+        return kk, dt
+
+    OP.build()
+    threads = OP.num_threads()
+    PB = OP.ParallelCSR(Bs)
+    PA = OP.ParallelCSR(As, T=PB if gkb else None)
+    k_all, dt_all = run(PA, PB, iters)
+    res = {"value": round(k_all / dt_all, 4), "unit": unit, "cores": threads, "kind": "port",
+           "nproc": _host_cores(), "cpu_model": _cpu_model(),
+           "sample": f"oracle/restatement.py {wl['solver']} on the same {wl['N']}^2 operator, one complete "
+                     f"{k_all}-iteration solve incl. its setup ({dt_all:.1f} s), CSR SpMV on {threads} OpenMP "
+                     f"threads (oracle/spmv_omp.c, bitwise = scipy), numpy BLAS unrestricted"}
+    if iters_single > 0:
+        with (threadpool_limits(limits=1) if threadpool_limits else contextlib.nullcontext()):
+            k1, dt1 = run(As, Bs, iters_single)
+        res["single_core"] = {"value": round(k1 / dt1, 4), "unit": unit, "cores": 1,
+                              "sample": f"same solver, {k1}-iteration solve incl. setup ({dt1:.1f} s), "
+                                        f"scipy CSR SpMV + numpy on 1 thread"}
+    return res
 
 
 if __name__ == "__main__":

@@ -2,11 +2,15 @@
 // operator management and the solver entry points that replace the reference's
 // MATLAB functions.  Every entry point converts C++ exceptions into a status code
 // and keeps the message for hgm_last_error().
+#include <limits.h>
+#include <link.h>
+
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <set>
 #include <vector>
 
 #include "internal.h"
@@ -184,16 +188,12 @@ void pinned_ring(hgm_ctx* c, size_t bytes) {
 // Events the host waits on before reading the pinned ring.  Every scalar the kernels put
 // in the ring is a system-scope store (st_sys, device_common.h), so the event needs no
 // system-scope release of its own (an L2 writeback + invalidate per record, ~4% of the
-// C2 step).  HGM_SYNC_EVENT_FENCE=1 restores the fenced events.
+// C2 step).  HGM_OPT_SYNC_EVENT_FENCE = 1 restores the fenced events.
 // With ranks the ring is a device buffer copied out by hipMemcpyAsync, so those events
 // keep the fence.
 static void sync_event(hgm_ctx* c, hipEvent_t& e, unsigned& have) {
-    static int v = -1;
-    if (v < 0) {
-        const char* env = std::getenv("HGM_SYNC_EVENT_FENCE");
-        v = env ? std::atoi(env) : 0;
-    }
-    const unsigned want = hipEventDisableTiming | ((v || c->world > 1) ? 0u : hipEventDisableSystemFence);
+    const bool fence = c->num.sync_event_fence;
+    const unsigned want = hipEventDisableTiming | ((fence || c->world > 1) ? 0u : hipEventDisableSystemFence);
     if (e && have != want) {
         HGM_HIP(hipEventDestroy(e));
         e = nullptr;
@@ -307,13 +307,33 @@ static void spmv_ref(hgm_ctx* c, const hgm_mat* A, const T* x, T* y) {
     pix_permute<T>(c, A->row_order, t, y, 1);
 }
 
+// Distinct HIP runtime files (libamdhip64*) mapped into this process.  PyTorch-ROCm ships its
+// own copy (torch/lib/libamdhip64.so, requested under that name) next to /opt/rocm's
+// (libamdhip64.so.7, which this library needs): if this library is loaded first and torch
+// after it, both get mapped and the process aborts at exit (double free in the runtimes'
+// static destructors).  Python loads torch first (hgmres/_lib.py); this check turns any
+// other order into a clear error instead of silent undefined behaviour.
+static int hip_runtime_cb(struct dl_phdr_info* info, size_t, void* data) {
+    auto* names = static_cast<std::set<std::string>*>(data);
+    const char* nm = info->dlpi_name;
+    if (nm && std::strstr(nm, "libamdhip64")) {
+        char real[PATH_MAX];
+        names->insert(realpath(nm, real) ? std::string(real) : std::string(nm));
+    }
+    return 0;
+}
+static std::set<std::string> hip_runtimes() {
+    std::set<std::string> names;
+    dl_iterate_phdr(hip_runtime_cb, &names);
+    return names;
+}
+
 static int ctx_init(hgm_ctx* c, int device) {
     c->device = device;
+    if (hip_runtimes().size() > 1) return HGM_E_HIP;   // see hgm_runtime_check
     const char* hs = std::getenv("HGM_HOST_STATS");
     c->host_stats = hs && hs[0] == '1';
     if (hipSetDevice(device) != hipSuccess) return HGM_E_HIP;
-    const char* pd = std::getenv("HGM_PIPE_DEPTH");
-    if (pd) c->pipe_depth = std::atoi(pd) < 1 ? 1 : (std::atoi(pd) > 6 ? 6 : std::atoi(pd));
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return HGM_E_HIP;
     if (hipMalloc(reinterpret_cast<void**>(&c->dscal), sizeof(double) * NSCAL) != hipSuccess) return HGM_E_NOMEM;
     if (hipMemset(c->dscal, 0, sizeof(double) * NSCAL) != hipSuccess) return HGM_E_HIP;
@@ -326,6 +346,16 @@ static int ctx_init(hgm_ctx* c, int device) {
 extern "C" {
 
 HGM_API int hgm_version(void) { return HGM_VERSION; }
+
+HGM_API int hgm_runtime_check(char* msg, int len) {
+    const std::set<std::string> names = hip_runtimes();
+    if (msg && len > 0) {
+        std::string m;
+        for (const auto& s : names) m += (m.empty() ? "" : ";") + s;
+        std::snprintf(msg, (size_t)len, "%s", m.c_str());
+    }
+    return (int)names.size();
+}
 
 HGM_API int hgm_device_count(int* count) {
     int n = 0;
@@ -414,6 +444,67 @@ HGM_API void hgm_ctx_destroy(hgm_ctx* c) {
 }
 
 HGM_API const char* hgm_last_error(const hgm_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
+    if (!c) return HGM_E_ARG;
+    hgm::Numerics& n = c->num;
+    const bool b01 = v == 0.0 || v == 1.0;
+    auto bad = [&](const char* what) {
+        c->err = std::string("hgm_ctx_set_option: ") + what;
+        return HGM_E_ARG;
+    };
+    switch (option) {
+        case HGM_OPT_PARITY: if (!b01) return bad("parity is 0 or 1"); n.parity = v != 0; break;
+        case HGM_OPT_MGS_FORM: if (!b01) return bad("mgs form is 0 or 1"); n.mgs_form = (int)v; break;
+        case HGM_OPT_MGS_SINGLE: if (!b01) return bad("mgs single is 0 or 1"); n.mgs_single = v != 0; break;
+        case HGM_OPT_GRAM_ERR: if (!b01) return bad("gram err is 0 or 1"); n.gram_err = v != 0; break;
+        case HGM_OPT_GRAM_ERR_MIN: if (!(v >= 0.0)) return bad("gram err min >= 0"); n.gram_err_min = v; break;
+        case HGM_OPT_RING_POLL: if (!b01) return bad("ring poll is 0 or 1"); n.ring_poll = v != 0; break;
+        case HGM_OPT_PEND_NORM: if (!b01) return bad("pend norm is 0 or 1"); n.pend_norm = v != 0; break;
+        case HGM_OPT_RECON_SERIAL:
+            if (v != -1.0 && !b01) return bad("recon serial is -1, 0 or 1");
+            n.recon_serial = (int)v;
+            break;
+        case HGM_OPT_RECON_SERIAL_N: if (!(v >= 0.0)) return bad("recon serial n >= 0"); n.recon_serial_n = (int64_t)v; break;
+        case HGM_OPT_PIPE_DEPTH:
+            if (!(v >= 1.0 && v <= 6.0) || v != (double)(int)v) return bad("pipe depth is 1..6");
+            n.pipe_depth = (int)v;
+            break;
+        case HGM_OPT_SYNC_EVENT_FENCE: if (!b01) return bad("sync event fence is 0 or 1"); n.sync_event_fence = v != 0; break;
+        case HGM_OPT_MGS_PPL:
+            if (!(v >= 1.0 && v <= 8.0) || v != (double)(int)v) return bad("mgs ppl is 1..8");
+            n.mgs_ppl = (int)v;
+            break;
+        case HGM_OPT_MGS1_PPL:
+            if (!(v >= 1.0 && v <= 8.0) || v != (double)(int)v) return bad("mgs1 ppl is 1..8");
+            n.mgs1_ppl = (int)v;
+            break;
+        default: return bad("unknown option");
+    }
+    return HGM_OK;
+}
+
+HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
+    if (!c || !v) return HGM_E_ARG;
+    const hgm::Numerics& n = c->num;
+    switch (option) {
+        case HGM_OPT_PARITY: *v = n.parity; break;
+        case HGM_OPT_MGS_FORM: *v = n.mgs_form; break;
+        case HGM_OPT_MGS_SINGLE: *v = n.mgs_single; break;
+        case HGM_OPT_GRAM_ERR: *v = n.gram_err; break;
+        case HGM_OPT_GRAM_ERR_MIN: *v = n.gram_err_min; break;
+        case HGM_OPT_RING_POLL: *v = n.ring_poll; break;
+        case HGM_OPT_PEND_NORM: *v = n.pend_norm; break;
+        case HGM_OPT_RECON_SERIAL: *v = n.recon_serial; break;
+        case HGM_OPT_RECON_SERIAL_N: *v = (double)n.recon_serial_n; break;
+        case HGM_OPT_PIPE_DEPTH: *v = n.pipe_depth; break;
+        case HGM_OPT_SYNC_EVENT_FENCE: *v = n.sync_event_fence; break;
+        case HGM_OPT_MGS_PPL: *v = n.mgs_ppl; break;
+        case HGM_OPT_MGS1_PPL: *v = n.mgs1_ppl; break;
+        default: return HGM_E_ARG;
+    }
+    return HGM_OK;
+}
 
 HGM_API int hgm_ctx_synchronize(hgm_ctx* c) {
     if (!c) return HGM_E_ARG;

@@ -58,9 +58,27 @@ struct Timing {
     void clear();
 };
 
+// Per-context numerics / scheduling options (hgm_ctx_set_option; defaults = production).
+struct Numerics {
+    bool parity = false;            // HGM_OPT_PARITY: fixed-order parity mode
+    int mgs_form = 1;               // 1 one-reduction MGS, 0 one launch per pass
+    bool mgs_single = true;         // one-workgroup sweep for short bases
+    bool gram_err = true;           // Gram error monitor
+    double gram_err_min = 0.01;
+    bool ring_poll = true;
+    bool pend_norm = true;
+    int recon_serial = -1;          // -1 automatic, 0 aux stream, 1 main stream
+    int64_t recon_serial_n = int64_t(4) << 20;
+    int pipe_depth = 2;
+    bool sync_event_fence = false;
+    int mgs_ppl = 1;
+    int mgs1_ppl = 2;
+};
+
 }  // namespace hgm
 
 struct hgm_ctx {
+    hgm::Numerics num;
     int device = 0;
     hipStream_t stream = nullptr;
     int rank = 0, world = 1;
@@ -85,7 +103,6 @@ struct hgm_ctx {
     hipStream_t aux = nullptr;
     hipEvent_t ev_step[8] = {};
     unsigned ev_flags[9] = {};   // creation flags of ev_step[0..7], ev_pipe (capi.cpp sync_event)
-    int pipe_depth = 2;                       // speculative Arnoldi steps in flight (HGM_PIPE_DEPTH)
     // prefix of workspace names while launching on `aux` (its scratch must not alias the
     // main stream's scratch: the two run concurrently)
     std::string ws_tag;
@@ -239,8 +256,8 @@ void recon(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T*
 // Leading dimension of a Krylov basis of vectors of length dim.  Short single-GPU bases
 // get ldq = 4096 k (zero-padded past dim) so one workgroup runs the whole MGS sweep with
 // no bounds checks (kernels.hip, k_mgs_single); the caller zeroes a padded basis.
-int64_t krylov_ld(int64_t dim, bool dist);
-bool krylov_padded(int64_t ldq);
+int64_t krylov_ld(const hgm_ctx* c, int64_t dim, bool dist);
+bool krylov_padded(const hgm_ctx* c, int64_t ldq);
 // src (optional): the vector to orthogonalise when it is not already Q(:,kk+1); the result
 // is written to Q(:,kk+1) either way.
 // side (optional): a multidot enqueued with the sweep (see MdotJob).
@@ -252,7 +269,7 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
 // step kk also writes qg[0..kk+1] = [q_kk'q_0 .. q_kk'q_{kk-1}, q_kk'q_kk, q_kk'x_true] (host
 // ring, system-scope stores), so ||Q y - x_true||^2 = xt'xt - 2 y'(Q'xt) + y'(Q'Q)y needs no
 // pass over the basis.
-bool mgs_gram_ok(int64_t ldq, int maxit, bool dist);
+bool mgs_gram_ok(const hgm_ctx* c, int64_t ldq, int maxit, bool dist);
 // defer (single GPU, one-reduction form only): leave v = Q(:,kk+1) unnormalised and return
 // its norm partials in *defer (np > 0) for the next step's SpMV epilogues (EPI_DIVH / EPI_ADDQ);
 // np == 0 on return means the sweep normalised v itself.  pend_h (device h): Q(:,kk) still
@@ -281,6 +298,17 @@ template <typename T> void fill(hgm_ctx* c, int64_t n, T* x, T v);
 template <typename T> void convert(hgm_ctx* c, int64_t n, const double* in, T* out);
 template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, double* out);
 template <typename T> void fro2(hgm_ctx* c, const hgm_mat* M, double* out_dev);
+
+// ---------------- fixed-order parity mode (kernels.hip; ctx->num.parity) ----------------
+// The documented fixed summation order of a length-n sum of terms t_i (oracle/restatement.py
+// fixed_order()): level 1 sums 64-term chunks sequentially, level 2 sums 64-value
+// chunks of those sequentially, and the level-2 values are summed sequentially.  Terms:
+// OP 0 a_i b_i, OP 1 a_i a_i, OP 2 (a_i - b_i)^2.  The index space may be the concatenation
+// of two segments [a1 (n1) | a2 (n2)] (the augmented vectors of hybrid_lsqr_solver.m:6).
+// *out is written with a system-scope store.
+template <typename T>
+void fixed_reduce(hgm_ctx* c, int op, int64_t n1, const T* a1, const T* b1, int64_t n2, const T* a2, const T* b2,
+                  T* out);
 
 // ---------------- operators (ops.hip) ----------------
 hgm_mat* mat_alloc(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, int dtype);

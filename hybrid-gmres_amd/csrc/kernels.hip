@@ -9,6 +9,8 @@
 //  * Reductions: per-lane sums -> wave butterfly -> 4-wave LDS sum in fixed order
 //    (single 1024-thread launch for vectors up to 256 Ki entries).
 //  * Krylov-basis GEMV (x = Q y) fused with the error monitor, elementwise GKB updates.
+#include <type_traits>
+
 #include "device_common.h"
 
 namespace hgm {
@@ -19,6 +21,84 @@ int parts_for(int64_t n) {
     if (nb < 1) nb = 1;
     if (nb > MAX_PARTS) nb = MAX_PARTS;
     return (int)nb;
+}
+
+// ------------------------------------------------------------------------------
+// Fixed-order sums (parity mode, HGM_OPT_PARITY; internal.h fixed_reduce).  The order is
+// the one oracle/restatement.py's fixed_order() implements with numpy (cumsum is a
+// sequential accumulation): 64-term chunks summed left to right, then 64-value chunks of
+// those, then the remaining values left to right.  Each term is rounded on its own (no
+// FMA: the library is built with -ffp-contract=off).  Throughput is not the point: one
+// thread per chunk, strided loads.
+// ------------------------------------------------------------------------------
+constexpr int FIX_CH = 64;
+
+template <typename T, int OP>
+__device__ __forceinline__ T fixed_term(int64_t i, int64_t n1, const T* a1, const T* b1, const T* a2, const T* b2) {
+    const T* a = i < n1 ? a1 : a2;
+    const T* b = i < n1 ? b1 : b2;
+    const int64_t j = i < n1 ? i : i - n1;
+    if (OP == 0) return a[j] * b[j];
+    if (OP == 1) return a[j] * a[j];
+    const T d = a[j] - b[j];
+    return d * d;
+}
+
+// level 1: c[t] = sequential sum of terms [64 t, 64 t + 64)
+template <typename T, int OP>
+__global__ __launch_bounds__(BS) void k_fixed_l1(int64_t n, int64_t n1, const T* a1, const T* b1, const T* a2,
+                                                 const T* b2, T* c) {
+    const int64_t t = (int64_t)blockIdx.x * BS + threadIdx.x;
+    const int64_t i0 = t * FIX_CH;
+    if (i0 >= n) return;
+    const int64_t i1 = i0 + FIX_CH < n ? i0 + FIX_CH : n;
+    T s = fixed_term<T, OP>(i0, n1, a1, b1, a2, b2);
+    for (int64_t i = i0 + 1; i < i1; ++i) {
+        const T p = fixed_term<T, OP>(i, n1, a1, b1, a2, b2);
+        s = s + p;
+    }
+    c[t] = s;
+}
+
+// level 2 + final, one block: d[l] = sequential sum of c[64 l, 64 l + 64), then out = d_0 + d_1 + ...
+template <typename T>
+__global__ __launch_bounds__(BS) void k_fixed_l2(int64_t nc, const T* __restrict__ c, T* __restrict__ d, T* out) {
+    const int64_t nd = (nc + FIX_CH - 1) / FIX_CH;
+    for (int64_t l = threadIdx.x; l < nd; l += BS) {
+        const int64_t j0 = l * FIX_CH, j1 = j0 + FIX_CH < nc ? j0 + FIX_CH : nc;
+        T s = c[j0];
+        for (int64_t j = j0 + 1; j < j1; ++j) s = s + c[j];
+        d[l] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T s = nd > 0 ? d[0] : T(0);
+        for (int64_t l = 1; l < nd; ++l) s = s + d[l];
+        st_sys(out, s);
+    }
+}
+
+template <typename T, int OP>
+static void fixed_reduce_op(hgm_ctx* c, int64_t n1, const T* a1, const T* b1, int64_t n2, const T* a2, const T* b2,
+                            T* out) {
+    const int64_t n = n1 + n2;
+    const int64_t nc = (n + FIX_CH - 1) / FIX_CH;
+    T* cbuf = c->buf<T>("fixed_c", nc + 1);
+    T* dbuf = c->buf<T>("fixed_d", (nc + FIX_CH - 1) / FIX_CH + 1);
+    if (nc > 0) {
+        const int64_t g = (nc + BS - 1) / BS;
+        k_fixed_l1<T, OP><<<(unsigned)g, BS, 0, c->stream>>>(n, n1, a1, b1, a2, b2, cbuf);
+    }
+    k_fixed_l2<T><<<1, BS, 0, c->stream>>>(nc, cbuf, dbuf, out);
+    HGM_HIP(hipGetLastError());
+}
+
+template <typename T>
+void fixed_reduce(hgm_ctx* c, int op, int64_t n1, const T* a1, const T* b1, int64_t n2, const T* a2, const T* b2,
+                  T* out) {
+    if (op == 0) fixed_reduce_op<T, 0>(c, n1, a1, b1, n2, a2, b2, out);
+    else if (op == 1) fixed_reduce_op<T, 1>(c, n1, a1, a1, n2, a2, a2, out);
+    else fixed_reduce_op<T, 2>(c, n1, a1, b1, n2, a2, b2, out);
 }
 
 // ------------------------------------------------------------------------------
@@ -83,6 +163,10 @@ constexpr int64_t SINGLE_MAX = 1 << 15;   // vectors up to 32 Ki entries: one la
 
 template <typename T, int OP>
 static void reduce_to(hgm_ctx* c, int64_t n, const T* a, const T* b, T* out) {
+    if (c->num.parity) {
+        fixed_reduce_op<T, OP>(c, n, a, b, 0, nullptr, nullptr, out);
+        return;
+    }
     if (n <= SINGLE_MAX) {
         k_reduce_single<T, OP><<<1, 1024, 0, c->stream>>>(n, a, b, out);
         HGM_HIP(hipGetLastError());
@@ -118,6 +202,11 @@ template <typename T>
 void multidot(hgm_ctx* c, int64_t n, int ncols, const T* Q, int64_t ldq, const T* w, T* out, const T* extra) {
     const int nc = ncols + (extra ? 1 : 0);
     if (nc <= 0) return;
+    if (c->num.parity) {   // one fixed-order dot per column (the oracle's fixed_order() Q'w)
+        for (int j = 0; j < ncols; ++j) fixed_reduce_op<T, 0>(c, n, Q + (int64_t)j * ldq, w, 0, nullptr, nullptr, out + j);
+        if (extra) fixed_reduce_op<T, 0>(c, n, extra, w, 0, nullptr, nullptr, out + ncols);
+        return;
+    }
     const int np = parts_for(n);
     T* parts = c->buf<T>("mdot_parts", (size_t)np * nc);
     k_multidot<T><<<dim3(np, nc), BS, 0, c->stream>>>(n, Q, ldq, w, parts, ncols, extra);
@@ -249,19 +338,17 @@ static int gemv_blocks(int64_t n, int ppl = 1) {
     return (int)nb;
 }
 
-// row pairs per lane of the MGS passes (experiment hook HGM_MGS_PPL; default 1)
-static int mgs_ppl() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = std::getenv("HGM_MGS_PPL");
-        v = (e && std::atoi(e) > 0) ? std::atoi(e) : 1;
-    }
-    return v;
-}
+// row pairs per lane of the MGS passes (HGM_OPT_MGS_PPL; default 1)
+static int mgs_ppl(const hgm_ctx* c) { return c->num.mgs_ppl > 0 ? c->num.mgs_ppl : 1; }
 
 template <typename T>
 void gemv_err(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T* x, const T* xt, T* err_out) {
     HGM_REQUIRE(k <= GEMV_KMAX && ldq % 2 == 0, "gemv: k too large");
+    if (c->num.parity) {   // x = Q y (sequential over the columns), then the fixed-order error norm
+        gemv<T>(c, n, k, Q, ldq, y, x, 0);
+        fixed_reduce_op<T, 2>(c, n, x, xt, 0, nullptr, nullptr, err_out);
+        return;
+    }
     const int np = gemv_blocks(n);
     T* parts = c->buf<T>("gemv_parts", MAX_PARTS);
     k_gemv2<T, 0, true><<<np, BS, sizeof(T) * (k > 0 ? k : 1), c->stream>>>(n, k, Q, ldq, y, x, xt, parts);
@@ -273,6 +360,7 @@ template <typename T>
 void recon(hgm_ctx* c, int64_t n, int k, const T* Q, int64_t ldq, const T* y, T* x, const T* xt, T* err_out,
            int64_t m, const T* AQ, int64_t ldaq, const T* b, T* res_out) {
     HGM_REQUIRE(k <= GEMV_KMAX && ldq % 2 == 0 && ldaq % 2 == 0, "recon: k too large");
+    HGM_REQUIRE(!c->num.parity, "recon: parity mode forms the monitors explicitly");
     // x == nullptr: the residual monitor only (the error comes from the Gram error monitor)
     const int nbx = x ? gemv_blocks(n) : 0, nbr = gemv_blocks(m);
     T* parts = c->buf<T>("recon_parts", 2 * MAX_PARTS);
@@ -297,6 +385,11 @@ __global__ __launch_bounds__(BS) void k_fro2(int64_t nnz, const T* __restrict__ 
 
 template <typename T>
 void fro2(hgm_ctx* c, const hgm_mat* M, double* out) {
+    if (c->num.parity && std::is_same<T, double>::value) {   // norm(A,'fro')^2 over the stored values
+        const double* v = reinterpret_cast<const double*>(M->val);
+        fixed_reduce_op<double, 1>(c, M->nnz, v, v, 0, nullptr, nullptr, out);
+        return;
+    }
     const int np = parts_for(M->nnz);
     double* parts = c->buf<double>("fro_parts", MAX_PARTS);
     k_fro2<T><<<np, BS, 0, c->stream>>>(M->nnz, reinterpret_cast<const T*>(M->val), parts);
@@ -520,26 +613,22 @@ __global__ __launch_bounds__(MGS1_BS) void k_mgs_single(int n, const T* __restri
     }
 }
 
-static bool mgs_single_on() {
-    static int mode = -1;   // HGM_MGS_SINGLE=0 disables (experiment hook)
-    if (mode < 0) {
-        const char* e = std::getenv("HGM_MGS_SINGLE");
-        mode = e ? std::atoi(e) : 1;
-    }
-    return mode != 0;
-}
+// one-workgroup sweep for short bases (HGM_OPT_MGS_SINGLE; never in parity mode)
+static bool mgs_single_on(const hgm_ctx* c) { return c->num.mgs_single && !c->num.parity; }
 
-int64_t krylov_ld(int64_t dim, bool dist) {
+int64_t krylov_ld(const hgm_ctx* c, int64_t dim, bool dist) {
     dim = dim > 0 ? dim : 1;
-    if (!dist && dim <= MGS1_MAX && mgs_single_on()) return (dim + 4 * MGS1_BS - 1) / (4 * MGS1_BS) * (4 * MGS1_BS);
+    if (!dist && dim <= MGS1_MAX && mgs_single_on(c)) return (dim + 4 * MGS1_BS - 1) / (4 * MGS1_BS) * (4 * MGS1_BS);
     return (dim + 63) / 64 * 64;
 }
 
-bool krylov_padded(int64_t ldq) { return ldq % (4 * MGS1_BS) == 0 && ldq <= MGS1_MAX && mgs_single_on(); }
+bool krylov_padded(const hgm_ctx* c, int64_t ldq) {
+    return ldq % (4 * MGS1_BS) == 0 && ldq <= MGS1_MAX && mgs_single_on(c);
+}
 
 template <typename T>
 static bool mgs_single(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, const T* src) {
-    if (!krylov_padded(ldq) || n > ldq) return false;
+    if (!krylov_padded(c, ldq) || n > ldq) return false;
     T* v = Q + (int64_t)(kk + 1) * ldq;
     hipStream_t st = c->stream;
     switch (ldq / MGS1_BS) {
@@ -581,21 +670,13 @@ static bool mgs_single(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol
 constexpr int MGS1_CG = 8;       // basis columns per workgroup of the dots pass
 constexpr int MGS1_MAXC = 120;   // k+1 <= 120: the Gram triangle fits 57 KiB of LDS
 
-static int mgs1_mode() {   // HGM_MGS_FORM: 1 = one-reduction (default), 0 = one launch per pass
-    const char* e = std::getenv("HGM_MGS_FORM");
-    return e ? std::atoi(e) : 1;
+// HGM_OPT_MGS_FORM: 1 = one-reduction (default), 0 = one launch per pass
+static int mgs1_mode(const hgm_ctx* c) { return c->num.mgs_form; }
+bool mgs_gram_ok(const hgm_ctx* c, int64_t ldq, int maxit, bool dist) {
+    return !dist && !c->num.parity && maxit <= MGS1_MAXC && mgs1_mode(c) == 1 && !krylov_padded(c, ldq);
 }
-bool mgs_gram_ok(int64_t ldq, int maxit, bool dist) {
-    return !dist && maxit <= MGS1_MAXC && mgs1_mode() == 1 && !krylov_padded(ldq);
-}
-static int mgs1_ppl() {    // element pairs per lane of the dots pass (fewer partials to sum)
-    static int v = -1;
-    if (v < 0) {
-        const char* e = std::getenv("HGM_MGS1_PPL");
-        v = (e && std::atoi(e) > 0) ? std::atoi(e) : 2;
-    }
-    return v;
-}
+// element pairs per lane of the dots pass (HGM_OPT_MGS1_PPL; fewer partials to sum)
+static int mgs1_ppl(const hgm_ctx* c) { return c->num.mgs1_ppl > 0 ? c->num.mgs1_ppl : 2; }
 
 // Forward substitution (I + L) h = r in wave 0 (rows j = lane, lane + 64):
 // s_j = ((r_j - h_0 G_j0) - h_1 G_j1) - ...;  h_i = s_i once rows < i are applied.
@@ -876,13 +957,65 @@ __global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, T* Q, int
     if (threadIdx.x == 0) pout[blockIdx.x] = tot;
 }
 
+// ------------------------------------------------------------------------------
+// MGS in parity mode (HGM_OPT_PARITY): hybrid_ba_gmres_rtp.m:20-26 as written, one
+// fixed-order dot and one axpy launch per column:
+//   h_j = Q(:,j)'v (fixed order) ; v = v - h_j Q(:,j) (two roundings) ; H(k+1,k) = norm(v) ;
+//   Q(:,k+1) = v / H(k+1,k) unless H(k+1,k) == 0
+// ------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(BS) void k_axpy_hdev(int64_t n, T* v, const T* src, const T* __restrict__ q,
+                                                  const T* hp) {
+    const T h = *hp;
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+        const T p = h * q[i];
+        v[i] = src[i] - p;
+    }
+}
+// hd[kk+1] = sqrt(hd[kk+1]) (the fixed-order sum of squares), H(0:kk+1,kk) -> Hcol (system-scope
+// stores: Hcol may be the host ring), then v = v / H(kk+1,kk) unless it is zero
+template <typename T>
+__global__ __launch_bounds__(BS) void k_mgs_parity_fin(int64_t n, int kk, T* v, const T* hd, T* Hcol) {
+    const T nrm = sqrt(hd[kk + 1]);
+    if (blockIdx.x == 0)
+        for (int j = threadIdx.x; j <= kk + 1; j += BS) st_sys(Hcol + j, j <= kk ? hd[j] : nrm);
+    if (nrm == T(0)) return;
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) v[i] = v[i] / nrm;
+}
+
+template <typename T>
+static void mgs_parity(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, const T* src) {
+    T* v = Q + (int64_t)(kk + 1) * ldq;
+    T* hd = c->buf<T>("mgsp_h", kk + 3);
+    const int g = grid_for(n);
+    const T* cur = src;
+    for (int j = 0; j <= kk; ++j) {
+        const T* qj = Q + (int64_t)j * ldq;
+        fixed_reduce_op<T, 0>(c, n, qj, cur, 0, nullptr, nullptr, hd + j);   // :21  H(j,k) = Q(:,j)'*v
+        k_axpy_hdev<T><<<g, BS, 0, c->stream>>>(n, v, cur, qj, hd + j);       // :22  v = v - H(j,k)*Q(:,j)
+        cur = v;
+    }
+    fixed_reduce_op<T, 1>(c, n, v, v, 0, nullptr, nullptr, hd + kk + 1);      // :24  H(k+1,k) = norm(v)
+    k_mgs_parity_fin<T><<<g, BS, 0, c->stream>>>(n, kk, v, hd, Hcol);         // :26  Q(:,k+1) = v / H(k+1,k)
+    HGM_HIP(hipGetLastError());
+}
+
 template <typename T>
 void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, const T* src,
          const MdotJob<T>* side, PendNorm<T>* defer, const T* pend_h, const T* xe, T* qg) {
     if (defer) defer->np = 0;
-    HGM_REQUIRE(!xe || (qg && !dist && kk + 1 <= MGS1_MAXC && mgs1_mode() == 1 && !krylov_padded(ldq)),
+    if (c->num.parity) {
+        HGM_REQUIRE(!dist && !xe && !pend_h, "mgs: parity mode is single-rank, without the fused monitors");
+        hipEvent_t t0 = nullptr;
+        timing_begin(c, KC_MGS, &t0);
+        mgs_parity<T>(c, n, Q, ldq, kk, Hcol, src ? src : Q + (int64_t)(kk + 1) * ldq);
+        if (side) multidot<T>(c, side->n, side->ncols, side->Q, side->ldq, side->w, side->out, side->e);
+        timing_end(c, KC_MGS, t0, sizeof(T) * (double)n * (4.0 * kk + 7.0));
+        return;
+    }
+    HGM_REQUIRE(!xe || (qg && !dist && kk + 1 <= MGS1_MAXC && mgs1_mode(c) == 1 && !krylov_padded(c, ldq)),
                 "mgs: the Gram error monitor needs the one-reduction form");
-    HGM_REQUIRE(!pend_h || (!dist && kk + 1 <= MGS1_MAXC && mgs1_mode() == 1 && !krylov_padded(ldq)),
+    HGM_REQUIRE(!pend_h || (!dist && kk + 1 <= MGS1_MAXC && mgs1_mode(c) == 1 && !krylov_padded(c, ldq)),
                 "mgs: pending normalisation needs the one-reduction form");
     hipEvent_t t0 = nullptr;
     timing_begin(c, KC_MGS, &t0);
@@ -894,7 +1027,7 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
         if (side) multidot<T>(c, side->n, side->ncols, side->Q, side->ldq, side->w, side->out, side->e);
         return;
     }
-    if (kk + 1 <= MGS1_MAXC && mgs1_mode() == 1) {
+    if (kk + 1 <= MGS1_MAXC && mgs1_mode(c) == 1) {
         MdotStage<T> s1, s2;
         if (side && !dist) {
             s1.j = *side;
@@ -905,7 +1038,7 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
             s2.stage = 2;
         }
         hipStream_t st = c->stream;
-        const int npr = gemv_blocks(n, mgs1_ppl());
+        const int npr = gemv_blocks(n, mgs1_ppl(c));
         const int ncg = (kk + MGS1_CG) / MGS1_CG;
         T* pr = c->buf<T>("mgs1_pr", (size_t)MGS1_MAXC * MAX_PARTS);
         T* pg = c->buf<T>("mgs1_pg", (size_t)(MGS1_MAXC + 2) * MAX_PARTS);
@@ -922,7 +1055,7 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
         } else {
             k_mgs1_solve<T, 0><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, nullptr, Gt, hdev, gx);
         }
-        const int nb = gemv_blocks(n, mgs_ppl());
+        const int nb = gemv_blocks(n, mgs_ppl(c));
         T* pout = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
         k_mgs1_update<T><<<nb + s2.blocks(), BS, 0, st>>>(n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout, s2, pend_h,
                                                         Gt + (size_t)kk * (kk - 1) / 2, gx, xe ? qg : nullptr);
@@ -961,7 +1094,7 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
     // One launch per pass: a dependent launch is the cheapest grid-wide exchange of the
     // block partials on gfx950 (2.6-2.9 us vs 3-25 us for in-kernel grid barriers,
     // scripts/barrier_bench.hip).
-    const int np = gemv_blocks(n, mgs_ppl());
+    const int np = gemv_blocks(n, mgs_ppl(c));
     T* P = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
     T* Pb[2] = {P, P + MAX_PARTS};
     T* ss = c->buf<T>("mgs_ss", 4);
@@ -1074,7 +1207,21 @@ __global__ __launch_bounds__(BS) void k_vnorm(int64_t n, T* __restrict__ v, cons
     if (blockIdx.x == 0 && threadIdx.x == 0) st_sys(nrm_out, nrm);
     for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) v[i] = v[i] / nrm;
 }
+// parity mode: v = v / sqrt(*ss) (*ss from a fixed-order sum), norm stored to *nrm_out
+template <typename T>
+__global__ __launch_bounds__(BS) void k_vnorm_ss(int64_t n, T* __restrict__ v, const T* ss, T* nrm_out) {
+    const T nrm = sqrt(*ss);
+    if (blockIdx.x == 0 && threadIdx.x == 0) st_sys(nrm_out, nrm);
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) v[i] = v[i] / nrm;
+}
 template <typename T> void normalize_to(hgm_ctx* c, int64_t n, T* v, T* nrm_out) {
+    if (c->num.parity) {
+        T* ss = c->buf<T>("vnorm_ss", 2);
+        fixed_reduce_op<T, 1>(c, n, v, v, 0, nullptr, nullptr, ss);
+        k_vnorm_ss<T><<<grid_for(n), BS, 0, c->stream>>>(n, v, ss, nrm_out);
+        HGM_HIP(hipGetLastError());
+        return;
+    }
     const int np = parts_for(n);
     T* parts = c->buf<T>("red_parts", MAX_PARTS);
     k_reduce_partial<T, 1><<<np, BS, 0, c->stream>>>(n, v, v, parts);
@@ -1227,7 +1374,8 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
     template void fill<T>(hgm_ctx*, int64_t, T*, T);                                           \
     template void convert<T>(hgm_ctx*, int64_t, const double*, T*);                            \
     template void convert_back<T>(hgm_ctx*, int64_t, const T*, double*);                       \
-    template void fro2<T>(hgm_ctx*, const hgm_mat*, double*);
+    template void fro2<T>(hgm_ctx*, const hgm_mat*, double*);                                   \
+    template void fixed_reduce<T>(hgm_ctx*, int, int64_t, const T*, const T*, int64_t, const T*, const T*, T*);
 
 HGM_INST(double)
 HGM_INST(float)

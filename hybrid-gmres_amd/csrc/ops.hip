@@ -28,12 +28,6 @@ hgm_mat* mat_alloc(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, int dtyp
     }
     M->group = pick_group(rows, nnz);
     M->variant = SPMV_VEC;
-    // tuning overrides (benchmarks only): HGM_SPMV_VARIANT=<bits>, HGM_SPMV_GROUP=<lanes>
-    if (const char* v = std::getenv("HGM_SPMV_VARIANT")) M->variant = std::atoi(v);
-    if (const char* g = std::getenv("HGM_SPMV_GROUP")) {
-        const int gg = std::atoi(g);
-        if (gg == 4 || gg == 8 || gg == 16 || gg == 32 || gg == 64) M->group = gg;
-    }
     return M;
 }
 
@@ -99,7 +93,6 @@ static int32_t* build_chunk_index(hgm_ctx* c, const int64_t* sp, int64_t nseg, i
 }
 
 static int stream_group(double avg) {
-    if (const char* g = std::getenv("HGM_STREAM_GROUP")) return std::atoi(g);
     return avg >= 512 ? 64 : (avg >= 128 ? 32 : (avg >= 40 ? 16 : 8));
 }
 
@@ -169,12 +162,10 @@ __global__ void k_narrow_ci(int64_t nnz, const int32_t* __restrict__ ci, uint16_
 
 // 16-bit column indices for operators with <= 65536 columns (the pixel-major B of C2/C3,
 // whose columns are rays): 10 instead of 12 bytes per fp64 entry for the row kernel.
-// HGM_CI16=0 disables.
 static void build_ci16(hgm_ctx* c, hgm_mat* M) {
     if (M->ci16) (void)hipFree(M->ci16);
     M->ci16 = nullptr;
-    const char* e = std::getenv("HGM_CI16");
-    if ((e && std::atoi(e) == 0) || M->nnz == 0 || M->cols > 65536) return;
+    if (M->nnz == 0 || M->cols > 65536) return;
     HGM_HIP(hipMalloc(&M->ci16, sizeof(uint16_t) * M->nnz));
     k_narrow_ci<<<grid_cap(M->nnz), BS, 0, c->stream>>>(M->nnz, M->ci, M->ci16);
     HGM_HIP(hipGetLastError());
@@ -210,12 +201,10 @@ void finalize_operator(hgm_ctx* c, hgm_mat* M) {
             M->group = avg >= 6 ? 8 : 4;
         }
     }
-    if (const char* v = std::getenv("HGM_SPMV_VARIANT")) M->variant = std::atoi(v);
 }
 
 int64_t auto_band_width(const hgm_mat* M) {
     const size_t vs = M->dtype == HGM_F32 ? 4 : 8;
-    if (const char* e = std::getenv("HGM_BAND_WIDTH")) return std::atoll(e);
     // x fits comfortably in one XCD's 4 MiB L2: no banding
     if ((double)M->cols * vs <= 4.0 * 1024 * 1024) return 0;
     // only long-row operators benefit (the short pixel-major rows of B gather an L2-resident y)
@@ -267,7 +256,6 @@ void set_bands(hgm_ctx* c, hgm_mat* M, int64_t W) {
     M->nbands = (int)nb;
     const double avg = (double)M->nnz / (double)nseg;
     M->bgroup = avg >= 96 ? 32 : (avg >= 24 ? 16 : 8);
-    if (const char* g = std::getenv("HGM_BAND_GROUP")) M->bgroup = std::atoi(g);
     // streaming index over the (band,row) segments; ~2/3 of them are non-empty for a
     // parallel-beam operator, hence the 1.5 factor in the average segment length
     M->bcfo = build_chunk_index(c, M->brp, nseg, M->nnz);

@@ -189,23 +189,10 @@ struct GmresSpec {
 // stream (rocprofv3 trace).  Every ring entry is written exactly once per
 // solve by a system-scope store (st_sys), so a non-sentinel value is final.
 constexpr uint64_t RING_SENTINEL = 0x7FF4DEADBEEF0001ull;   // a NaN no kernel produces
-static bool ring_poll_on() {
-    const char* e = std::getenv("HGM_RING_POLL");
-    return !e || std::atoi(e) != 0;
-}
-// Gram error monitor (HGM_GRAM_ERR=0 disables).  HGM_GRAM_ERR_MIN: the smallest
-// ||x - x_true||^2 / ||x_true||^2 it is used for (default 0.01; below, x is formed per iteration).
-static bool gram_err_on() {
-    const char* e = std::getenv("HGM_GRAM_ERR");
-    return !e || std::atoi(e) != 0;
-}
-static double gram_err_min() {
-    const char* e = std::getenv("HGM_GRAM_ERR_MIN");
-    return e ? std::atof(e) : 0.01;
-}
-// Spin until ring[i] for i in idx are all non-sentinel.  Checks the stream for errors (and
-// for going idle with an entry never written, a bug) once per ms so a fault cannot hang.
-static void ring_wait(hgm_ctx* c, const double* ring, const std::vector<size_t>& idx) {
+// Spin until ring[i] for i in idx are all non-sentinel.  Checks the streams that write them
+// (main and, when it is a different one, aux) for errors, and for all going idle with an entry
+// never written (a bug), once per ms so a fault cannot hang.
+static void ring_wait(hgm_ctx* c, const double* ring, const std::vector<size_t>& idx, hipStream_t aux = nullptr) {
     const volatile uint64_t* r = reinterpret_cast<const volatile uint64_t*>(ring);
     const auto t0 = std::chrono::steady_clock::now();
     auto last = t0;
@@ -221,8 +208,12 @@ static void ring_wait(hgm_ctx* c, const double* ring, const std::vector<size_t>&
         const auto now = std::chrono::steady_clock::now();
         if (now - last > std::chrono::milliseconds(1)) {
             last = now;
-            const hipError_t q = hipStreamQuery(c->stream);
+            hipError_t q = hipStreamQuery(c->stream);
             if (q != hipSuccess && q != hipErrorNotReady) HGM_HIP(q);
+            if (aux && aux != c->stream && q == hipSuccess) {   // idle only when both streams are
+                q = hipStreamQuery(aux);
+                if (q != hipSuccess && q != hipErrorNotReady) HGM_HIP(q);
+            }
             if (q == hipSuccess) {
                 if (idle_seen) throw Error{HGM_E_HIP, "ring poll: stream idle with a ring entry never written"};
                 idle_seen = true;   // one more round: the last stores may still be in flight
@@ -232,16 +223,6 @@ static void ring_wait(hgm_ctx* c, const double* ring, const std::vector<size_t>&
     if (c->host_stats) {
         c->wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
-}
-
-// n from which the GMRES reconstruction is serialised on the main stream (see gmres_family)
-static int64_t recon_serial_min_n() {
-    static int64_t v = -1;
-    if (v < 0) {
-        const char* e = std::getenv("HGM_RECON_SERIAL_N");
-        v = e ? std::atoll(e) : (int64_t)(4 << 20);
-    }
-    return v;
 }
 
 int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_mat* A, const hgm_mat* B,
@@ -263,11 +244,15 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     const bool nspace = sp.side == HGM_SIDE_BA;
     const int64_t dim = nspace ? n : m;
     const bool dist = nspace && dist_n(c);
-    const int64_t ldq = krylov_ld(dim, dist);
+    // parity mode (HGM_OPT_PARITY): the reference's own sequence of operations in
+    // fixed summation orders; every fused or reformulated monitor below is switched off
+    const bool parity = c->num.parity;
+    HGM_REQUIRE(!parity || (!dist_n(c) && po.trivial()), "parity mode: single rank, reference pixel order");
+    const int64_t ldq = krylov_ld(c, dim, dist);
     hipStream_t st = c->stream;
 
     T* Q = c->buf<T>("Q", (size_t)ldq * (maxit + 1));
-    if (krylov_padded(ldq)) HGM_HIP(hipMemsetAsync(Q, 0, sizeof(T) * ldq * (maxit + 1), st));
+    if (krylov_padded(c, ldq)) HGM_HIP(hipMemsetAsync(Q, 0, sizeof(T) * ldq * (maxit + 1), st));
     T* x = c->buf<T>("x", n > 0 ? n : 1);
     T* t = c->buf<T>("t_m", m > 0 ? m : 1);        // m-vector scratch (A*q, residual)
     T* tn = c->buf<T>("t_n", n > 0 ? n : 1);       // n-vector scratch (AB side: B*q)
@@ -276,7 +261,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     const int64_t ldaq = round_up(m > 0 ? m : 1, 64);
     // n-space side: keep the operator's products A*Q(:,j) (the RTP Gram matrix needs them,
     // and the residual monitor b - A*x = b - (A*Q) y reuses them instead of another SpMV)
-    const bool reuse = !(o && (o->flags & HGM_EXPLICIT_RESIDUAL));
+    const bool reuse = !(o && (o->flags & HGM_EXPLICIT_RESIDUAL)) && !parity;
     const bool aq_res = nspace && reuse;
     T* AQ = (sp.proj == PROJ_ABRTP || aq_res) ? c->buf<T>("AQ", (size_t)ldaq * maxit) : nullptr;
     // m-space side: keep B*Q(:,j) and A*(B*Q(:,j)) (the latter is the new Arnoldi vector
@@ -298,9 +283,9 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // Gram error monitor: step k's MGS sweep appends [Q(:,k)'Q(:,0:k-1),
     // Q(:,k)'Q(:,k), Q(:,k)'x_true] to the ring (LQ doubles) and the host evaluates
     // ||Q y_k - x_true||^2 from them, so an iteration's reconstruction reads only the kept A*Q.
-    const bool gem = aq_res && zc && ring_poll_on() && orth == HGM_MGS && mgs_gram_ok(ldq, maxit, dist) &&
-                     gram_err_on();
-    const double gem_min = gram_err_min();
+    const bool gem = aq_res && zc && c->num.ring_poll && orth == HGM_MGS && mgs_gram_ok(c, ldq, maxit, dist) &&
+                     c->num.gram_err;
+    const double gem_min = c->num.gram_err_min;
     const size_t LQ = (size_t)maxit + 2, offQG = offS + 4;
     const size_t ring_n = offQG + (gem ? (size_t)maxit * LQ : 0);
     // single GPU: reconstructions run on the auxiliary stream, concurrently with the
@@ -310,13 +295,13 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // serialised behind the steps (HGM_RECON_SERIAL=0/1 overrides).
     // (with the Gram error monitor the per-iteration reconstruction reads only the kept A*Q,
     // so it stays on the aux stream at any n: C3 1,376 vs 1,368 iters/s serialised)
-    bool recon_serial = !gem && (int64_t)n >= recon_serial_min_n();
-    if (const char* e = std::getenv("HGM_RECON_SERIAL")) recon_serial = std::atoi(e) != 0;
+    bool recon_serial = !gem && (int64_t)n >= c->num.recon_serial_n;
+    if (c->num.recon_serial >= 0) recon_serial = c->num.recon_serial != 0;
     hipStream_t rs_stream = (zc && !recon_serial) ? aux_stream(c) : st;
     if (rs_stream != st) HGM_HIP(hipStreamSynchronize(rs_stream));
     pinned_ring(c, sizeof(double) * ring_n);
     const double* hr = c->hring;
-    const bool poll = zc && ring_poll_on();
+    const bool poll = zc && c->num.ring_poll && !parity;
     if (poll) {
         uint64_t* r = reinterpret_cast<uint64_t*>(c->hring);
         for (size_t i = 0; i < (size_t)maxit * LH; ++i) r[i] = RING_SENTINEL;
@@ -383,9 +368,8 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // leaves v_{k+1} = Q(:,k+1) undivided and step k+1 applies q = v / H(k+1,k) where it reads
     // it — A: (A*v)/h, which also publishes h = H(k+1,k); B: B*(A*q) + lambda*q; the MGS dots
     // kernel writes q back over v — so the sweep needs no scale pass.  Step k's event is then
-    // recorded at the end of step k+1.  HGM_PEND_NORM=0 keeps the scale pass.
-    const char* pn_env = std::getenv("HGM_PEND_NORM");
-    const bool pn_ok = nspace && !dist && orth == HGM_MGS && (!pn_env || std::atoi(pn_env) != 0) &&
+    // recorded at the end of step k+1.  HGM_OPT_PEND_NORM = 0 keeps the scale pass.
+    const bool pn_ok = nspace && !dist && orth == HGM_MGS && c->num.pend_norm && !parity &&
                        spmv_pn_ok(A, EPI_DIVH) && spmv_pn_ok(B, EPI_ADDQ);
     PendNorm<T> pend;                                  // np > 0: Q(:,next step) awaits its division
     T* pn_h = c->buf<T>("pn_h", 2);
@@ -514,7 +498,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         publish(offM + 2 * (size_t)kq, 2);
         pipe_record(c);
     };
-    // Software pipeline over two streams, L = ctx->pipe_depth:
+    // Software pipeline over two streams, L = HGM_OPT_PIPE_DEPTH:
     //     main: S0 S1 S2 S3 ...          (S_k: Arnoldi step k -> H(:,k), Q(:,k+1))
     //     aux :       R0 R1 R2 ...       (R_k: x = Q y_k, monitors of iteration k)
     // At iteration k the host waits for S_k and R_{k-1}, solves for y_k, enqueues R_k
@@ -523,7 +507,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // speculative steps are discarded: they write only Q(:,>k+1), AQ(:,>k), their own
     // ring slots and scratch — never x or a history — so every output equals the
     // reference's.  (Multi-GPU: both sequences share one stream, same semantics.)
-    const int L = c->pipe_depth;                         // speculative steps in flight
+    const int L = c->num.pipe_depth;                     // speculative steps in flight
     for (int j = 0; j <= L && j < maxit; ++j) enqueue_step(j);
     bool done = false;
     for (k = 0; k < maxit; ++k) {
@@ -540,8 +524,9 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             if (gem)
                 for (int i = 0; i < k + 2; ++i) idx.push_back(offQG + (size_t)k * LQ + i);
             ring_wait(c, hr, idx);
-            if (k == 0) {                                // the setup norms (written before step 0)
-                ring_wait(c, hr, {offS, offS + 1, offS + 2});
+            if (k == 0) {                                // the setup norms (written before step 0;
+                                                         // with device inputs partly on the aux stream)
+                ring_wait(c, hr, {offS, offS + 1, offS + 2}, rs_stream);
                 beta = hr[offS];
                 nb = std::sqrt(hr[offS + 1]);
                 nxt = std::sqrt(hr[offS + 2]);
@@ -643,7 +628,8 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         // all maxit iterations ran: the last monitors are still outstanding.  With the
         // reconstruction on the aux stream, x is staged out behind it there (one sync, no
         // host wake-up in between).
-        if (rs_stream != st && x_assigned) {
+        // (x_out == NULL: nothing to stage, so wait for the last monitors explicitly)
+        if (rs_stream != st && x_assigned && x_out != nullptr) {
             StreamScope scope(c, rs_stream, "aux:");
             stage_out_n<T>(c, x_out, x, n, dev, po);     // ends with a sync of the aux stream
             staged = true;
@@ -684,6 +670,8 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     const PixOrder po = n_order(c, A, At);
     HGM_REQUIRE(b_in != nullptr && xt_in != nullptr, "b and x_true are required");
     HGM_REQUIRE(maxit >= 1, "maxit must be >= 1");
+    const bool parity = c->num.parity;   // fixed summation orders
+    HGM_REQUIRE(!parity || (!dist_n(c) && po.trivial()), "parity mode: single rank, reference pixel order");
     const bool dev = o && (o->flags & HGM_DEVICE_PTRS);
     const int64_t m = A->rows, n = A->cols;
     const T* b = stage_in<T>(c, "in_b", b_in, m, dev);
@@ -733,7 +721,13 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
             fill<T>(c, n, tl, T(0));
             epilogue<T>(c, n, tl, EPI_ADD, sq, v);                     // tl = 0 + sq*v (exact: sq*v)
             epilogue<T>(c, n, tl, EPI_SUB, (T)alpha, un);              // tl = tl - alpha*u_n
-            nsumsq<T>(c, n, tl, sl + S_AUX);
+            if (parity) {
+                // norm of the augmented [u_m; u_n] (:23) in one fixed order over the concatenation
+                fixed_reduce<T>(c, 1, m, t, t, n, tl, tl, sl + S_BETA);
+                HGM_HIP(hipMemsetAsync(sl + S_AUX, 0, sizeof(T), c->stream));
+            } else {
+                nsumsq<T>(c, n, tl, sl + S_AUX);
+            }
             Reader rr(c);
             rr.add(&hs[0], sl + S_BETA, sizeof(T));
             rr.add(&hs[1], sl + S_AUX, sizeof(T));
@@ -810,6 +804,8 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     HGM_REQUIRE(At != nullptr, "At is NULL");
     const PixOrder po = n_order(c, A, At);
     HGM_REQUIRE(b_in != nullptr, "b is required");
+    const bool parity = c->num.parity;   // fixed summation orders
+    HGM_REQUIRE(!parity || (!dist_n(c) && po.trivial()), "parity mode: single rank, reference pixel order");
     const bool dev = o && (o->flags & HGM_DEVICE_PTRS);
     const int64_t m = A->rows, n = A->cols;
     if (maxit <= 0) maxit = (int)std::min<int64_t>(m, n);                    // :5 default min(m,n)
@@ -832,8 +828,10 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
 
     sumsq<T>(c, m, b, sl + S_NB);
     if (xt) nsumsq_diff<T>(c, n, xt, x, sl + S_NXT);
-    // ||A||_F (lsmr_solver.m:71, loop-invariant): cached per matrix
-    if (A->fro < 0) {
+    // ||A||_F (lsmr_solver.m:71, loop-invariant): cached per matrix (parity mode: recomputed in
+    // the fixed order, not cached)
+    double normA = A->fro;
+    if (A->fro < 0 || parity) {
         double* f = reinterpret_cast<double*>(c->dscal) + 64;
         if (A->dtype == HGM_F32) fro2<float>(c, A, f); else fro2<double>(c, A, f);
         if (dist_n(c)) allreduce(c, f, 1);
@@ -841,9 +839,9 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         Reader rf(c);
         rf.add(&fv, f, sizeof(double));
         rf.go();
-        const_cast<hgm_mat*>(A)->fro = std::sqrt(fv);
+        normA = std::sqrt(fv);
+        if (!parity) const_cast<hgm_mat*>(A)->fro = normA;
     }
-    const double normA = A->fro;
     Reader r0(c);
     r0.add(&hs[0], sl + S_NB, sizeof(T));
     if (xt) r0.add(&hs[1], sl + S_NXT, sizeof(T));
@@ -855,7 +853,7 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     // are kept, and the images A*x, A'A*x follow the x/h/hbar recurrences (lsmr_monitor).  The
     // iterates u, v, x, h, hbar are the same bits either way (the epilogues below are the
     // fused ones, applied as a separate pass).
-    const bool kept = !(o && (o->flags & HGM_EXPLICIT_RESIDUAL));
+    const bool kept = !(o && (o->flags & HGM_EXPLICIT_RESIDUAL)) && !parity;
     T *Av = nullptr, *Atu0 = nullptr, *Atu1 = nullptr, *Atb = nullptr;
     double *Ihm = nullptr, *Ihbm = nullptr, *Ixm = nullptr, *Ihn = nullptr, *Ihbn = nullptr, *Ixn = nullptr;
     double* dmon = reinterpret_cast<double*>(c->dscal) + 72;   // [||r||^2, ||A'r||^2]
@@ -995,6 +993,7 @@ int hybrid_lsmr(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* 
     HGM_REQUIRE(At != nullptr, "At is NULL");
     const PixOrder po = n_order(c, A, At);
     HGM_REQUIRE(A->dtype == HGM_F64, "hybrid LSMR is fp64");
+    HGM_REQUIRE(!c->num.parity || (!dist_n(c) && po.trivial()), "parity mode: single rank, reference pixel order");
     HGM_REQUIRE(b_in != nullptr && xt_in != nullptr, "b and x_true are required");
     HGM_REQUIRE(maxit >= 1, "maxit must be >= 1");
     using T = double;
@@ -1103,10 +1102,11 @@ int arnoldi(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b_in, 
     const bool nspace = side == HGM_SIDE_BA;
     const int64_t dim = nspace ? n : m;
     const bool dist = nspace && dist_n(c);
-    const int64_t ldq = krylov_ld(dim, dist);
+    const int64_t ldq = krylov_ld(c, dim, dist);
+    HGM_REQUIRE(!c->num.parity || !dist_n(c), "parity mode: single rank");
     const T* b = stage_in<T>(c, "in_b", b_in, m, false);
     T* Q = c->buf<T>("Q", (size_t)ldq * (kg + 1));
-    if (krylov_padded(ldq)) HGM_HIP(hipMemsetAsync(Q, 0, sizeof(T) * ldq * (kg + 1), c->stream));
+    if (krylov_padded(c, ldq)) HGM_HIP(hipMemsetAsync(Q, 0, sizeof(T) * ldq * (kg + 1), c->stream));
     T* Hd = c->buf<T>("H", (size_t)(kg + 1) * kg);
     T* t = c->buf<T>("t_m", m + 1);
     T* tn = c->buf<T>("t_n", n + 1);

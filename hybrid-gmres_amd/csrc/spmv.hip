@@ -339,6 +339,38 @@ __global__ __launch_bounds__(BS) void k_band_reduce(int64_t rows, int nbands, co
     }
 }
 
+// Parity mode (HGM_OPT_PARITY): one thread per row, entries summed sequentially in stored
+// order with a separate multiply and add: s = ((0 + a_0 x_0) + a_1 x_1) + ...  This is
+// scipy's csr_matvec (the oracle's `A @ v`), and, for B = A' from the stable device
+// transpose, its csc_matvec of `A.T @ u` too; the epilogue keeps the closures' two roundings.
+template <typename T, int EPI>
+__global__ __launch_bounds__(BS) void k_spmv_seq(int64_t rows, const int64_t* __restrict__ rp,
+                                                 const int32_t* __restrict__ ci, const T* __restrict__ val,
+                                                 const T* __restrict__ x, T* y, T a, const T* z) {
+    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BS) {
+        T s = 0;
+        for (int64_t j = rp[r]; j < rp[r + 1]; ++j) {
+            const T p = val[j] * x[ci[j]];
+            s = s + p;
+        }
+        y[r] = apply_epi<T, EPI>(s, a, z, r);
+    }
+}
+
+template <typename T>
+static void spmv_seq(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z) {
+    HGM_REQUIRE(epi == EPI_NONE || epi == EPI_ADD || epi == EPI_SUB || epi == EPI_RSUB,
+                "parity mode: pending-normalisation epilogues are not used");
+    const T* val = reinterpret_cast<const T*>(M->val);
+    const dim3 g((unsigned)grid_for(M->rows)), b(BS);
+    switch (epi) {
+        case EPI_NONE: launch(c, true, k_spmv_seq<T, EPI_NONE>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z); break;
+        case EPI_ADD: launch(c, true, k_spmv_seq<T, EPI_ADD>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z); break;
+        case EPI_SUB: launch(c, true, k_spmv_seq<T, EPI_SUB>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z); break;
+        default: launch(c, true, k_spmv_seq<T, EPI_RSUB>, g, b, M->rows, M->rp, M->ci, val, x, y, a, z); break;
+    }
+}
+
 int pick_group(int64_t rows, int64_t nnz) {
     const double avg = rows > 0 ? (double)nnz / (double)rows : 0.0;
     if (avg >= 128) return 64;
@@ -556,8 +588,10 @@ void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T*
     timing_begin(c, kclass, &t0);
     const bool stream = (M->variant & SPMV_STREAM) && (M->nbands > 1 ? M->bcfo != nullptr : M->cfo != nullptr);
     const bool rowk = !stream && M->nbands <= 1;
-    T* nrm = (rowk && (epi == EPI_SUB || epi == EPI_RSUB)) ? sumsq_out : nullptr;
-    if (stream) {
+    T* nrm = (rowk && !c->num.parity && (epi == EPI_SUB || epi == EPI_RSUB)) ? sumsq_out : nullptr;
+    if (c->num.parity) {
+        spmv_seq<T>(c, M, x, y, epi, a, z);
+    } else if (stream) {
         spmv_streamed<T>(c, M, x, y, epi, a, z, pn);
     } else if (M->nbands > 1) {
         spmv_banded<T>(c, M, x, y, epi, a, z, pn);

@@ -19,6 +19,10 @@ HGM_E_NOT_ASSIGNED = -5
 HGM_E_UNSUPPORTED = -6
 
 HGM_F64, HGM_F32 = 0, 1
+# hgm_ctx_option
+OPTIONS = {"parity": 1, "mgs_form": 2, "mgs_single": 3, "gram_err": 4, "gram_err_min": 5, "ring_poll": 6,
+           "pend_norm": 7, "recon_serial": 8, "recon_serial_n": 9, "pipe_depth": 10, "sync_event_fence": 11,
+           "mgs_ppl": 12, "mgs1_ppl": 13}
 HGM_MGS, HGM_CGS2 = 0, 1
 HGM_SIDE_AB, HGM_SIDE_BA = 0, 1
 HGM_DEVICE_PTRS = 1
@@ -41,6 +45,9 @@ class hgm_opts(C.Structure):
 # name -> (restype, argtypes)
 _SIGS = {
     "hgm_version": (c_int, []),
+    "hgm_runtime_check": (c_int, [C.c_char_p, c_int]),
+    "hgm_ctx_set_option": (c_int, [c_void_p, c_int, c_double]),
+    "hgm_ctx_get_option": (c_int, [c_void_p, c_int, P(c_double)]),
     "hgm_device_count": (c_int, [P(c_int)]),
     "hgm_ctx_create": (c_int, [c_int, P(c_void_p)]),
     "hgm_comm_unique_id": (c_int, [c_void_p]),
@@ -117,8 +124,20 @@ def load() -> C.CDLL:
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
+    n, paths = runtime_check(lib)
+    if n > 1:
+        raise ImportError(f"two HIP runtimes are mapped in this process ({paths}): load PyTorch before "
+                          "libhgmres (import hgmres / hgmres.load_library() does), or not at all")
     _lib = lib
     return lib
+
+
+def runtime_check(lib=None):
+    """(number of distinct HIP runtime files mapped, their paths) — hgm_runtime_check."""
+    lib = lib or load()
+    buf = C.create_string_buffer(4096)
+    n = lib.hgm_runtime_check(buf, len(buf))
+    return n, buf.value.decode(errors="replace")
 
 
 def declared_symbols():

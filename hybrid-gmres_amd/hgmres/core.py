@@ -71,6 +71,9 @@ class Context:
             h = C.c_void_p()
             rc = lib.hgm_ctx_create(device, C.byref(h))
             if rc != L.HGM_OK:
+                n, paths = L.runtime_check(lib)
+                if n > 1:
+                    raise HgmError(f"hgm_ctx_create refused: two HIP runtimes are mapped ({paths})")
                 raise HgmError(f"hgm_ctx_create(device={device}) failed with status {rc} (is a GPU visible?)")
             _handle = h
         self._h = _handle
@@ -84,6 +87,32 @@ class Context:
         r, w = C.c_int(), C.c_int()
         _check(L.load().hgm_ctx_rank(self._h, C.byref(r), C.byref(w)), self)
         return r.value, w.value
+
+    def set_option(self, name, value):
+        """Per-context numerics option (``hgm_ctx_set_option``; names in ``_lib.OPTIONS``),
+        e.g. ``ctx.set_option("parity", 1)``.  Returns the previous value."""
+        prev = self.get_option(name)
+        _check(L.load().hgm_ctx_set_option(self._h, L.OPTIONS[name], float(value)), self)
+        return prev
+
+    def get_option(self, name):
+        v = C.c_double()
+        _check(L.load().hgm_ctx_get_option(self._h, L.OPTIONS[name], C.byref(v)), self)
+        return v.value
+
+    def options(self, **kw):
+        """Context manager: set options for a block, restore them after."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def _cm():
+            prev = {k: self.set_option(k, v) for k, v in kw.items()}
+            try:
+                yield self
+            finally:
+                for k, v in prev.items():
+                    self.set_option(k, v)
+        return _cm()
 
     def synchronize(self):
         _check(L.load().hgm_ctx_synchronize(self._h), self)

@@ -81,12 +81,43 @@ typedef struct hgm_opts {
     double* H_out;    /* optional host buffer, (maxit+1) x maxit column-major Hessenberg */
 } hgm_opts;
 
+/* Per-context numerics and scheduling options (hgm_ctx_set_option).  Each changes only the
+ * context it is set on; nothing is read from the process environment.  Values are passed
+ * as doubles (integral options take integral values).  Defaults in brackets. */
+enum hgm_ctx_option {
+    /* Fixed-order parity mode [0]: every SpMV row is summed sequentially in
+     * stored order (scipy's csr_matvec), every dot product / norm in the documented fixed
+     * order of oracle/restatement.py's fixed_order() (64-element sequential chunks, twice,
+     * then sequential), MGS runs one dot + axpy pass per column exactly as
+     * hybrid_ba_gmres_rtp.m:20-26, x = Q*y sums sequentially over the columns, and the
+     * monitors are formed explicitly (b - A*x).  Single rank, reference pixel order, fp64.
+     * For parity checks only: a fraction of the production kernels' throughput. */
+    HGM_OPT_PARITY = 1,
+    HGM_OPT_MGS_FORM = 2,          /* MGS for long vectors: 1 one-reduction form [1], 0 one launch per pass */
+    HGM_OPT_MGS_SINGLE = 3,        /* one-workgroup MGS sweep for short bases [1] */
+    HGM_OPT_GRAM_ERR = 4,          /* Gram error monitor of the n-space GMRES solvers [1] */
+    HGM_OPT_GRAM_ERR_MIN = 5,      /* ... used while ||x-x_true||^2/||x_true||^2 >= this [0.01] */
+    HGM_OPT_RING_POLL = 6,         /* single GPU: host polls the pinned ring instead of events [1] */
+    HGM_OPT_PEND_NORM = 7,         /* pending normalisation of the Krylov vector [1] */
+    HGM_OPT_RECON_SERIAL = 8,      /* GMRES reconstruction: -1 automatic [-1], 0 aux stream, 1 main stream */
+    HGM_OPT_RECON_SERIAL_N = 9,    /* automatic: serialise from this n on [4194304] */
+    HGM_OPT_PIPE_DEPTH = 10,       /* speculative Arnoldi steps in flight, 1..6 [2] */
+    HGM_OPT_SYNC_EVENT_FENCE = 11, /* system-scope release on the pipeline events [0] */
+    HGM_OPT_MGS_PPL = 12,          /* row pairs per lane of the MGS update / pass kernels [1] */
+    HGM_OPT_MGS1_PPL = 13          /* row pairs per lane of the one-reduction dots kernel [2] */
+};
+
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for
  * shard emulation / testing on one device. */
 typedef int (*hgm_allreduce_fn)(double* buf, int64_t count, void* user);
 
 /* ---- context ---------------------------------------------------------- */
 HGM_API int hgm_version(void);
+/* Number of distinct HIP runtime files (libamdhip64*) mapped into the process, their paths
+ * ';'-separated in msg.  More than one (e.g. PyTorch's bundled copy loaded AFTER this library
+ * pulled /opt/rocm's) is refused: hgm_ctx_create then fails with HGM_E_HIP.  Load PyTorch
+ * before this library, or not at all. */
+HGM_API int hgm_runtime_check(char* msg, int len);
 HGM_API int hgm_device_count(int* count);
 HGM_API int hgm_ctx_create(int device, hgm_ctx** ctx);
 HGM_API int hgm_comm_unique_id(void* id_out /* HGM_UNIQUE_ID_BYTES */);
@@ -97,6 +128,9 @@ HGM_API const char* hgm_last_error(const hgm_ctx* ctx);
 HGM_API int hgm_ctx_synchronize(hgm_ctx* ctx);
 HGM_API void* hgm_ctx_stream(hgm_ctx* ctx);
 HGM_API int hgm_ctx_rank(const hgm_ctx* ctx, int* rank, int* world);
+/* Set / read one hgm_ctx_option (HGM_E_ARG for an unknown option or a value out of range). */
+HGM_API int hgm_ctx_set_option(hgm_ctx* ctx, int option, double value);
+HGM_API int hgm_ctx_get_option(const hgm_ctx* ctx, int option, double* value);
 
 /* ---- sparse operators --------------------------------------------------- */
 /* CSR from host arrays (row_ptr: rows+1 int64, col_idx: nnz int32, val: nnz

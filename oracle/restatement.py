@@ -27,22 +27,103 @@ algorithms (``scipy.sparse.linalg.lsqr`` / ``lsmr``, a dense Krylov least-square
 solve) and against the equivalences the reference itself asserts in
 ``run_equivalence_plots.m:12-22`` and ``run_ptr_rtp_comparison.m:15-19``
 (see ``tests/test_oracle.py``).
+
+FIXED-ORDER MODE (:func:`fixed_order`): MATLAB's own summation orders (MKL-blocked
+``ddot``/``dnrm2``, its sparse ``mtimes``) cannot be reproduced by any other
+implementation, so parity at the ulp level needs one documented order that both sides
+follow.  Inside ``with fixed_order():`` every inner product and 2-norm of this module
+sums its terms in the order of :func:`_fsum` (64-term chunks left to right, then 64-value
+chunks of those, then the rest left to right), ``Q*y`` sums over the columns left to
+right, and the Gram products ``AQk'*AQk`` / ``AQk'*b`` are inner products of that kind.
+Sparse products stay scipy's (each CSR row, and each ``A.T @ u`` output, summed
+sequentially in stored order).  libhgmres' parity mode (``HGM_OPT_PARITY``) runs the same
+orders on the GPU, so the two agree to the last bit on the Krylov recurrences.
 """
 from __future__ import annotations
+
+import contextlib
 
 import numpy as np
 import scipy.linalg as sla
 import scipy.sparse as sp
 
 EPS = np.finfo(np.float64).eps
+_FIXED = False      # fixed-order mode (fixed_order())
+_FIX_CH = 64        # chunk length of _fsum (kernels.hip FIX_CH)
 
 
 class OutputNotAssigned(RuntimeError):
     """MATLAB: 'Output argument "x" not assigned during call'."""
 
 
+@contextlib.contextmanager
+def fixed_order(on=True):
+    """Run the restatement with the documented fixed summation order (module docstring)."""
+    global _FIXED
+    prev, _FIXED = _FIXED, bool(on)
+    try:
+        yield
+    finally:
+        _FIXED = prev
+
+
+def _fsum(p):
+    """Fixed-order sum of the terms p (each already rounded): level 1 sums 64-term chunks
+    left to right, level 2 sums 64-value chunks of those left to right, then the level-2
+    values left to right.  np.cumsum is a sequential accumulation; padding with +0.0 does not
+    change a sum.  Mirrors kernels.hip k_fixed_l1 / k_fixed_l2."""
+    p = np.ascontiguousarray(p, dtype=np.float64).ravel()
+    if p.size == 0:
+        return 0.0
+    for _ in range(2):
+        r = (-p.size) % _FIX_CH
+        if r:
+            p = np.concatenate([p, np.zeros(r)])
+        p = np.cumsum(p.reshape(-1, _FIX_CH), axis=1)[:, -1]
+    return float(np.cumsum(p)[-1])
+
+
 def _norm(v):
+    if _FIXED:
+        v = np.asarray(v, dtype=np.float64)
+        return float(np.sqrt(_fsum(v * v)))
     return float(np.linalg.norm(v))
+
+
+def _dot(a, b):
+    """Inner product a'*b (``Q(:,j)'*v``)."""
+    if _FIXED:
+        return _fsum(np.asarray(a, dtype=np.float64) * np.asarray(b, dtype=np.float64))
+    return float(a @ b)
+
+
+def _gemv(Q, y):
+    """``Q*y`` for a dense basis: in fixed-order mode ((Q0 y0 + Q1 y1) + Q2 y2) + ..."""
+    if not _FIXED:
+        return Q @ y
+    x = Q[:, 0] * y[0]
+    for j in range(1, Q.shape[1]):
+        x = x + Q[:, j] * y[j]
+    return x
+
+
+def _tmat(M, v):
+    """``M'*v`` for a dense tall M (one inner product per column)."""
+    if not _FIXED:
+        return M.T @ v
+    return np.array([_dot(M[:, j], v) for j in range(M.shape[1])])
+
+
+def _gram(M):
+    """``M'*M`` for a dense tall M."""
+    if not _FIXED:
+        return M.T @ M
+    k = M.shape[1]
+    G = np.empty((k, k))
+    for i in range(k):
+        for j in range(k):
+            G[i, j] = _dot(M[:, i], M[:, j])
+    return G
 
 
 def mldivide(M, rhs):
@@ -73,7 +154,7 @@ def _mgs_arnoldi_step(Q, H, k, v, breakdown_tol=None):
     """Arnoldi MGS inner loop, ``hybrid_ba_gmres_rtp.m:20-26`` (0-based k).
     Returns True on breakdown."""
     for j in range(k + 1):                       # :20  for j = 1:k
-        H[j, k] = Q[:, j] @ v                    # :21  H(j,k) = Q(:,j)'*v
+        H[j, k] = _dot(Q[:, j], v)               # :21  H(j,k) = Q(:,j)'*v
         v = v - H[j, k] * Q[:, j]                # :22  v = v - H(j,k)*Q(:,j)
     H[k + 1, k] = _norm(v)                       # :24  H(k+1,k) = norm(v)
     if breakdown_tol is None:
@@ -108,7 +189,7 @@ def hybrid_ba_gmres_rtp(A, B, b, x_true, tol, maxit, lam, return_H=False):
         rhs = np.zeros(k + 2)
         rhs[0] = beta
         yk = mldivide(Hk, rhs)                   # :29
-        x = Q[:, : k + 1] @ yk                   # :30
+        x = _gemv(Q[:, : k + 1], yk)             # :30
         residual_norm[k] = _norm(b - A @ x) / nb     # :32
         error_norm[k] = _norm(x - x_true) / nxt      # :33
         if residual_norm[k] <= tol:              # :35
@@ -140,9 +221,9 @@ def hybrid_ab_gmres_rtp(A, B, b, x_true, tol, maxit, lam, return_H=False):
             break
         Qk = Q[:, : k + 1]                       # :28
         AQk = A @ Qk                             # :31
-        G = AQk.T @ AQk
-        yk = mldivide(G + lam * np.eye(k + 1), AQk.T @ b)   # :32
-        x = Qk @ yk                              # :33
+        G = _gram(AQk)
+        yk = mldivide(G + lam * np.eye(k + 1), _tmat(AQk, b))   # :32
+        x = _gemv(Qk, yk)                        # :33
         residual_norm[k] = _norm(b - A @ x) / nb     # :35
         error_norm[k] = _norm(x - x_true) / nxt      # :36
         if residual_norm[k] <= tol:              # :38
@@ -226,6 +307,8 @@ def lsmr_solver(A, b, x_true=None, tol=None, maxit=None):
     nb = _norm(b)
     if hasattr(A, "fro_norm"):                   # operator wrappers used by the tests
         normA = A.fro_norm()
+    elif _FIXED and sp.issparse(A):              # norm(A,'fro') over the stored values
+        normA = _norm(sp.csr_matrix(A).data)
     else:
         normA = float(sp.linalg.norm(A, "fro")) if sp.issparse(A) else float(np.linalg.norm(A, "fro"))
     k = 0
@@ -354,7 +437,7 @@ def hybrid_lsmr_solver(A, b, x_true, tol, maxit, lam):
         e1[0] = 1.0
         RHS = B_k[0, 0] * beta1 * (G @ e1)       # :42
         yk = mldivide(LHS, RHS)                  # :44
-        x = V[:, : k + 1] @ yk                   # :45
+        x = _gemv(V[:, : k + 1], yk)             # :45
         error_norm[k] = _norm(x - x_true) / nxt  # :47
         residual_norm[k] = _norm(b - A @ x) / nb # :48
         if residual_norm[k] <= tol:              # :50
@@ -404,7 +487,7 @@ def _gmres_ptr(A, B, b, x_true, tol, maxit, lam, side, hybrid, explicit_BA=False
             yk = mldivide(Hk.T @ Hk + lam * np.eye(k + 1), Hk.T @ tk)   # hybrid :34-36
         else:
             yk = mldivide(Hk, tk)                # nonhybrid :35
-        zk = Q[:, : k + 1] @ yk                  # :37 / :36
+        zk = _gemv(Q[:, : k + 1], yk)            # :37 / :36
         xk = B @ zk if side == "ab" else zk      # AB :38 ; BA :37
         res[k] = _norm(b - A @ xk) / nb          # :40 / :39
         err[k] = _norm(xk - x_true) / nxt        # :41 / :40

@@ -1,0 +1,26 @@
+/*
+ * ORACLE — all-core CPU SpMV for the bench's cpu_baseline leg (test infrastructure only;
+ * never linked into libhgmres).
+ *
+ * y = M x for a CSR matrix, rows split into contiguous static blocks across OpenMP
+ * threads.  Every row is summed sequentially in stored order with a separate multiply
+ * and add (built with -ffp-contract=off), i.e. exactly scipy's csr_matvec
+ * (`sum += Ax[jj] * Xx[Aj[jj]]`, scipy/sparse/sparsetools/csr.h), so the product is
+ * bitwise identical to `M @ x` in oracle/restatement.py — only the wall time changes.
+ * The reference computes these products with MATLAB's multithreaded sparse mtimes
+ * (e.g. hybrid_ab_gmres_rtp.m:6,19; ABgmres_nonhybrid_bounds.m:25).
+ */
+#include <omp.h>
+#include <stdint.h>
+
+void oracle_csr_matvec(int64_t rows, const int64_t* rp, const int32_t* ci, const double* val, const double* x,
+                       double* y) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < rows; ++i) {
+        double s = 0.0;
+        for (int64_t j = rp[i]; j < rp[i + 1]; ++j) s += val[j] * x[ci[j]];
+        y[i] = s;
+    }
+}
+
+int oracle_num_threads(void) { return omp_get_max_threads(); }

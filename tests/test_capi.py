@@ -85,3 +85,42 @@ def test_no_cpu_fallback_without_device():
         pytest.skip("a device is visible")
     with pytest.raises(hgmres.HgmError):
         hgmres.Context(0)
+
+
+def test_hip_runtime_order_guard(tmp_path):
+    """One HIP runtime per process.  hgmres loads PyTorch's runtime
+    before libhgmres, so importing torch afterwards maps no second copy and the process
+    exits 0; loading libhgmres by hand BEFORE torch maps two runtimes, which
+    hgm_runtime_check reports and hgm_ctx_create refuses (that process still aborts in the
+    runtimes' exit handlers, hence only its output is checked)."""
+    import subprocess
+    import sys
+    pkg = os.path.join(ROOT, "hybrid-gmres_amd")
+    good = subprocess.run([sys.executable, "-c",
+                           f"import sys; sys.path.insert(0, {pkg!r})\n"
+                           "import hgmres; from hgmres import _lib as L\n"
+                           "hgmres.load_library(); import torch\n"
+                           "print(L.runtime_check()[0])"], capture_output=True, text=True, timeout=300,
+                          cwd=str(tmp_path))
+    assert good.returncode == 0, good.stderr[-2000:]
+    assert good.stdout.strip().splitlines()[-1] == "1"
+    bad = subprocess.run([sys.executable, "-c",
+                          "import ctypes\n"
+                          f"lib = ctypes.CDLL({L.LIB_PATH!r}, mode=ctypes.RTLD_GLOBAL)\n"
+                          "import torch\n"
+                          "buf = ctypes.create_string_buffer(4096)\n"
+                          "h = ctypes.c_void_p()\n"
+                          "print(lib.hgm_runtime_check(buf, 4096), lib.hgm_ctx_create(0, ctypes.byref(h)), flush=True)\n"],
+                         capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert bad.stdout.split()[:2] == ["2", str(L.HGM_E_HIP)], (bad.stdout, bad.stderr[-2000:])
+
+
+def test_ctx_option_api_without_gpu():
+    lib = hgmres.load_library()
+    v = ctypes.c_double()
+    assert lib.hgm_ctx_set_option(None, 1, 1.0) == L.HGM_E_ARG
+    assert lib.hgm_ctx_get_option(None, 1, ctypes.byref(v)) == L.HGM_E_ARG
+    assert set(L.OPTIONS.values()) == set(range(1, 14))
+    txt = open(os.path.join(ROOT, "include", "hgmres.h")).read()
+    for name, val in L.OPTIONS.items():   # the Python names mirror the header's enum
+        assert re.search(rf"HGM_OPT_{name.upper()}\s*=\s*{val}\b", txt), name

@@ -75,12 +75,18 @@ class _Rounded:
         return _Rounded(sp.vstack([self.M, np.sqrt(lam) * sp.identity(n, format="csr")]).tocsr(), self.rng, self.c)
 
 
-def _gkb_check(fn, A, out, seeds=tuple(range(1, 9)), k=100.0, nhist=2):
-    """Compare a GPU result `out` = (x, hist1, hist2, ...) with the oracle `fn(A)`.
-    Tolerance per quantity and per history entry: max(1e-10, k x the largest spread
-    of the oracle itself under the rounding-error model (8 seeds: LSQR without
-    reorthogonalisation amplifies rounding chaotically, and at tomo64 the max over 3
-    seeds underestimates the max over 20 by up to 10x at late iterations))."""
+GKB_CAP = 1e-6   # no production-kernel tolerance above this
+
+
+def _gkb_check(fn, A, out, seeds=tuple(range(1, 9)), k=100.0, nhist=2, label=""):
+    """Compare a GPU result `out` = (x, hist1, hist2, ...) of the PRODUCTION kernels with the
+    oracle `fn(A)`.  Tolerance per quantity and per history entry: max(1e-10, k x the largest
+    spread of the oracle itself under the rounding-error model (8 seeds: LSQR without
+    reorthogonalisation amplifies rounding chaotically)), capped at GKB_CAP = 1e-6.  Entries
+    whose envelope would exceed the cap (late iterations where any two correct fp64 summation
+    orders disagree by more than 1e-8) are not judged here: the fixed-order parity mode
+    (tests/test_gpu_parity_mode.py) holds every entry, and x, at 1e-10.  Measured deviations
+    are printed (pytest -s / -rA) so the margin is visible."""
     ref = fn(A)
     sx = 0.0
     sh = [np.zeros(np.size(r_)) for r_ in ref[1:1 + nhist]]
@@ -93,14 +99,21 @@ def _gkb_check(fn, A, out, seeds=tuple(range(1, 9)), k=100.0, nhist=2):
                 d = np.abs(p_ - r_) / np.maximum(np.abs(r_), 1e-300)
             sh[i] = np.maximum(sh[i], np.nan_to_num(d))
     tx = max(TOL, k * sx)
-    assert rel(out[0], ref[0]) <= tx, (rel(out[0], ref[0]), tx)
+    dx = rel(out[0], ref[0])
+    msg = [f"x: dev {dx:.2e} tol {min(tx, GKB_CAP):.2e}" + (" (over cap: parity mode)" if tx > GKB_CAP else "")]
+    if tx <= GKB_CAP:
+        assert dx <= tx, (dx, tx)
     for i in range(nhist):
         a_, r_ = np.asarray(out[1 + i]), np.asarray(ref[1 + i])
         assert a_.shape == r_.shape
         ok = ~(np.isnan(a_) & np.isnan(r_))
         tol_v = np.maximum(TOL, k * sh[i])
-        d = np.abs(a_ - r_)[ok] / np.maximum(np.abs(r_), 1e-300)[ok]
-        assert np.all(d <= tol_v[ok]), (np.max(d / tol_v[ok]), i)
+        judged = ok & (tol_v <= GKB_CAP)
+        d = np.abs(a_ - r_) / np.maximum(np.abs(r_), 1e-300)
+        assert np.all(d[judged] <= tol_v[judged]), (np.max(d[judged] / tol_v[judged]), i)
+        msg.append(f"hist{i}: max dev {np.max(d[judged], initial=0):.2e} over {int(judged.sum())} judged entries, "
+                   f"{int((ok & ~judged).sum())} left to parity mode")
+    print(f"[gkb {label}] " + "; ".join(msg))
     return ref
 
 
@@ -403,116 +416,71 @@ def test_dimension_mismatch_raises(gpu_ctx, P64):
         hgmres.lsqr_solver(P64.A, P64.b[:-1], P64.x_true, 0.0, 3, ctx=gpu_ctx)
 
 
-_MGS_CHILD = r"""
-import sys, numpy as np
-sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + "/hybrid-gmres_amd")
-import hgmres
-from hgmres.problems import tomo_problem
-P = tomo_problem(int(sys.argv[3]), int(sys.argv[4]), noise=1e-2, seed=3)
-ctx = hgmres.Context(0)
-out = {}
-for side, fn in (("ab", hgmres.hybrid_ab_gmres_rtp), ("ba", hgmres.hybrid_ba_gmres_rtp)):
-    x, e, r, k, H = fn(P.A, P.B, P.b, P.x_true, 0.0, 12, 1e-2, ctx=ctx, return_H=True)
-    out[side + "_x"], out[side + "_H"] = x, H
-np.savez(sys.argv[2], **out)
-"""
+def _gm_solve(ctx, P, maxit, tags, tols=None, **opts):
+    """Solve with per-context options set for the call (hgm_ctx_set_option)."""
+    fns = {"hab": (hgmres.hybrid_ab_gmres_rtp, (1e-2,)), "hba": (hgmres.hybrid_ba_gmres_rtp, (1e-2,)),
+           "abn": (hgmres.ABgmres_nonhybrid_bounds, ())}
+    out = {}
+    with ctx.options(**opts):
+        for tag in tags:
+            fn, lam = fns[tag]
+            tol = (tols or {}).get(tag, 0.0)
+            o = fn(P.A, P.B, P.b, P.x_true, tol, maxit, *lam, ctx=ctx, return_H=True)
+            out[tag + "_x"], out[tag + "_e"], out[tag + "_r"], out[tag + "_H"] = o[0], o[1], o[2], o[-1]
+    return out
 
 
 @pytest.mark.parametrize("N,na", [(64, 64), (128, 8), (40, 30)])
-def test_mgs_single_workgroup_matches_multiblock(tmp_path, N, na):
+def test_mgs_single_workgroup_matches_multiblock(gpu_ctx, N, na):
     """The one-workgroup MGS sweep (short bases, ldq = 4096 k zero-padded) against the
-    per-pass multi-block sweep (HGM_MGS_SINGLE=0), each in its own process (the switch is
-    read once per process).  Sizes cover a padded m-space (AB) and n-space (BA) basis,
-    dim a multiple of 4096 (128^2 / 4 chunks: no padding) and a ragged dim."""
-    res = {}
-    for mode in ("1", "0"):
-        f = str(tmp_path / f"mgs{mode}.npz")
-        env = dict(os.environ, HGM_MGS_SINGLE=mode)
-        subprocess.run([sys.executable, "-c", _MGS_CHILD, ROOT, f, str(N), str(na)], env=env, check=True,
-                       timeout=600)
-        res[mode] = np.load(f)
-    for side in ("ab", "ba"):
-        H_ok(res["1"][side + "_H"], res["0"][side + "_H"], 1e-12)
-        assert rel(res["1"][side + "_x"], res["0"][side + "_x"]) < 1e-11
-
-
-_MGS_FORM_CHILD = r"""
-import sys, numpy as np
-sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + "/hybrid-gmres_amd")
-import hgmres
-from hgmres.problems import tomo_problem
-P = tomo_problem(int(sys.argv[3]), int(sys.argv[4]), noise=1e-2, seed=0)
-maxit = int(sys.argv[5])
-ctx = hgmres.Context(0)
-out = {}
-for tag, fn, lam in (("hab", hgmres.hybrid_ab_gmres_rtp, (1e-2,)), ("hba", hgmres.hybrid_ba_gmres_rtp, (1e-2,)),
-                     ("abn", hgmres.ABgmres_nonhybrid_bounds, ())):
-    o = fn(P.A, P.B, P.b, P.x_true, 0.0, maxit, *lam, ctx=ctx, return_H=True)
-    out[tag + "_x"], out[tag + "_H"], out[tag + "_r"], out[tag + "_e"] = o[0], o[-1], o[2], o[1]
-o = hgmres.hybrid_ba_gmres_rtp(P.A, P.B, P.b, P.x_true, 0.0, maxit, 1e-2, ctx=ctx, return_H=True)
-out["hba_x2"], out["hba_H2"] = o[0], o[-1]
-np.savez(sys.argv[2], **out)
-"""
+    multi-block sweep (HGM_OPT_MGS_SINGLE = 0), switched per context.  Sizes cover a padded
+    m-space (AB) and n-space (BA) basis, dim a multiple of 4096 (128^2 / 4 chunks: no
+    padding) and a ragged dim."""
+    P = tomo_problem(N, na, noise=1e-2, seed=3)
+    res = {mode: _gm_solve(gpu_ctx, P, 12, ("hab", "hba"), mgs_single=mode) for mode in (1, 0)}
+    for side in ("hab", "hba"):
+        H_ok(res[1][side + "_H"], res[0][side + "_H"], 1e-12)
+        assert rel(res[1][side + "_x"], res[0][side + "_x"]) < 1e-11
 
 
 @pytest.mark.parametrize("N,na,maxit", [(64, 91, 80), (64, 90, 20)])
-def test_mgs_one_reduction_form(tmp_path, N, na, maxit):
+def test_mgs_one_reduction_form(gpu_ctx, N, na, maxit):
     """MGS in one-reduction form (default for multi-block sweeps: dots, forward
     substitution with the kept Gram triangle, update, scale) against the one-launch-per-pass
-    form (HGM_MGS_FORM=0) and the oracle's sequential MGS.  HGM_MGS_SINGLE=0 forces the
-    multi-block path at this size.  64^2/91 has an odd m (m-space basis of ABgmres) and
-    80 iterations cover the 10 column groups of the dots pass and the second row per lane
-    of the substitution (k >= 64).  Bar: 1e-10 (north_star) against the oracle."""
-    res = {}
-    for form in ("1", "0"):
-        f = str(tmp_path / f"form{form}.npz")
-        env = dict(os.environ, HGM_MGS_SINGLE="0", HGM_MGS_FORM=form)
-        subprocess.run([sys.executable, "-c", _MGS_FORM_CHILD, ROOT, f, str(N), str(na), str(maxit)], env=env,
-                       check=True, timeout=600)
-        res[form] = np.load(f)
+    form (HGM_OPT_MGS_FORM = 0) and the oracle's sequential MGS.  HGM_OPT_MGS_SINGLE = 0
+    forces the multi-block path at this size.  64^2/91 has an odd m (m-space basis of
+    ABgmres) and 80 iterations cover the 10 column groups of the dots pass and the second row
+    per lane of the substitution (k >= 64).  Bar: 1e-10 (north_star) against the oracle."""
     P = tomo_problem(N, na, noise=1e-2, seed=0)
+    tags = ("hab", "hba", "abn")
+    res = {form: _gm_solve(gpu_ctx, P, maxit, tags, mgs_single=0, mgs_form=form) for form in (1, 0)}
     refs = {"hab": R.hybrid_ab_gmres_rtp(P.A, P.B, P.b, P.x_true, 0.0, maxit, 1e-2, return_H=True),
             "hba": R.hybrid_ba_gmres_rtp(P.A, P.B, P.b, P.x_true, 0.0, maxit, 1e-2, return_H=True),
             "abn": R.ABgmres_nonhybrid_bounds(P.A, P.B, P.b, P.x_true, 0.0, maxit, return_H=True)}
     for tag, ref in refs.items():
-        for form in ("1", "0"):
+        for form in (1, 0):
             g = res[form]
             H_ok(g[tag + "_H"], ref[-1])
             assert rel(g[tag + "_x"], ref[0]) < TOL, (tag, form)
             hist_ok(g[tag + "_r"], ref[2], TOL)
             hist_ok(g[tag + "_e"], ref[1], TOL)
-        H_ok(res["1"][tag + "_H"], res["0"][tag + "_H"], 1e-10)
-    for form in ("1", "0"):   # fixed summation orders: repeated solves are bitwise equal
-        assert np.array_equal(res[form]["hba_x"], res[form]["hba_x2"])
-        assert np.array_equal(res[form]["hba_H"], res[form]["hba_H2"])
-
-
-_GEM_CHILD = r"""
-import sys, numpy as np
-sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + "/hybrid-gmres_amd")
-import hgmres
-from hgmres.problems import tomo_problem
-P = tomo_problem(int(sys.argv[3]), int(sys.argv[4]), noise=1e-2, seed=0)
-maxit = int(sys.argv[5])
-tols = {"hab": float(sys.argv[6]), "hba": float(sys.argv[7])}
-ctx = hgmres.Context(0)
-out = {}
-for tag, fn in (("hab", hgmres.hybrid_ab_gmres_rtp), ("hba", hgmres.hybrid_ba_gmres_rtp)):
-    x, e, r, k, H = fn(P.A, P.B, P.b, P.x_true, tols[tag], maxit, 1e-2, ctx=ctx, return_H=True)
-    out[tag + "_x"], out[tag + "_e"], out[tag + "_r"], out[tag + "_H"] = x, e, r, H
-np.savez(sys.argv[2], **out)
-"""
+        H_ok(res[1][tag + "_H"], res[0][tag + "_H"], 1e-10)
+    for form in (1, 0):   # fixed summation orders: repeated solves are bitwise equal
+        again = _gm_solve(gpu_ctx, P, maxit, ("hba",), mgs_single=0, mgs_form=form)
+        assert np.array_equal(res[form]["hba_x"], again["hba_x"])
+        assert np.array_equal(res[form]["hba_H"], again["hba_H"])
 
 
 @pytest.mark.parametrize("N,na,maxit,stop", [(64, 90, 20, False), (64, 91, 80, False), (64, 90, 20, True)])
-def test_gram_error_monitor(tmp_path, N, na, maxit, stop):
+def test_gram_error_monitor(gpu_ctx, N, na, maxit, stop):
     """Gram error monitor: the error history as x_true'x_true - 2y'(Q'x_true)
     + y'(Q'Q)y, with Q'Q and Q'x_true from the one-reduction MGS sweep, and x formed once
-    after the loop.  Variants: off (HGM_GRAM_ERR=0), on (default threshold) and mixed
-    (threshold at the median error: later iterations form x explicitly).  x, H and the
-    residual history are bitwise the explicit path's (same kernels); the error history agrees
-    with it to 1e-12 and with the oracle to 1e-10.  `stop` ends both solves by `tol` at k = 5
-    (hybrid_*_rtp.m:35), so x is that of an iteration before the last Arnoldi step."""
+    after the loop.  Variants (per-context options): off (gram_err = 0), on (default
+    threshold) and mixed (threshold at the median error: later iterations form x explicitly).
+    x, H and the residual history are bitwise the explicit path's (same kernels); the error
+    history agrees with it to 1e-12 and with the oracle to 1e-10.  `stop` ends both solves by
+    `tol` at k = 5 (hybrid_*_rtp.m:35), so x is that of an iteration before the last Arnoldi
+    step."""
     P = tomo_problem(N, na, noise=1e-2, seed=0)
     fns = {"hab": R.hybrid_ab_gmres_rtp, "hba": R.hybrid_ba_gmres_rtp}
     tols = {t: 0.0 for t in fns}
@@ -520,15 +488,8 @@ def test_gram_error_monitor(tmp_path, N, na, maxit, stop):
         tols = {t: float(f(P.A, P.B, P.b, P.x_true, 0.0, maxit, 1e-2)[2][4]) * (1 + 1e-9) for t, f in fns.items()}
     refs = {t: f(P.A, P.B, P.b, P.x_true, tols[t], maxit, 1e-2, return_H=True) for t, f in fns.items()}
     thr = float(np.median(refs["hab"][1])) ** 2
-    variants = {"off": {"HGM_GRAM_ERR": "0"}, "on": {"HGM_GRAM_ERR": "1"},
-                "mix": {"HGM_GRAM_ERR": "1", "HGM_GRAM_ERR_MIN": repr(thr)}}
-    res = {}
-    for v, extra in variants.items():
-        f = str(tmp_path / f"gem_{v}.npz")
-        env = dict(os.environ, HGM_MGS_SINGLE="0", **extra)
-        subprocess.run([sys.executable, "-c", _GEM_CHILD, ROOT, f, str(N), str(na), str(maxit),
-                        repr(tols["hab"]), repr(tols["hba"])], env=env, check=True, timeout=600)
-        res[v] = np.load(f)
+    variants = {"off": dict(gram_err=0), "on": dict(gram_err=1), "mix": dict(gram_err=1, gram_err_min=thr)}
+    res = {v: _gm_solve(gpu_ctx, P, maxit, ("hab", "hba"), tols=tols, mgs_single=0, **o) for v, o in variants.items()}
     off = res["off"]
     for tag, ref in refs.items():
         if stop:
@@ -542,6 +503,50 @@ def test_gram_error_monitor(tmp_path, N, na, maxit, stop):
             hist_ok(g[tag + "_e"], off[tag + "_e"], 1e-12)
             hist_ok(g[tag + "_e"], ref[1], TOL)
             assert rel(g[tag + "_x"], ref[0]) < TOL
+
+
+def test_ctx_options_roundtrip(gpu_ctx):
+    """hgm_ctx_set_option / get_option: per-context values, range checks, restore."""
+    prev = gpu_ctx.get_option("pipe_depth")
+    with gpu_ctx.options(pipe_depth=4, gram_err_min=0.5):
+        assert gpu_ctx.get_option("pipe_depth") == 4 and gpu_ctx.get_option("gram_err_min") == 0.5
+    assert gpu_ctx.get_option("pipe_depth") == prev
+    with pytest.raises(ValueError):
+        gpu_ctx.set_option("pipe_depth", 9)
+    with pytest.raises(ValueError):
+        gpu_ctx.set_option("parity", 0.5)
+    other = hgmres.Context(0)          # options are per context
+    try:
+        gpu_ctx.set_option("mgs_form", 0)
+        assert other.get_option("mgs_form") == 1
+    finally:
+        gpu_ctx.set_option("mgs_form", 1)
+        other.close()
+
+
+def test_gmres_null_x_monitors(gpu_ctx, P64):
+    """ABI: x may be NULL (the caller wants only the histories).  The last iteration's monitors
+    must still be waited for (they are read from the pinned ring)."""
+    import ctypes as C
+    from hgmres import _lib as L
+    Ao = hgmres.SparseOperator.from_scipy(P64.A, gpu_ctx)
+    Bo = hgmres.SparseOperator.from_scipy(P64.B, gpu_ctx)
+    lib = L.load()
+    for fn in ("hgm_hybrid_ab_gmres_rtp_ex", "hgm_hybrid_ba_gmres_rtp_ex"):
+        hist = {}
+        for with_x in (True, False):
+            x = np.zeros(P64.A.shape[1])
+            e, r, it = np.zeros(15), np.zeros(15), C.c_int(0)
+            o = L.hgm_opts()
+            o.flags, o.orth, o.H_out = 0, L.HGM_MGS, None
+            rc = getattr(lib, fn)(gpu_ctx.handle, C.byref(o), Ao._h, Bo._h, P64.b.ctypes.data_as(L.dp),
+                                  P64.x_true.ctypes.data_as(L.dp), 0.0, 15, 1e-2,
+                                  x.ctypes.data_as(L.dp) if with_x else None, e.ctypes.data_as(L.dp),
+                                  r.ctypes.data_as(L.dp), C.byref(it))
+            assert rc == 0 and it.value == 15
+            hist[with_x] = (e, r)
+        assert np.array_equal(hist[True][0], hist[False][0]) and np.array_equal(hist[True][1], hist[False][1]), fn
+        assert hist[False][1][-1] > 0
 
 
 def test_cgs2_matches_mgs(gpu_ctx, P64):
@@ -570,16 +575,20 @@ def test_lsqr_family(gpu_ctx, name, P64):
         (lambda AA: R.hybrid_lsmr_solver(AA, b, xt, 0.0, maxit, lam),
          lambda: hgmres.hybrid_lsmr_solver(A, b, xt, 0.0, maxit, lam, ctx=gpu_ctx)),
     ]
-    for ref_fn, gpu_fn in cases:
+    for label, (ref_fn, gpu_fn) in zip(("lsqr", "hybrid_lsqr", "hybrid_lsmr"), cases):
         out = gpu_fn()
-        ref = _gkb_check(ref_fn, A, out)
+        ref = _gkb_check(ref_fn, A, out, label=f"{label} {name}")
         assert out[3] == ref[3]
+    # lsqr_solver's error history is read once after the loop: its last entry is the returned x's
+    x, e, r, k = hgmres.lsqr_solver(A, b, xt, 0.0, maxit, ctx=gpu_ctx)
+    assert abs(e[-1] - np.linalg.norm(x - xt) / np.linalg.norm(xt)) <= 1e-12 * e[-1]
+    assert abs(r[-1] - np.linalg.norm(b - A @ x) / np.linalg.norm(b)) <= 1e-12 * r[-1]   # lsqr_solver.m:52
 
 
 def test_lsmr(gpu_ctx, P64):
     A, b, xt = P64.A, P64.b, P64.x_true
     x, eh, rh, ah, it = hgmres.lsmr_solver(A, b, xt, 0.0, 20, ctx=gpu_ctx)
-    ref = _gkb_check(lambda AA: R.lsmr_solver(AA, b, xt, 0.0, 20), A, (x, eh, rh, ah), nhist=3)
+    ref = _gkb_check(lambda AA: R.lsmr_solver(AA, b, xt, 0.0, 20), A, (x, eh, rh, ah), nhist=3, label="lsmr tomo64")
     assert it == ref[4] == 20
     # defaults and the NaN error history (lsmr_solver.m:3,5,28)
     x2, eh2, rh2, ah2, it2 = hgmres.lsmr_solver(A, b, ctx=gpu_ctx)

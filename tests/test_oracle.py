@@ -219,3 +219,59 @@ def test_golden_c1_operator_hash():
         h.update(np.ascontiguousarray(a).tobytes())
     assert h.hexdigest() == str(g["A_sha256"])
     assert np.array_equal(P.b, g["b"])
+
+
+# ---- fixed-order mode (the order libhgmres' parity mode follows) --------
+def _fsum_loops(p, ch=64):
+    """Plain-Python restatement of the fixed order (for checking R._fsum's numpy form)."""
+    def level(v):
+        out = []
+        for i in range(0, len(v), ch):
+            s = v[i]
+            for t in v[i + 1:i + ch]:
+                s = s + t
+            out.append(s)
+        return out
+    c = level([float(t) for t in p])
+    d = level(c)
+    s = d[0]
+    for t in d[1:]:
+        s = s + t
+    return s
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 4095, 4096, 4097, 70001])
+def test_fsum_matches_loop_form(n):
+    p = np.random.default_rng(n).standard_normal(n) * np.exp(np.random.default_rng(n + 1).uniform(-20, 20, n))
+    assert R._fsum(p) == _fsum_loops(p)
+    import math
+    assert abs(R._fsum(p) - math.fsum(p)) <= 1e-12 * np.sum(np.abs(p))
+
+
+def test_fixed_order_switches_only_the_summation_order(P64):
+    """Fixed-order solves agree with the default-order restatement to rounding (they are the
+    same algorithm), and the mode is scoped to the with-block."""
+    A, B, b, xt = P64.A, P64.B.tocsr(), P64.b, P64.x_true
+    o1 = R.hybrid_ab_gmres_rtp(A, B, b, xt, 0.0, 12, 1e-2, return_H=True)
+    with R.fixed_order():
+        assert R._FIXED
+        o2 = R.hybrid_ab_gmres_rtp(A, B, b, xt, 0.0, 12, 1e-2, return_H=True)
+        l2 = R.lsqr_solver(A, b, xt, 0.0, 6)
+    assert not R._FIXED
+    assert np.max(np.abs(o1[-1] - o2[-1])) <= 1e-12 * np.max(np.abs(o1[-1]))
+    assert rel(o1[0], o2[0]) < 1e-11
+    assert rel(R.lsqr_solver(A, b, xt, 0.0, 6)[0], l2[0]) < 1e-9
+
+
+def test_parallel_oracle_spmv_is_bitwise_scipy(P64):
+    """bench.py cpu_baseline's all-core leg: oracle/spmv_omp.c gives scipy's bits."""
+    from oracle import parallel as OP
+    OP.build()
+    A = P64.A.tocsr()
+    PA = OP.ParallelCSR(A)
+    rng = np.random.default_rng(0)
+    v, u = rng.standard_normal(A.shape[1]), rng.standard_normal(A.shape[0])
+    assert np.array_equal(PA @ v, A @ v)
+    assert np.array_equal(PA.T @ u, A.T @ u)
+    assert np.array_equal(R.lsqr_solver(PA, P64.b, P64.x_true, 0.0, 5)[0],
+                          R.lsqr_solver(A, P64.b, P64.x_true, 0.0, 5)[0])
