@@ -302,10 +302,16 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     pinned_ring(c, sizeof(double) * ring_n);
     const double* hr = c->hring;
     const bool poll = zc && c->num.ring_poll && !parity;
-    if (poll) {
+    if (zc) {
+        // the kernels store into the mapped ring with system-scope stores, and the pipeline
+        // events carry no system-scope release, so a store may land after its kernel's event
+        // has completed: the host spins on a sentinel for every entry it reads, with or without
+        // polling (an event wait then only saves the spinning)
         uint64_t* r = reinterpret_cast<uint64_t*>(c->hring);
         for (size_t i = 0; i < (size_t)maxit * LH; ++i) r[i] = RING_SENTINEL;
-        for (size_t i = offS; i < offS + 3; ++i) r[i] = RING_SENTINEL;
+        for (size_t i = offM; i < offM + 2 * (size_t)maxit; ++i) r[i] = RING_SENTINEL;
+        if (poll)
+            for (size_t i = offS; i < offS + 3; ++i) r[i] = RING_SENTINEL;
         for (size_t i = offQG; i < ring_n; ++i) r[i] = RING_SENTINEL;
     }
     T* dr = zc ? c->hring_dev : c->buf<T>("ring_dev", ring_n);
@@ -509,21 +515,36 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // reference's.  (Multi-GPU: both sequences share one stream, same semantics.)
     const int L = c->num.pipe_depth;                     // speculative steps in flight
     for (int j = 0; j <= L && j < maxit; ++j) enqueue_step(j);
+    // the mapped-ring entries of step kq (H column, Gram column, Gram error row)
+    auto wait_step = [&](int kq) {
+        std::vector<size_t> idx;
+        for (int i = 0; i < kq + 2; ++i) idx.push_back((size_t)kq * LH + i);
+        if (sp.proj == PROJ_ABRTP)
+            for (int i = 0; i < kq + 2; ++i) idx.push_back((size_t)kq * LH + (maxit + 2) + i);
+        if (gem)
+            for (int i = 0; i < kq + 2; ++i) idx.push_back(offQG + (size_t)kq * LQ + i);
+        ring_wait(c, hr, idx);
+    };
+    // the monitors of reconstruction R_kq (the error slot is not written when the Gram error
+    // monitor supplied the error)
+    auto wait_mon = [&](int kq) {
+        if (!zc) return;
+        std::vector<size_t> idx{offM + 2 * (size_t)kq};
+        if (gerr[kq] < 0) idx.push_back(offM + 2 * (size_t)kq + 1);
+        ring_wait(c, hr, idx, rs_stream);
+    };
     bool done = false;
     for (k = 0; k < maxit; ++k) {
-        if (k >= 1) pipe_wait(c);                        // R_{k-1}
+        if (k >= 1) {                                    // R_{k-1}
+            pipe_wait(c);
+            wait_mon(k - 1);
+        }
         if (poll) {
             // S_k: H(0:k+1,k) (+ Gram column k).  H(k+1,k) is written by a kernel that starts
             // after every kernel of step k has finished (the scale pass of step k, or with the
             // pending normalisation the A product of step k+1), so once it is visible Q(:,0:k)
             // and the kept products of step k, which R_k reads, are complete.
-            std::vector<size_t> idx;
-            for (int i = 0; i < k + 2; ++i) idx.push_back((size_t)k * LH + i);
-            if (sp.proj == PROJ_ABRTP)
-                for (int i = 0; i < k + 2; ++i) idx.push_back((size_t)k * LH + (maxit + 2) + i);
-            if (gem)
-                for (int i = 0; i < k + 2; ++i) idx.push_back(offQG + (size_t)k * LQ + i);
-            ring_wait(c, hr, idx);
+            wait_step(k);
             if (k == 0) {                                // the setup norms (written before step 0;
                                                          // with device inputs partly on the aux stream)
                 ring_wait(c, hr, {offS, offS + 1, offS + 2}, rs_stream);
@@ -534,6 +555,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             }
         } else {
             step_wait(c, k);                             // S_k: H(:,k) (+ Gram column k)
+            if (zc) wait_step(k);
         }
         if (k >= 1) {
             const double* mk = hr + offM + 2 * (size_t)(k - 1);
@@ -637,6 +659,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             pipe_wait(c);
         }
         k = maxit - 1;
+        wait_mon(k);
         const double* mk = hr + offM + 2 * (size_t)k;
         res[k] = std::sqrt(mk[0]) / nb;
         err[k] = gerr[k] >= 0 ? gerr[k] : std::sqrt(mk[1]) / nxt;

@@ -126,15 +126,181 @@ def _gram(M):
     return G
 
 
+# ---- the k x k kernels in the documented order (fixed-order mode) -------------------------
+# MATLAB's `\` is LAPACK (MKL), whose operation order is not specified either.  In
+# fixed-order mode the small dense solves follow one documented order: the unblocked
+# right-looking forms below (Cholesky R'R = M column by column, LU with partial pivoting,
+# Householder QR with column pivoting), each multiply and subtract rounded on its own.
+# libhgmres' host code (csrc/dense.cpp) runs the same loops.
+def _chol_solve_fixed(M, b):
+    n = len(b)
+    R = [[float(M[i, j]) for j in range(n)] for i in range(n)]
+    for j in range(n):
+        s = R[j][j]
+        for k in range(j):
+            s = s - R[k][j] * R[k][j]
+        if not s > 0:
+            return None
+        rjj = float(np.sqrt(s))
+        R[j][j] = rjj
+        for i in range(j + 1, n):
+            t = R[j][i]
+            for k in range(j):
+                t = t - R[k][j] * R[k][i]
+            R[j][i] = t / rjj
+    z = [float(v) for v in b]
+    for i in range(n):                       # R' z = b
+        t = z[i]
+        for k in range(i):
+            t = t - R[k][i] * z[k]
+        z[i] = t / R[i][i]
+    x = [0.0] * n
+    for i in range(n - 1, -1, -1):           # R x = z
+        t = z[i]
+        for k in range(i + 1, n):
+            t = t - R[i][k] * x[k]
+        x[i] = t / R[i][i]
+    return np.array(x)
+
+
+def _lu_solve_fixed(M, b):
+    n = len(b)
+    A = [[float(M[i, j]) for j in range(n)] for i in range(n)]
+    r = [float(v) for v in b]
+    for k in range(n):
+        p, best = k, abs(A[k][k])
+        for i in range(k + 1, n):
+            if abs(A[i][k]) > best:
+                best, p = abs(A[i][k]), i
+        if p != k:
+            A[k], A[p] = A[p], A[k]
+            r[k], r[p] = r[p], r[k]
+        piv = A[k][k]
+        for i in range(k + 1, n):
+            lik = A[i][k] / piv
+            A[i][k] = lik
+            for j in range(k + 1, n):
+                A[i][j] = A[i][j] - lik * A[k][j]
+            r[i] = r[i] - lik * r[k]
+    x = [0.0] * n
+    for i in range(n - 1, -1, -1):
+        t = r[i]
+        for j in range(i + 1, n):
+            t = t - A[i][j] * x[j]
+        x[i] = t / A[i][i]
+    return np.array(x)
+
+
+def _qr_ls_fixed(M, b):
+    m, n = M.shape
+    A = [[float(M[i, j]) for i in range(m)] for j in range(n)]   # columns
+    r = [float(v) for v in b]
+    piv = list(range(n))
+    cn = []
+    for j in range(n):
+        s = 0.0
+        for i in range(m):
+            s = s + A[j][i] * A[j][i]
+        cn.append(s)
+    kmax = min(m, n)
+    for k in range(kmax):
+        p = k
+        for j in range(k + 1, n):
+            if cn[j] > cn[p]:
+                p = j
+        if p != k:
+            A[k], A[p] = A[p], A[k]
+            piv[k], piv[p] = piv[p], piv[k]
+            cn[k], cn[p] = cn[p], cn[k]
+        alpha = 0.0
+        for i in range(k, m):
+            alpha = alpha + A[k][i] * A[k][i]
+        alpha = float(np.sqrt(alpha))
+        if alpha == 0:
+            continue
+        x0 = A[k][k]
+        beta = -alpha if x0 > 0 else alpha
+        v0 = x0 - beta
+        v = [1.0] + [A[k][i] / v0 for i in range(k + 1, m)]
+        tau = (beta - x0) / beta
+        A[k][k] = beta
+        for i in range(k + 1, m):
+            A[k][i] = 0.0
+        for j in range(k + 1, n):
+            s = 0.0
+            for i in range(k, m):
+                s = s + v[i - k] * A[j][i]
+            s = s * tau
+            for i in range(k, m):
+                A[j][i] = A[j][i] - s * v[i - k]
+        s = 0.0
+        for i in range(k, m):
+            s = s + v[i - k] * r[i]
+        s = s * tau
+        for i in range(k, m):
+            r[i] = r[i] - s * v[i - k]
+        for j in range(k + 1, n):
+            s = 0.0
+            for i in range(k + 1, m):
+                s = s + A[j][i] * A[j][i]
+            cn[j] = s
+    z = [0.0] * n
+    for i in range(kmax - 1, -1, -1):
+        t = r[i]
+        for j in range(i + 1, kmax):
+            t = t - A[j][i] * z[j]
+        d = A[i][i]
+        z[i] = t / d if d != 0 else 0.0
+    y = np.empty(n)
+    for j in range(n):
+        y[piv[j]] = z[j]
+    return y
+
+
+def _gram_small(Hk):
+    """``Hk'*Hk`` of a small dense matrix, each entry summed over the rows in order."""
+    r, k = Hk.shape
+    G = np.empty((k, k))
+    for i in range(k):
+        for j in range(k):
+            s = 0.0
+            for q in range(r):
+                s = s + float(Hk[q, i]) * float(Hk[q, j])
+            G[i, j] = s
+    return G
+
+
+def _matmul_small(X, Y):
+    """``X*Y`` of small dense matrices, each entry summed over the inner index in order."""
+    n, p = X.shape[0], Y.shape[1]
+    Z = np.empty((n, p))
+    for i in range(n):
+        for j in range(p):
+            s = 0.0
+            for q in range(X.shape[1]):
+                s = s + float(X[i, q]) * float(Y[q, j])
+            Z[i, j] = s
+    return Z
+
+
 def mldivide(M, rhs):
     """MATLAB ``M \\ rhs`` for the small dense systems the solvers form.
 
     Square + symmetric + positive diagonal -> Cholesky (falls back to LU when
     not positive definite); square otherwise -> LU; rectangular -> QR least
-    squares with column pivoting (LAPACK xGEQP3, as MATLAB)."""
+    squares with column pivoting (LAPACK xGEQP3, as MATLAB).  In fixed-order mode
+    the same three factorisations run in their documented loop order."""
     M = np.asarray(M, dtype=np.float64)
     rhs = np.asarray(rhs, dtype=np.float64)
     r, c = M.shape
+    if _FIXED:
+        if r != c:
+            return _qr_ls_fixed(M, rhs)
+        if np.array_equal(M, M.T) and np.all(np.diag(M) > 0):
+            x = _chol_solve_fixed(M, rhs)
+            if x is not None:
+                return x
+        return _lu_solve_fixed(M, rhs)
     if r == c:
         if np.array_equal(M, M.T) and np.all(np.diag(M) > 0):
             try:
@@ -429,13 +595,14 @@ def hybrid_lsmr_solver(A, b, x_true, tol, maxit, lam):
         Bk = B_k[: k + 2, : k + 1]               # :37
         alpha_k1 = alpha1                        # :38
         beta_k1 = beta_k                         # :39
-        G = Bk.T @ Bk
+        G = _gram_small(Bk) if _FIXED else Bk.T @ Bk
         E11 = np.zeros((k + 1, k + 1))
         E11[0, 0] = 1.0
-        LHS = G @ G + (alpha_k1 * beta_k1) ** 2 * E11 + lam * np.eye(k + 1)   # :41
+        GG = _matmul_small(G, G) if _FIXED else G @ G
+        LHS = GG + (alpha_k1 * beta_k1) ** 2 * E11 + lam * np.eye(k + 1)   # :41
         e1 = np.zeros(k + 1)
         e1[0] = 1.0
-        RHS = B_k[0, 0] * beta1 * (G @ e1)       # :42
+        RHS = B_k[0, 0] * beta1 * (G[:, 0].copy() if _FIXED else G @ e1)   # :42
         yk = mldivide(LHS, RHS)                  # :44
         x = _gemv(V[:, : k + 1], yk)             # :45
         error_norm[k] = _norm(x - x_true) / nxt  # :47
@@ -484,7 +651,10 @@ def _gmres_ptr(A, B, b, x_true, tol, maxit, lam, side, hybrid, explicit_BA=False
         tk = np.zeros(k + 2)
         tk[0] = beta
         if hybrid:
-            yk = mldivide(Hk.T @ Hk + lam * np.eye(k + 1), Hk.T @ tk)   # hybrid :34-36
+            if _FIXED:                           # tk = beta e1: Hk'*tk = beta Hk(1,:)'
+                yk = mldivide(_gram_small(Hk) + lam * np.eye(k + 1), Hk[0, :] * beta)   # hybrid :34-36
+            else:
+                yk = mldivide(Hk.T @ Hk + lam * np.eye(k + 1), Hk.T @ tk)   # hybrid :34-36
         else:
             yk = mldivide(Hk, tk)                # nonhybrid :35
         zk = _gemv(Q[:, : k + 1], yk)            # :37 / :36

@@ -275,3 +275,19 @@ def test_parallel_oracle_spmv_is_bitwise_scipy(P64):
     assert np.array_equal(PA.T @ u, A.T @ u)
     assert np.array_equal(R.lsqr_solver(PA, P64.b, P64.x_true, 0.0, 5)[0],
                           R.lsqr_solver(A, P64.b, P64.x_true, 0.0, 5)[0])
+
+
+def test_fixed_order_dense_kernels_match_lapack():
+    """The documented-order k x k solves of fixed_order() (mirrors of csrc/dense.cpp) solve
+    the same systems as LAPACK to rounding."""
+    rng = np.random.default_rng(4)
+    for n in (1, 5, 20):
+        X = rng.standard_normal((n + 1, n))
+        M = X.T @ X + 1e-2 * np.eye(n)
+        b = rng.standard_normal(n)
+        assert rel(R._chol_solve_fixed(M, b), np.linalg.solve(M, b)) < 1e-10
+        Mn = rng.standard_normal((n, n))
+        assert rel(R._lu_solve_fixed(Mn, b), np.linalg.solve(Mn, b)) < 1e-9
+        c = rng.standard_normal(n + 1)
+        assert rel(R._qr_ls_fixed(X, c), np.linalg.lstsq(X, c, rcond=None)[0]) < 1e-10
+    assert R._chol_solve_fixed(np.array([[1.0, 2.0], [2.0, 1.0]]), np.ones(2)) is None   # not PD
