@@ -332,7 +332,33 @@ def _mgs_arnoldi_step(Q, H, k, v, breakdown_tol=None):
     return False
 
 
-def hybrid_ba_gmres_rtp(A, B, b, x_true, tol, maxit, lam, return_H=False):
+def _cgs2_arnoldi_step(Q, H, k, v, breakdown_tol=None):
+    """Classical Gram-Schmidt applied twice in place of MGS (BASELINE configs[2]'s option; the
+    reference itself only has MGS, hybrid_ba_gmres_rtp.m:20-23): h1 = Q'v, v -= Q h1,
+    h2 = Q'v, v -= Q h2, H(1:k,k) = h1 + h2; normalisation and breakdown as :24-26."""
+    Qk = Q[:, : k + 1]
+    h1 = _tmat(Qk, v)
+    v = v - _gemv(Qk, h1)
+    h2 = _tmat(Qk, v)
+    v = v - _gemv(Qk, h2)
+    H[: k + 1, k] = h1 + h2
+    H[k + 1, k] = _norm(v)
+    if breakdown_tol is None:
+        if H[k + 1, k] == 0:
+            return True
+    elif H[k + 1, k] < breakdown_tol:
+        return True
+    Q[:, k + 1] = v / H[k + 1, k]
+    return False
+
+
+def _arnoldi_step(Q, H, k, v, breakdown_tol=None, orth="mgs"):
+    if orth == "cgs2":
+        return _cgs2_arnoldi_step(Q, H, k, v, breakdown_tol)
+    return _mgs_arnoldi_step(Q, H, k, v, breakdown_tol)
+
+
+def hybrid_ba_gmres_rtp(A, B, b, x_true, tol, maxit, lam, return_H=False, orth="mgs"):
     """``hybrid_ba_gmres_rtp.m:1-42``."""
     n = A.shape[1]                               # :3
     x = np.zeros(n)                              # :4
@@ -349,7 +375,7 @@ def hybrid_ba_gmres_rtp(A, B, b, x_true, tol, maxit, lam, return_H=False):
     k = 0
     for k in range(maxit):                       # :18
         v = M_reg(Q[:, k])                       # :19
-        if _mgs_arnoldi_step(Q, H, k, v):        # :20-26
+        if _arnoldi_step(Q, H, k, v, orth=orth): # :20-26
             break
         Hk = H[: k + 2, : k + 1]                 # :28
         rhs = np.zeros(k + 2)
@@ -692,7 +718,7 @@ def BAgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, explicit_
                       explicit_BA=explicit_BA, return_H=return_H)
 
 
-def arnoldi(A, B, b, k_gcv, gcv_type, breakdown_tol=1e-12):
+def arnoldi(A, B, b, k_gcv, gcv_type, breakdown_tol=1e-12, orth="mgs"):
     """Arnoldi part of ``gcv_function.m:3-33``: returns (H, beta) with H of
     size (k_gcv+1) x k_gcv (zero columns kept after a break, ``:33``)."""
     if gcv_type == "ab":
@@ -709,7 +735,7 @@ def arnoldi(A, B, b, k_gcv, gcv_type, breakdown_tol=1e-12):
     Q[:, 0] = r0 / beta                          # :15
     for k in range(k_gcv):                       # :18
         v = op(Q[:, k])
-        if _mgs_arnoldi_step(Q, H, k, v, breakdown_tol=breakdown_tol):   # :25-31
+        if _arnoldi_step(Q, H, k, v, breakdown_tol=breakdown_tol, orth=orth):   # :25-31
             break
     return H, beta
 

@@ -59,6 +59,16 @@ def main():
     res.update(lsqr_x=x, lsqr_res=r, lsqr_err=e)
     out_ = hgmres.ABgmres_hybrid_bounds(A_g, B_g, P.b, xt, 0.0, 12, 1e-2, ctx=ctx)
     res.update(abp_x=out_[0], abp_res=out_[2], abp_err=out_[1])
+    # configs[3]'s AB-GMRES (m-space Arnoldi, replicated basis, one all-reduce per A*(B*q))
+    out_ = hgmres.ABgmres_nonhybrid_bounds(A_g, B_g, P.b, xt, 0.0, 12, ctx=ctx, return_H=True)
+    res.update(abn_x=out_[0], abn_res=out_[2], abn_err=out_[1], abn_H=out_[-1])
+    x, e, r, k, H = hgmres.hybrid_ab_gmres_rtp(A_g, B_g, P.b, xt, 0.0, 12, 1e-2, ctx=ctx, return_H=True)
+    res.update(hab_x=x, hab_res=r, hab_err=e, hab_H=H)
+    # configs[4]: the Golub-Kahan path on fp32 shards
+    A32 = hgmres.SparseOperator.from_scipy(A_g, ctx, dtype=1)
+    B32 = hgmres.SparseOperator.from_scipy(B_g, ctx, dtype=1)
+    x, e, r, k = hgmres.lsqr_solver(A32, P.b, xt, 0.0, 4, ctx=ctx, At=B32)
+    res.update(lsqr32_x=x, lsqr32_res=r, lsqr32_err=e)
     np.savez(os.path.join(out, f"rank{rank}_of{world}.npz"), lo=lo, hi=hi, **res)
     if conn is not None:
         conn.close()

@@ -63,7 +63,30 @@ def dump(name, P, maxit, lam, tol=0.0, store_raw=True):
     print("wrote", name, {k: (v.shape if hasattr(v, "shape") else v) for k, v in d.items() if "sha" in k or k == "shape"})
 
 
+def dump_c3(name="c3_2048.npz", k=5):
+    """BASELINE configs[2] at full size (2048^2, 19 angles, nnz 1.01e8): BA-GMRES + GCV Arnoldi
+    with MGS (the reference's orthogonalisation, hybrid_ba_gmres_rtp.m:20-23) and with CGS2 (the
+    config's alternative), k steps.  The operator is pinned by its CSR hash (the device generator
+    reproduces it bitwise); x is stored as its norm plus every 997th entry."""
+    P = tomo_problem(2048, 19, noise=1e-2, seed=0, backprojector="matched")
+    A, B, b, xt = P.A, P.B.tocsr(), P.b, P.x_true
+    d = {"maxit": k, "lam": 1e-2, "N": 2048, "n_angles": 19, "A_sha256": csr_hash(A), "b": b,
+         "sample_stride": 997}
+    for orth in ("mgs", "cgs2"):
+        x, e, r, kk, H = R.hybrid_ba_gmres_rtp(A, B, b, xt, 0.0, k, 1e-2, return_H=True, orth=orth)
+        d.update({f"hba_{orth}_H": H, f"hba_{orth}_err": e, f"hba_{orth}_res": r, f"hba_{orth}_k": kk,
+                  f"hba_{orth}_xnorm": np.linalg.norm(x), f"hba_{orth}_xs": x[::997].copy()})
+        Hg, beta = R.arnoldi(A, B, b, k, "ba", orth=orth)
+        d.update({f"gcv_{orth}_H": Hg, f"gcv_{orth}_beta": beta})
+    np.savez_compressed(os.path.join(OUT, name), **d)
+    print("wrote", name, "MGS vs CGS2 |dH|/|H| =",
+          np.max(np.abs(d["hba_mgs_H"] - d["hba_cgs2_H"])) / np.max(np.abs(d["hba_mgs_H"])))
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["c3"]:
+        dump_c3()
+        sys.exit(0)
     # matched back-projector B = A^T (run_equivalence_plots.m:5 style), 24^2 phantom, 12 angles
     dump("tomo24_matched.npz", tomo_problem(24, 12, noise=1e-2, seed=0, backprojector="matched"), maxit=12, lam=1e-2)
     # unmatched pixel-driven back-projector (the reference's B != A^T setting)

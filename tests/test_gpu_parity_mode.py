@@ -180,3 +180,21 @@ def test_parity_mode_is_not_the_production_path(gpu_ctx):
     with R.fixed_order():
         ref = R.hybrid_ba_gmres_rtp(A, B, b, xt, 0.0, 20, 1e-2, return_H=True)
     assert float(np.max(np.abs(out[-1] - ref[-1])) / np.max(np.abs(ref[-1]))) < TOL
+
+
+@pytest.mark.parametrize("name", sorted(PROBLEMS))
+def test_parity_cgs2(pctx, name):
+    """CGS2 (BASELINE configs[2]'s orthogonalisation option) in parity mode against the
+    oracle's CGS2 restatement in the same fixed order: H, x and histories bit-identical."""
+    A, B, b, xt = PROBLEMS[name]
+    with R.fixed_order():
+        ref = R.hybrid_ba_gmres_rtp(A, B, b, xt, 0.0, 20, 1e-2, return_H=True, orth="cgs2")
+        Hr, br = R.arnoldi(A, B, b, 12, "ba", orth="cgs2")
+    out = hgmres.hybrid_ba_gmres_rtp(A, B, b, xt, 0.0, 20, 1e-2, ctx=pctx, return_H=True, orth="cgs2")
+    H, beta, kd = hgmres.arnoldi(A, B, b, 12, "ba", ctx=pctx, orth="cgs2")
+    _record(f"hba_cgs2/{name}", H=float(np.max(np.abs(out[-1] - ref[-1])) / np.max(np.abs(ref[-1]))),
+            H_bitwise=bool(np.array_equal(out[-1], ref[-1])), x=_rel_dev(out[0], ref[0]),
+            gcv_H_bitwise=bool(np.array_equal(H, Hr)))
+    assert np.array_equal(out[-1], ref[-1]) and np.array_equal(out[0], ref[0])
+    assert np.array_equal(out[1], ref[1]) and np.array_equal(out[2], ref[2])
+    assert np.array_equal(H, Hr) and beta == br
