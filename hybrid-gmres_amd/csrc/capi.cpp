@@ -653,13 +653,20 @@ HGM_API int hgm_mat_set_bands(hgm_ctx* c, hgm_mat* M, int64_t band_width, int gr
         HGM_HIP(hipSetDevice(c->device));
         set_bands(c, M, band_width == -1 ? auto_band_width(M) : band_width);
         if (group && M->nbands > 1) M->bgroup = group;
+        if (M->variant & SPMV_STREAM) build_page_index(c, M);
     });
     return HGM_OK;
 }
 
 HGM_API int hgm_mat_tune(hgm_mat* M, int variant, int group) {
-    if (!M || variant < 0 || variant > 15) return HGM_E_ARG;
+    if (!M || variant < 0 || variant > 31) return HGM_E_ARG;
     if (group != 0 && group != 4 && group != 8 && group != 16 && group != 32 && group != 64) return HGM_E_ARG;
+    if ((variant & SPMV_PAGED) && !M->pg_ptr) {   // page index on demand (over the current stream)
+        HGM_TRY(M->ctx, {
+            HGM_HIP(hipSetDevice(M->ctx->device));
+            build_page_index(M->ctx, M);
+        });
+    }
     M->variant = variant;
     if (group && (variant & SPMV_STREAM)) M->sgroup = M->bsgroup = group;   // lanes per segment reduction
     else if (group) M->group = group;

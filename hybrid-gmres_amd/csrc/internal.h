@@ -166,18 +166,39 @@ struct hgm_mat {
     int32_t* cfo = nullptr;      // rows as segments (nchunks+1)
     int32_t* bcfo = nullptr;     // (band,row) segments
     int sgroup = 8, bsgroup = 16;  // lanes per segment in the streaming reduction
+    // x-page index of the paged streaming kernel, built over the stream the
+    // SpMV reads (the banded copy when there is one): chunk k's entries gather from the distinct
+    // 128-B pages of x pg_ids[pg_ptr[k] .. pg_ptr[k+1]) (staged in LDS), and entry e from
+    // page-local position pg_lidx[e] = slot * (128 / sizeof value) + col % (128 / sizeof value).
+    // pg_ptr[k+1] == pg_ptr[k]: the chunk touches more pages than fit; it gathers through the
+    // 32-bit column indices instead.
+    int32_t* pg_ptr = nullptr;
+    int32_t* pg_ids = nullptr;
+    uint16_t* pg_lidx = nullptr;
 };
 
 namespace hgm {
 // SpMV kernel variants (bit flags): 16-byte paired loads, nontemporal val/col loads,
 // XCD-aware row-block order, nnz-balanced streaming (chunked) kernel.
-enum SpmvVariant { SPMV_VEC = 1, SPMV_NT = 2, SPMV_XCD = 4, SPMV_STREAM = 8 };
+enum SpmvVariant { SPMV_VEC = 1, SPMV_NT = 2, SPMV_XCD = 4, SPMV_STREAM = 8, SPMV_PAGED = 16 };
+
 // entries per streaming chunk (256 threads x 16): C4 sweep, 2048 -> 4096 took A from
 // 2.90 to 2.48 ms and B from 2.78 to 2.47 ms (profiles/r1_spmv_sweep_c4_sch.jsonl)
 #ifndef HGM_SCH
 #define HGM_SCH 4096
 #endif
 constexpr int SCH = HGM_SCH;
+// x pages per streaming chunk that the paged kernel stages in LDS (one 128-B line each).  The
+// chunk's product buffer (SCH values) is reused for them, extended to HGM_PG_MAX64 pages in fp64
+// (C4 A chunks touch 235 pages on average, up to 272: scripts/page_stats.py); fp32: 128 pages.
+#ifndef HGM_PG_MAX64
+#define HGM_PG_MAX64 256
+#endif
+constexpr int PG_BYTES = 128;
+template <typename T> constexpr int pg_max() { return sizeof(T) == 8 ? HGM_PG_MAX64 : SCH * (int)sizeof(T) / PG_BYTES; }
+template <typename T> constexpr int stream_lds_bytes(bool paged) {
+    return paged && pg_max<T>() * PG_BYTES > SCH * (int)sizeof(T) ? pg_max<T>() * PG_BYTES : SCH * (int)sizeof(T);
+}
 
 struct SegIndex {
     int64_t nnz, nseg, nchunks;
@@ -320,6 +341,9 @@ hgm_mat* row_slice(hgm_ctx* c, const hgm_mat* M, int64_t lo, int64_t hi);
 void set_bands(hgm_ctx* c, hgm_mat* M, int64_t band_w);
 // chunk index of the nnz-balanced streaming kernel over the rows
 void build_stream_index(hgm_ctx* c, hgm_mat* M);
+// x-page index of the paged streaming kernel (over the banded copy when M has bands)
+void build_page_index(hgm_ctx* c, hgm_mat* M);
+void free_page_index(hgm_mat* M);
 // everything a freshly created operator gets: automatic bands + streaming index
 void finalize_operator(hgm_ctx* c, hgm_mat* M);
 int64_t auto_band_width(const hgm_mat* M);

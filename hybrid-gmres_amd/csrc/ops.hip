@@ -5,6 +5,7 @@
 //    hgmres/problems.py so the two generators agree bit for bit).
 #include <hipcub/hipcub.hpp>
 
+#include <climits>
 #include <cmath>
 #include <cstdlib>
 
@@ -104,6 +105,123 @@ void build_stream_index(hgm_ctx* c, hgm_mat* M) {
     HGM_HIP(hipStreamSynchronize(c->stream));
 }
 
+// --------------------------------------------------------------------------
+// x-page index of the paged streaming kernel (spmv.hip).  One 256-thread block per chunk of
+// SCH entries: block radix sort of (page, position) pairs, head flags, block scan -> slots.
+// Pass 0 counts the distinct pages (0 when more than PG_MAX: the chunk keeps the 32-bit
+// gathers); pass 1 writes the page list and the page-local 16-bit indices.
+// --------------------------------------------------------------------------
+template <int PGV, int PGMAX, bool FILL>
+__global__ __launch_bounds__(256) void k_page_index(int64_t nnz, const int32_t* __restrict__ ci,
+                                                    int32_t* __restrict__ cnt, const int32_t* __restrict__ pptr,
+                                                    int32_t* __restrict__ pids, uint16_t* __restrict__ lidx) {
+    constexpr int IPT = SCH / 256;
+    using Sort = hipcub::BlockRadixSort<int, 256, IPT, int>;
+    using Scan = hipcub::BlockScan<int, 256>;
+    __shared__ typename Sort::TempStorage ts;
+    __shared__ typename Scan::TempStorage tsc;
+    __shared__ int last_key[256];
+    const int64_t k = blockIdx.x, c0 = k * SCH;
+    int keys[IPT], vals[IPT];
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+        const int pos = threadIdx.x * IPT + i;
+        const int64_t e = c0 + pos;
+        if (e < nnz) {
+            const int col = ci[e];
+            keys[i] = col / PGV;
+            vals[i] = (pos << 6) | (col % PGV);
+        } else {
+            keys[i] = INT_MAX;
+            vals[i] = -1;
+        }
+    }
+    Sort(ts).Sort(keys, vals);            // blocked: thread t holds sorted items [IPT t, IPT t + IPT)
+    last_key[threadIdx.x] = keys[IPT - 1];
+    __syncthreads();
+    int flag[IPT], heads = 0;
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+        const int prev = i > 0 ? keys[i - 1] : (threadIdx.x > 0 ? last_key[threadIdx.x - 1] : -1);
+        flag[i] = (keys[i] != INT_MAX && keys[i] != prev) ? 1 : 0;
+        heads += flag[i];
+    }
+    int excl = 0, total = 0;
+    Scan(tsc).ExclusiveSum(heads, excl, total);
+    const bool fits = total <= PGMAX && c0 + SCH <= nnz;   // full chunks only
+    if (!FILL) {
+        if (threadIdx.x == 0) cnt[k] = fits ? total : 0;
+        return;
+    }
+    if (!fits) return;
+    int slot = excl - 1;
+    const int base = pptr[k];
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+        if (keys[i] == INT_MAX) continue;
+        if (flag[i]) {
+            ++slot;
+            pids[base + slot] = keys[i];
+        }
+        lidx[c0 + (vals[i] >> 6)] = (uint16_t)(slot * PGV + (vals[i] & 63));
+    }
+}
+
+void free_page_index(hgm_mat* M) {
+    if (M->pg_ptr) (void)hipFree(M->pg_ptr);
+    if (M->pg_ids) (void)hipFree(M->pg_ids);
+    if (M->pg_lidx) (void)hipFree(M->pg_lidx);
+    M->pg_ptr = M->pg_ids = nullptr;
+    M->pg_lidx = nullptr;
+    M->variant &= ~SPMV_PAGED;
+}
+
+template <int PGV, int PGMAX>
+static void build_page_index_t(hgm_ctx* c, hgm_mat* M) {
+    const bool banded = M->nbands > 1;
+    const int32_t* ci = banded ? M->bci : M->ci;
+    const int64_t nch = stream_chunks(M->nnz);
+    hipStream_t st = c->stream;
+    int32_t* cnt = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    try {
+        HGM_HIP(hipMalloc(&cnt, sizeof(int32_t) * (nch + 1)));
+        HGM_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (nch + 1), st));
+        HGM_HIP(hipMalloc(&M->pg_ptr, sizeof(int32_t) * (nch + 1)));
+        k_page_index<PGV, PGMAX, false><<<(unsigned)nch, 256, 0, st>>>(M->nnz, ci, cnt, nullptr, nullptr, nullptr);
+        HGM_HIP(hipGetLastError());
+        HGM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, M->pg_ptr, (int)(nch + 1), st));
+        HGM_HIP(hipMalloc(&tmp, tmp_bytes));
+        HGM_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, M->pg_ptr, (int)(nch + 1), st));
+        int32_t total = 0;
+        HGM_HIP(hipMemcpyAsync(&total, M->pg_ptr + nch, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        HGM_HIP(hipStreamSynchronize(st));
+        HGM_HIP(hipMalloc(&M->pg_ids, sizeof(int32_t) * (total > 0 ? total : 1)));
+        HGM_HIP(hipMalloc(&M->pg_lidx, sizeof(uint16_t) * M->nnz));
+        k_page_index<PGV, PGMAX, true><<<(unsigned)nch, 256, 0, st>>>(M->nnz, ci, nullptr, M->pg_ptr, M->pg_ids,
+                                                                     M->pg_lidx);
+        HGM_HIP(hipGetLastError());
+        HGM_HIP(hipStreamSynchronize(st));
+    } catch (...) {
+        (void)hipFree(cnt);
+        (void)hipFree(tmp);
+        free_page_index(M);
+        throw;
+    }
+    (void)hipFree(cnt);
+    (void)hipFree(tmp);
+}
+
+void build_page_index(hgm_ctx* c, hgm_mat* M) {
+    free_page_index(M);
+    HGM_REQUIRE(stream_chunks(M->nnz) < (int64_t)INT32_MAX, "page index: too many chunks");
+    if (M->nnz < SCH) return;
+    if (M->dtype == HGM_F32) build_page_index_t<PG_BYTES / 4, pg_max<float>()>(c, M);
+    else build_page_index_t<PG_BYTES / 8, pg_max<double>()>(c, M);
+    M->variant |= SPMV_PAGED;
+}
+
 static void free_bands(hgm_mat* M) {
     if (M->bcfo) (void)hipFree(M->bcfo);
     M->bcfo = nullptr;
@@ -119,6 +237,7 @@ static void free_bands(hgm_mat* M) {
 
 void mat_free(hgm_mat* M) {
     if (!M) return;
+    free_page_index(M);
     free_bands(M);
     if (M->ci16) (void)hipFree(M->ci16);
     if (M->cfo) (void)hipFree(M->cfo);
@@ -201,6 +320,8 @@ void finalize_operator(hgm_ctx* c, hgm_mat* M) {
             M->group = avg >= 6 ? 8 : 4;
         }
     }
+    // streaming operators gather x through LDS-staged pages
+    if (M->variant & SPMV_STREAM) build_page_index(c, M);
 }
 
 int64_t auto_band_width(const hgm_mat* M) {
@@ -215,6 +336,7 @@ int64_t auto_band_width(const hgm_mat* M) {
 }
 
 void set_bands(hgm_ctx* c, hgm_mat* M, int64_t W) {
+    free_page_index(M);   // it indexes the stream the bands replace; the caller rebuilds it
     free_bands(M);
     if (W <= 0 || W >= M->cols || M->nnz == 0) return;
     const int64_t nb = (M->cols + W - 1) / W;

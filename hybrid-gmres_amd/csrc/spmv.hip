@@ -188,17 +188,51 @@ __global__ __launch_bounds__(BS) void k_spmv_band(int64_t rows, int nbands, cons
 // partial in tail[k] and every later chunk's share in head[j]; k_stream_fixup adds them
 // in chunk order.  Fixed chunking => fixed summation order => bitwise reproducible.
 // ------------------------------------------------------------------------------
-template <typename T, int G, int EPI, bool NT, typename IX = int32_t>
+// Paged x gathers (SPMV_PAGED, hgm_mat::pg_*).  PMC at C4 (profiles/r2_pmc_spmv/): with one
+// global gather per entry the A and B stream kernels make ~1 L1 tag lookup per entry and keep
+// the TA 80-90 % busy -- the address path, not HBM, bounds them (420 G entries/s in fp64 and
+// only 500 G/s in fp32 on a third fewer bytes).  A 4096-entry chunk touches 87 (B) / 235 (A)
+// distinct 128-B lines of x on average (scripts/page_stats.py), so the chunk stages those pages
+// in LDS with coalesced 16-B loads and gathers from LDS through 16-bit page-local indices:
+// ~L1 lookups per chunk drop from ~4096 to the page count and the index stream from 4 to 2
+// bytes per entry.  Products and summation order are unchanged (same bits as the unpaged kernel).
+template <typename T>
+struct Paged {
+    const int32_t* pptr = nullptr;
+    const int32_t* pids = nullptr;
+    const uint16_t* lidx = nullptr;
+    int64_t xlen = 0;
+};
+
+// 16 bytes of page `pid` for lane `pl` of the page's loaders, zero past the end of x
+template <typename V16, typename T>
+__device__ __forceinline__ V16 load_page16(const T* __restrict__ x, int64_t pid, int pl, int64_t xlen) {
+    constexpr int PGV = PG_BYTES / (int)sizeof(T), VE = 16 / (int)sizeof(T);
+    const int64_t e0 = pid * PGV + (int64_t)pl * VE;
+    if (e0 + VE <= xlen) return *reinterpret_cast<const V16*>(x + e0);
+    V16 v;
+    const T* vp = reinterpret_cast<const T*>(&v);
+    T tmp[VE];
+#pragma unroll
+    for (int i = 0; i < VE; ++i) tmp[i] = e0 + i < xlen ? x[e0 + i] : T(0);
+    (void)vp;
+    __builtin_memcpy(&v, tmp, 16);
+    return v;
+}
+
+template <typename T, int G, int EPI, bool NT, typename IX = int32_t, bool PG = false>
 __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, const int64_t* __restrict__ sp,
                                                     const int32_t* __restrict__ fo, const IX* __restrict__ ci,
                                                     const T* __restrict__ val, const T* __restrict__ x,
                                                     T* __restrict__ out, T a, const T* __restrict__ z,
-                                                    T* __restrict__ head, T* __restrict__ tail, PendNorm<T> pn) {
+                                                    T* __restrict__ head, T* __restrict__ tail, PendNorm<T> pn,
+                                                    Paged<T> pg) {
     static_assert(EPI != EPI_DIVH, "EPI_DIVH is applied by the band reduction or the row kernel");
     using T2 = typename NV2<T>::t;
     using IV2 = std::conditional_t<sizeof(IX) == 2, nus2, ni2>;   // index pair / quad of the type
     using IV4 = std::conditional_t<sizeof(IX) == 2, nus4, ni4>;
-    __shared__ T prod[SCH];
+    __shared__ __attribute__((aligned(16))) unsigned char smem[stream_lds_bytes<T>(PG)];
+    T* prod = reinterpret_cast<T*>(smem);
     const int64_t k = blockIdx.x;
     const int64_t c0 = k * SCH;
     const int64_t c1 = (c0 + SCH < nnz) ? c0 + SCH : nnz;
@@ -221,7 +255,63 @@ __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, c
         p0 = q <= nseg ? sp[q] : 0;
         p1 = q + 1 <= nseg ? sp[q + 1] : 0;
     };
-    if (n == SCH && sizeof(T) == 4) {
+    bool staged = false;
+    if constexpr (PG) {
+        // ---- paged gathers: x pages -> LDS (prod[] doubles as the page buffer), then products ----
+        const int pp0 = pg.pptr[k];
+        const int npg = n == SCH ? pg.pptr[k + 1] - pp0 : 0;      // 0: gather through ci (below)
+        if (npg > 0) {
+            constexpr int LPP = PG_BYTES / 16;                       // lanes per page, 16 B each
+            constexpr int PPP = BS / LPP;                            // pages per pass
+            constexpr int NPASS = (pg_max<T>() + PPP - 1) / PPP;
+            using V16 = std::conditional_t<sizeof(T) == 8, nd2, nf4>;
+            using VV = std::conditional_t<sizeof(T) == 8, nd2, nf4>;        // values per lane per step
+            using LV = std::conditional_t<sizeof(T) == 8, nus2, nus4>;      // their page-local indices
+            constexpr int VE = 16 / (int)sizeof(T);                  // entries per lane per step
+            constexpr int U = SCH / (VE * BS);
+            const int pl = threadIdx.x % LPP, ps = threadIdx.x / LPP;
+            VV vv[U];
+            LV lc[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int j = VE * threadIdx.x + u * VE * BS;
+                vv[u] = ld<NT>(reinterpret_cast<const VV*>(val + c0 + j));
+                lc[u] = ld<NT>(reinterpret_cast<const LV*>(pg.lidx + c0 + j));
+            }
+            int pid[NPASS];
+#pragma unroll
+            for (int i = 0; i < NPASS; ++i) {
+                const int sl = ps + i * PPP;
+                pid[i] = sl < npg ? pg.pids[pp0 + sl] : -1;
+            }
+            V16 pv[NPASS];
+#pragma unroll
+            for (int i = 0; i < NPASS; ++i)
+                if (pid[i] >= 0) pv[i] = load_page16<V16>(x, pid[i], pl, pg.xlen);
+            __builtin_amdgcn_sched_barrier(0);
+            bookkeeping();
+            __builtin_amdgcn_sched_barrier(0);
+            V16* pages = reinterpret_cast<V16*>(prod);
+#pragma unroll
+            for (int i = 0; i < NPASS; ++i)
+                if (pid[i] >= 0) pages[(ps + i * PPP) * LPP + pl] = pv[i];
+            __syncthreads();
+            T pr[U * VE];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int e = 0; e < VE; ++e) pr[u * VE + e] = vv[u][e] * prod[lc[u][e]];
+            __syncthreads();                                          // pages no longer read
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int e = 0; e < VE; ++e) prod[VE * threadIdx.x + u * VE * BS + e] = pr[u * VE + e];
+            staged = true;
+        }
+    }
+    if (staged) {
+        // products are in prod[]
+    } else if (n == SCH && sizeof(T) == 4) {
         // fp32: four entries per lane per step (16-B value and 16-B index loads, both fully
         // coalesced across the wave)
         constexpr int U = SCH / (4 * BS);
@@ -394,15 +484,24 @@ __global__ __launch_bounds__(BS) void k_epi(int64_t n, T* __restrict__ y, T a, c
 // ------------------------------------------------------------------------------
 template <typename T, int G, int EPI, bool NT, typename IX>
 static void launch_stream_e(hgm_ctx* c, bool last, const SegIndex& si, const IX* ci, const T* val, const T* x,
-                            T* out, T a, const T* z, T* head, T* tail, const PendNorm<T>& pn) {
+                            T* out, T a, const T* z, T* head, T* tail, const PendNorm<T>& pn, const Paged<T>& pg) {
     if (si.nnz == 0) {
         int64_t g = (si.nseg + BS - 1) / BS;
         if (g > 4096) g = 4096;
         if (g > 0) launch(c, last, k_fill_epi<T, EPI>, dim3(g), dim3(BS), si.nseg, out, a, z);
         return;
     }
-    launch(c, false, k_spmv_stream<T, G, EPI, NT, IX>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg, si.sp, si.fo, ci,
-           val, x, out, a, z, head, tail, pn);
+    if constexpr (std::is_same<IX, int32_t>::value) {
+        if (pg.pptr)
+            launch(c, false, k_spmv_stream<T, G, EPI, NT, IX, true>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg,
+                   si.sp, si.fo, ci, val, x, out, a, z, head, tail, pn, pg);
+        else
+            launch(c, false, k_spmv_stream<T, G, EPI, NT, IX, false>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg,
+                   si.sp, si.fo, ci, val, x, out, a, z, head, tail, pn, pg);
+    } else {
+        launch(c, false, k_spmv_stream<T, G, EPI, NT, IX, false>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg, si.sp,
+               si.fo, ci, val, x, out, a, z, head, tail, pn, pg);
+    }
     int64_t g = (si.nchunks + BS - 1) / BS;
     if (g > 4096) g = 4096;
     launch(c, last, k_stream_fixup<T, EPI>, dim3(g), dim3(BS), si.nnz, si.nchunks, si.sp, si.fo, out, a, z,
@@ -411,24 +510,26 @@ static void launch_stream_e(hgm_ctx* c, bool last, const SegIndex& si, const IX*
 
 template <typename T, int G, bool NT, typename IX>
 static void launch_stream_g(hgm_ctx* c, bool last, const SegIndex& si, const IX* ci, const T* val, const T* x,
-                            T* out, int epi, T a, const T* z, T* head, T* tail, const PendNorm<T>& pn) {
+                            T* out, int epi, T a, const T* z, T* head, T* tail, const PendNorm<T>& pn,
+                            const Paged<T>& pg) {
     switch (epi) {
-        case EPI_NONE: launch_stream_e<T, G, EPI_NONE, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn); break;
-        case EPI_ADD: launch_stream_e<T, G, EPI_ADD, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn); break;
-        case EPI_SUB: launch_stream_e<T, G, EPI_SUB, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn); break;
-        case EPI_ADDQ: launch_stream_e<T, G, EPI_ADDQ, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn); break;
-        default: launch_stream_e<T, G, EPI_RSUB, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn); break;
+        case EPI_NONE: launch_stream_e<T, G, EPI_NONE, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
+        case EPI_ADD: launch_stream_e<T, G, EPI_ADD, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
+        case EPI_SUB: launch_stream_e<T, G, EPI_SUB, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
+        case EPI_ADDQ: launch_stream_e<T, G, EPI_ADDQ, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
+        default: launch_stream_e<T, G, EPI_RSUB, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
     }
 }
 
 template <typename T, typename IX = int32_t>
 static void spmv_stream(hgm_ctx* c, bool last, const SegIndex& si, int G, bool nt, const IX* ci, const T* val,
-                        const T* x, T* out, int epi, T a, const T* z, const PendNorm<T>& pn = PendNorm<T>{}) {
+                        const T* x, T* out, int epi, T a, const T* z, const PendNorm<T>& pn = PendNorm<T>{},
+                        const Paged<T>& pg = Paged<T>{}) {
     T* head = c->buf<T>("stream_head", si.nchunks + 1);
     T* tail = c->buf<T>("stream_tail", si.nchunks + 1);
-#define HGM_SG(GG)                                                                                  \
-    if (nt) launch_stream_g<T, GG, true, IX>(c, last, si, ci, val, x, out, epi, a, z, head, tail, pn);  \
-    else launch_stream_g<T, GG, false, IX>(c, last, si, ci, val, x, out, epi, a, z, head, tail, pn);
+#define HGM_SG(GG)                                                                                      \
+    if (nt) launch_stream_g<T, GG, true, IX>(c, last, si, ci, val, x, out, epi, a, z, head, tail, pn, pg);  \
+    else launch_stream_g<T, GG, false, IX>(c, last, si, ci, val, x, out, epi, a, z, head, tail, pn, pg);
     switch (G) {
         case 64: HGM_SG(64) break;
         case 32: HGM_SG(32) break;
@@ -556,11 +657,19 @@ template <typename T>
 static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z,
                           const PendNorm<T>& pn) {
     const bool nt = M->variant & SPMV_NT;
+    // paged x gathers need the page index and a 16-B aligned x (vector page loads)
+    Paged<T> pg;
+    if ((M->variant & SPMV_PAGED) && M->pg_ptr && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+        pg.pptr = M->pg_ptr;
+        pg.pids = M->pg_ids;
+        pg.lidx = M->pg_lidx;
+        pg.xlen = M->cols;
+    }
     if (M->nbands > 1) {
         T* yp = c->buf<T>("band_part", (size_t)M->nbands * M->rows + 1);
         SegIndex si{M->nnz, (int64_t)M->nbands * M->rows, stream_chunks(M->nnz), M->brp, M->bcfo};
         spmv_stream<T>(c, false, si, M->bsgroup, nt, M->bci, reinterpret_cast<const T*>(M->bval), x, yp, EPI_NONE,
-                       T(0), nullptr);
+                       T(0), nullptr, PendNorm<T>{}, pg);
         band_reduce<T>(c, M, yp, y, epi, a, z, pn);
     } else {
         SegIndex si{M->nnz, M->rows, stream_chunks(M->nnz), M->rp, M->cfo};
@@ -568,7 +677,8 @@ static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int ep
             spmv_stream<T, uint16_t>(c, true, si, M->sgroup, nt, M->ci16, reinterpret_cast<const T*>(M->val), x, y,
                                      epi, a, z, pn);
         else
-            spmv_stream<T>(c, true, si, M->sgroup, nt, M->ci, reinterpret_cast<const T*>(M->val), x, y, epi, a, z, pn);
+            spmv_stream<T>(c, true, si, M->sgroup, nt, M->ci, reinterpret_cast<const T*>(M->val), x, y, epi, a, z, pn,
+                           pg);
     }
 }
 
@@ -610,6 +720,8 @@ void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T*
     // algorithmic bytes: nnz*(s+4) + 8(rows+1) + s*cols + s*rows (+ s*rows epilogue operand)
     const double s = sizeof(T);
     // 16-bit indices read (row kernel without paired loads, or the unbanded streaming kernel)
+    // (the paged kernel also reads 2-byte indices, plus its page lists; the roofline keeps
+    // SURVEY.md §8(d)'s 4-byte CSR definition of the work and reports the physical bytes as traffic)
     const bool narrow = M->ci16 && ((rowk && !nrm && !(M->variant & SPMV_VEC)) || (stream && M->nbands <= 1));
     double bytes = (double)M->nnz * (s + (narrow ? 2 : 4)) + 8.0 * (M->rows + 1) + s * M->cols + s * M->rows;
     if (epi != EPI_NONE && epi != EPI_DIVH) bytes += s * M->rows;   // epilogue operand read

@@ -176,7 +176,9 @@ HGM_API int hgm_mat_order(const hgm_mat* mat, int which, int* N, int* tile, int*
 HGM_API int hgm_mat_info(const hgm_mat* mat, int64_t* rows, int64_t* cols, int64_t* nnz, int* dtype);
 /* SpMV kernel selection for this operator (tuning/benchmark hook): variant bits
  * 1 = 16-byte paired loads, 2 = nontemporal val/col loads, 4 = XCD-aware row-block
- * order, 8 = nnz-balanced streaming kernel (2048-entry chunks, LDS-staged products);
+ * order, 8 = nnz-balanced streaming kernel (4096-entry chunks, LDS-staged products),
+ * 16 = with the streaming kernel, gather x through LDS-staged 128-B pages (the operator's page
+ * index; streaming operators are created with it);
  * group = lanes per row, or per segment reduction with bit 8 (4, 8, 16, 32 or 64;
  * 0 keeps the current choice). */
 HGM_API int hgm_mat_tune(hgm_mat* mat, int variant, int group);

@@ -188,6 +188,40 @@ def test_stream_spmv(gpu_ctx, P64, variant, group):
     hist_ok(r, rr, TOL)
 
 
+@pytest.mark.parametrize("group", [4, 8, 32])
+@pytest.mark.parametrize("dtype", [0, 1])
+def test_paged_stream_spmv_bitwise(gpu_ctx, P64, group, dtype):
+    """Paged x gathers (variant bit 16: the chunk's x pages staged in LDS, 16-bit page-local
+    indices) give exactly the unpaged streaming kernel's bits -- plain and banded, fp64 and
+    fp32, every epilogue through a solve -- on the tomography operators and a ragged matrix
+    (empty rows, rows spanning several chunks, a final partial chunk)."""
+    rng = np.random.default_rng(11)
+    for M in (P64.A, P64.B, _ragged_matrix()):
+        Mo = hgmres.SparseOperator.from_scipy(M, gpu_ctx, dtype=dtype)
+        x = rng.standard_normal(M.shape[1])
+        for bands in ((0,) if M.shape[1] <= 2000 else (0, M.shape[1] // 5 + 1)):
+            if bands:
+                Mo.set_bands(bands, 0)
+            Mo.tune(8 | 2, group)
+            y0 = Mo @ x
+            Mo.tune(8 | 2 | 16, group)
+            y1 = Mo @ x
+            assert np.array_equal(y0, y1), (M.shape, bands, dtype)
+    if dtype == 0:
+        Ao = hgmres.SparseOperator.from_scipy(P64.A, gpu_ctx)
+        Bo = hgmres.SparseOperator.from_scipy(P64.B, gpu_ctx)
+        outs = []
+        for v in (8 | 2, 8 | 2 | 16):
+            Ao.tune(v, group)
+            Bo.tune(v, group)
+            outs.append(hgmres.hybrid_ab_gmres_rtp(Ao, Bo, P64.b, P64.x_true, 0.0, 12, 1e-2, ctx=gpu_ctx,
+                                                   return_H=True))
+            outs.append(hgmres.lsqr_solver(Ao, P64.b, P64.x_true, 0.0, 8, ctx=gpu_ctx, At=Bo))
+        for a_, b_ in zip(outs[:2], outs[2:]):
+            for u, w in zip(a_, b_):
+                assert np.array_equal(np.asarray(u), np.asarray(w))
+
+
 @pytest.mark.parametrize("width,group", [(512, 8), (1000, 16), (1 << 11, 32), (333, 64)])
 def test_banded_spmv(gpu_ctx, P64, width, group):
     """Column-banded A (cache-blocked x gather) equals the plain CSR product; bands are
