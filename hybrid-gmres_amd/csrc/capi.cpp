@@ -38,6 +38,11 @@ int hybrid_lsmr(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* 
                 double* res_out, int* niters);
 int arnoldi(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b_in, int kg, int side, double btol,
             int orth, double* H_out, double* beta_out, int* kdone);
+// bounds.cpp
+int gmres_bounds_filter(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* B, const double* b,
+                        const double* xt, double tol, int maxit, double lambda, int side, int hybrid,
+                        const hgm_mat* dML, const hgm_mat* dMR, int ritz_steps, double* x_out, double* err_out,
+                        double* res_out, int* niters, double* phi, double* dphi, double* mu_out, double* ritz_res);
 
 enum { PROJ_LS = 0, PROJ_PTR = 1, PROJ_ABRTP = 2 };
 
@@ -914,6 +919,44 @@ HGM_API int hgm_gcv_fminbnd(const double* H, int k, double beta, double trace_m,
     if (!H || k < 1 || !lambda_opt || !(hi > lo)) return HGM_E_ARG;
     *lambda_opt = dense::gcv_fminbnd(H, k, beta, trace_m, lo, hi, tolx, gcv_opt);
     return HGM_OK;
+}
+
+HGM_API int hgm_gmres_bounds_filter(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* B,
+                                    const double* b, const double* xt, double tol, int maxit, double lambda,
+                                    int side, int hybrid, const hgm_mat* dM_left, const hgm_mat* dM_right,
+                                    int ritz_steps, double* x, double* err, double* res, int* niters,
+                                    double* phi_iter, double* dphi_iter, double* mu, double* ritz_resid) {
+    if (side != HGM_SIDE_AB && side != HGM_SIDE_BA) return HGM_E_ARG;
+    HGM_SOLVE(c, gmres_bounds_filter(c, o, A, B, b, xt, tol, maxit, lambda, side, hybrid, dM_left, dM_right,
+                                     ritz_steps, x, err, res, niters, phi_iter, dphi_iter, mu, ritz_resid));
+}
+
+HGM_API int hgm_filter_factors(const double* H, int ldh, int k, const double* dK, int lddk, const double* mu,
+                               const double* dmu, double lambda, int side, int hybrid, double* phi, double* dphi) {
+    if (!H || !dK || !mu || !dmu || !phi || !dphi || k < 1 || ldh < k + 1 || lddk < k) return HGM_E_ARG;
+    if (side != HGM_SIDE_AB && side != HGM_SIDE_BA) return HGM_E_ARG;
+    try {
+        dense::filter_factors(H, ldh, k, dK, lddk, mu, dmu, lambda, side, hybrid, phi, dphi);
+    } catch (const Error& e) {
+        return e.code;
+    }
+    return HGM_OK;
+}
+
+HGM_API int hgm_ritz(const double* Hp, int ldh, int p, double h_next, const double* G, int ldg, int nev, double* mu,
+                     double* dmu, double* resid) {
+    if (!Hp || !G || !mu || !dmu || p < 1 || nev < 1 || nev > p || ldh < p || ldg < p) return HGM_E_ARG;
+    try {
+        dense::ritz(Hp, ldh, p, h_next, G, ldg, nev, mu, dmu, resid);
+    } catch (const Error& e) {
+        return e.code;
+    }
+    return HGM_OK;
+}
+
+HGM_API int hgm_eig(int n, const double* A, double* wr, double* wi, double* V) {
+    if (n < 1 || !A || !wr || !wi) return HGM_E_ARG;
+    return dense::eig_general(n, A, wr, wi, V) ? HGM_OK : HGM_E_ARG;
 }
 
 HGM_API int hgm_kernel_timing(hgm_ctx* c, int enable) {

@@ -316,6 +316,8 @@ void lsmr_monitor(hgm_ctx* c, int64_t n, const T* p1, const T* p0, double c1, do
 // out[i] = epi(in[i], a, z[i]) (out may alias z): the epilogue of an SpMV applied to its raw product
 template <typename T> void epilogue_to(hgm_ctx* c, int64_t n, const T* in, T* out, int epi, T a, const T* z);
 template <typename T> void fill(hgm_ctx* c, int64_t n, T* x, T v);
+// x_i = deterministic pseudo-random value in (-1, 1) (splitmix64 of seed + i)
+template <typename T> void fill_hash(hgm_ctx* c, int64_t n, T* x, uint64_t seed);
 template <typename T> void convert(hgm_ctx* c, int64_t n, const double* in, T* out);
 template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, double* out);
 template <typename T> void fro2(hgm_ctx* c, const hgm_mat* M, double* out_dev);
@@ -419,6 +421,17 @@ double gcv_from_H(const double* H, int ldh, int k, double beta, double lambda, d
 // MATLAB fminbnd (Brent / Forsythe-Malcolm-Moler fmin) of gcv_from_H over [lo, hi].
 double gcv_fminbnd(const double* H, int k, double beta, double trace_m, double lo, double hi,
                    double tolx, double* gopt);
+// spectral.cpp: MATLAB eig of a real n x n (col-major) matrix: eigenvalues wr + i wi, unit 2-norm
+// eigenvectors in the LAPACK dgeev layout (V may be NULL).  false: no convergence.
+bool eig_general(int n, const double* A, double* wr, double* wi, double* V);
+// phi / dphi of iteration k of the *_bounds.m files (H: (k+1) x k leading part, ldh; dK = Qk' DeltaM Qk;
+// mu / dmu: the k leading eigenvalues of M (descending) and u_i' DeltaM u_i)
+void filter_factors(const double* H, int ldh, int k, const double* dK, int lddk, const double* mu,
+                    const double* dmu, double lambda, int side, int hybrid, double* phi, double* dphi);
+// Ritz values of a p-step Arnoldi (Hp p x p, h_next = H(p+1,p)), descending by real part, with
+// y_i' G y_i (G = Qp' DeltaM Qp) and the residual norms |h_next| |e_p' y_i| of the first nev
+void ritz(const double* Hp, int ldh, int p, double h_next, const double* G, int ldg, int nev, double* mu,
+          double* dmu, double* resid);
 }  // namespace dense
 
 }  // namespace hgm

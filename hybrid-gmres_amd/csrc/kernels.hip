@@ -1333,6 +1333,23 @@ template <typename T> void fill(hgm_ctx* c, int64_t n, T* x, T v) {
     HGM_HIP(hipGetLastError());
 }
 
+// Deterministic pseudo-random vector in (-1, 1): x_i = splitmix64(seed + i) scaled (the start
+// vector of the Ritz Arnoldi in bounds.cpp; the same bits on every device and run).
+template <typename T>
+__global__ __launch_bounds__(BS) void k_fill_hash(int64_t n, T* x, uint64_t seed) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+        uint64_t z = seed + 0x9E3779B97F4A7C15ull * (uint64_t)(i + 1);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        x[i] = (T)((double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0);
+    }
+}
+template <typename T> void fill_hash(hgm_ctx* c, int64_t n, T* x, uint64_t seed) {
+    k_fill_hash<T><<<grid_for(n), BS, 0, c->stream>>>(n, x, seed);
+    HGM_HIP(hipGetLastError());
+}
+
 template <typename T>
 __global__ __launch_bounds__(BS) void k_convert(int64_t n, const double* in, T* out) {
     for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = (T)in[i];
@@ -1372,6 +1389,7 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
     template void lsmr_monitor<T>(hgm_ctx*, int64_t, const T*, const T*, double, double, double*, double*, \
                                   double*, const T*, double, double, double, bool, double*);   \
     template void fill<T>(hgm_ctx*, int64_t, T*, T);                                           \
+    template void fill_hash<T>(hgm_ctx*, int64_t, T*, uint64_t);                               \
     template void convert<T>(hgm_ctx*, int64_t, const double*, T*);                            \
     template void convert_back<T>(hgm_ctx*, int64_t, const T*, double*);                       \
     template void fro2<T>(hgm_ctx*, const hgm_mat*, double*);                                   \

@@ -17,6 +17,9 @@ from .core import (  # noqa: F401
     arnoldi,
     as_operator,
     default_context,
+    eig,
+    filter_factors,
+    ritz,
     gcv_fminbnd,
     gcv_from_H,
     gcv_function,
@@ -28,6 +31,8 @@ from .core import (  # noqa: F401
     lsqr_solver,
 )
 from . import problems  # noqa: F401
+from . import regtools  # noqa: F401
+from . import analysis  # noqa: F401
 from ._lib import LIB_PATH, load as load_library  # noqa: F401
 
 __all__ = [
@@ -35,5 +40,6 @@ __all__ = [
     "hybrid_lsqr_solver", "hybrid_lsmr_solver", "gcv_function", "arnoldi", "gcv_from_H",
     "gcv_fminbnd", "ABgmres_hybrid_bounds", "ABgmres_nonhybrid_bounds",
     "BAgmres_hybrid_bounds", "BAgmres_nonhybrid_bounds", "Context", "SparseOperator",
-    "as_operator", "default_context", "HgmError", "OutputNotAssigned", "problems",
+    "as_operator", "default_context", "HgmError", "OutputNotAssigned", "problems", "regtools", "analysis",
+    "eig", "filter_factors", "ritz",
 ]

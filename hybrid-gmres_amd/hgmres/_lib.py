@@ -93,6 +93,11 @@ _SIGS = {
     "hgm_gcv_from_H": (c_int, [dp, c_int, c_double, c_double, c_double, dp]),
     "hgm_gcv_function": (c_int, [c_void_p, c_double, c_void_p, c_void_p, dp, c_int64, c_int, c_int, dp]),
     "hgm_gcv_fminbnd": (c_int, [dp, c_int, c_double, c_double, c_double, c_double, c_double, dp, dp]),
+    "hgm_gmres_bounds_filter": (c_int, [c_void_p, P(hgm_opts), c_void_p, c_void_p, dp, dp, c_double, c_int, c_double,
+                                        c_int, c_int, c_void_p, c_void_p, c_int, dp, dp, dp, P(c_int), dp, dp, dp, dp]),
+    "hgm_filter_factors": (c_int, [dp, c_int, c_int, dp, c_int, dp, dp, c_double, c_int, c_int, dp, dp]),
+    "hgm_ritz": (c_int, [dp, c_int, c_int, c_double, dp, c_int, c_int, dp, dp, dp]),
+    "hgm_eig": (c_int, [c_int, dp, dp, dp, dp]),
     "hgm_kernel_timing": (c_int, [c_void_p, c_int]),
     "hgm_kernel_timing_read": (c_int, [c_void_p, c_int, dp, ip64, dp]),
     "hgm_kernel_timing_pause": (c_int, [c_void_p, c_int]),

@@ -423,40 +423,93 @@ def hybrid_ba_gmres_rtp(A, B, b, x_true, tol, maxit, lambda_, *, ctx=None, orth=
                        explicit_residual=explicit_residual)
 
 
-def _bounds(A, B, b, x_true, tol, maxit, lam, side, hybrid, ctx, orth, return_H, explicit_residual=False):
-    out = _gmres_call("hgm_gmres_bounds_ex", A, B, b, x_true, tol, maxit, lam, ctx, orth, return_H,
-                      extra=(lam, side, hybrid), explicit_residual=explicit_residual)
-    # outputs 5-8 (phi_final, dphi_final, phi_iter, dphi_iter): dense spectral bounds, out of scope
-    return out[:4] + (None, None, None, None) + out[4:]
+def _delta_ops(DeltaM, ctx):
+    """DeltaM as one device operator, or as a factored product (L, R) = L*R applied to vectors."""
+    if isinstance(DeltaM, (tuple, list)):
+        L_, R_ = DeltaM
+        return as_operator(_sparse(L_), ctx), as_operator(_sparse(R_), ctx)
+    return as_operator(_sparse(DeltaM), ctx), None
+
+
+def _sparse(M):
+    if isinstance(M, SparseOperator) or sp.issparse(M):
+        return M
+    return sp.csr_matrix(np.asarray(M, dtype=np.float64))
+
+
+def _bounds(A, B, b, x_true, tol, maxit, lam, side, hybrid, ctx, orth, return_H, explicit_residual=False,
+            DeltaM=None, ritz_steps=0, return_ritz=False):
+    if DeltaM is None:
+        out = _gmres_call("hgm_gmres_bounds_ex", A, B, b, x_true, tol, maxit, lam, ctx, orth, return_H,
+                          extra=(lam, side, hybrid), explicit_residual=explicit_residual)
+        # outputs 5-8 need DeltaM (the reference's 8th / 7th argument)
+        return out[:4] + (None, None, None, None) + out[4:]
+    # outputs 5-8: filter factors phi and their first-order perturbation dphi (*_bounds.m:42-81)
+    ctx, Ao, Bo = _ops(A, B, ctx)
+    DL, DR = _delta_ops(DeltaM, ctx)
+    m, n = Ao.shape
+    maxit = int(maxit)
+    b = _f64(b, m, "b")
+    xt = _f64(x_true, n, "x_true")
+    x, err, res, it = np.zeros(n), np.zeros(maxit), np.zeros(maxit), C.c_int(0)
+    phi = np.zeros(maxit * maxit)
+    dphi = np.zeros(maxit * maxit)
+    mu = np.zeros(maxit)
+    rres = np.zeros(maxit)
+    H = np.zeros((maxit + 1) * maxit) if return_H else None
+    o = _opts(orth, H, explicit_residual=explicit_residual)
+    _check(L.load().hgm_gmres_bounds_filter(ctx.handle, C.byref(o), Ao._h, Bo._h, _dp(b), _dp(xt), float(tol),
+                                            maxit, float(lam), side, hybrid, DL._h, DR._h if DR else None,
+                                            int(ritz_steps), _dp(x), _dp(err), _dp(res), C.byref(it), _dp(phi),
+                                            _dp(dphi), _dp(mu), _dp(rres)), ctx)
+    k = it.value
+    P_ = phi.reshape(maxit, maxit)
+    D_ = dphi.reshape(maxit, maxit)
+    phi_iter = [P_[j, : j + 1].copy() for j in range(k)]
+    dphi_iter = [D_[j, : j + 1].copy() for j in range(k)]
+    if k and np.isnan(phi_iter[-1]).all():         # breakdown at iteration k: phi_iter{k} = []
+        phi_iter[-1] = np.zeros(0)
+        dphi_iter[-1] = np.zeros(0)
+    out = (x, err[:k].copy(), res[:k].copy(), k, phi_iter[-1], dphi_iter[-1], phi_iter, dphi_iter)
+    if return_H:
+        out = out + (H.reshape(maxit, maxit + 1).T.copy(),)
+    if return_ritz:
+        out = out + (mu[:k].copy(), rres[:k].copy())
+    return out
 
 
 def ABgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lambda_, DeltaM=None, *, ctx=None, orth="mgs", return_H=False,
-                             explicit_residual=False):
-    """``ABgmres_hybrid_bounds.m`` outputs 1-4: m-space Arnoldi on ``A*B``, PTR Tikhonov, ``x = B*z``."""
+                             explicit_residual=False, ritz_steps=0, return_ritz=False):
+    """``ABgmres_hybrid_bounds.m``: m-space Arnoldi on ``A*B``, PTR Tikhonov, ``x = B*z``; outputs 5-8
+    (filter factors) when ``DeltaM`` (a matrix, or a factored pair ``(L, R)`` = L*R) is given."""
     return _bounds(A, B, b, x_true, tol, maxit, lambda_, L.HGM_SIDE_AB, 1, ctx, orth, return_H,
-                   explicit_residual=explicit_residual)
+                   explicit_residual=explicit_residual,
+                   DeltaM=DeltaM, ritz_steps=ritz_steps, return_ritz=return_ritz)
 
 
 def ABgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, *, ctx=None, orth="mgs", return_H=False,
-                             explicit_residual=False):
-    """``ABgmres_nonhybrid_bounds.m`` outputs 1-4."""
+                             explicit_residual=False, ritz_steps=0, return_ritz=False):
+    """``ABgmres_nonhybrid_bounds.m`` (outputs 5-8 with ``DeltaM``)."""
     return _bounds(A, B, b, x_true, tol, maxit, 0.0, L.HGM_SIDE_AB, 0, ctx, orth, return_H,
-                   explicit_residual=explicit_residual)
+                   explicit_residual=explicit_residual,
+                   DeltaM=DeltaM, ritz_steps=ritz_steps, return_ritz=return_ritz)
 
 
 def BAgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lambda_, DeltaM=None, *, ctx=None, orth="mgs", return_H=False,
-                             explicit_residual=False):
-    """``BAgmres_hybrid_bounds.m`` outputs 1-4: n-space Arnoldi on ``B*A``, PTR Tikhonov."""
+                             explicit_residual=False, ritz_steps=0, return_ritz=False):
+    """``BAgmres_hybrid_bounds.m``: n-space Arnoldi on ``B*A``, PTR Tikhonov (outputs 5-8 with ``DeltaM``)."""
     return _bounds(A, B, b, x_true, tol, maxit, lambda_, L.HGM_SIDE_BA, 1, ctx, orth, return_H,
-                   explicit_residual=explicit_residual)
+                   explicit_residual=explicit_residual,
+                   DeltaM=DeltaM, ritz_steps=ritz_steps, return_ritz=return_ritz)
 
 
 def BAgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, *, ctx=None, orth="mgs", return_H=False,
-                             explicit_residual=False):
-    """``BAgmres_nonhybrid_bounds.m`` outputs 1-4.  The reference forms ``M = B*A``
+                             explicit_residual=False, ritz_steps=0, return_ritz=False):
+    """``BAgmres_nonhybrid_bounds.m`` (outputs 5-8 with ``DeltaM``).  The reference forms ``M = B*A``
     explicitly (``:4``); here the operator is applied as ``B*(A*q)``."""
     return _bounds(A, B, b, x_true, tol, maxit, 0.0, L.HGM_SIDE_BA, 0, ctx, orth, return_H,
-                   explicit_residual=explicit_residual)
+                   explicit_residual=explicit_residual,
+                   DeltaM=DeltaM, ritz_steps=ritz_steps, return_ritz=return_ritz)
 
 
 def _gkb_ops(A, ctx, At=None, dtype=L.HGM_F64):
@@ -576,3 +629,60 @@ def gcv_fminbnd(H, beta, trace_m, lo=1e-9, hi=1e-1, tolx=1e-8):
     if rc != L.HGM_OK:
         raise ValueError("hgm_gcv_fminbnd: invalid arguments")
     return lo_.value, g.value
+
+
+# ---------------------------------------------------------------------------
+# Host-only spectral helpers of the filter-factor bounds (spectral.cpp)
+# ---------------------------------------------------------------------------
+def eig(M):
+    """MATLAB ``[V, D] = eig(M)`` of a real square matrix (host): (w, V), complex, unit 2-norm columns."""
+    M = np.asarray(M, dtype=np.float64)
+    n = M.shape[0]
+    Mf = np.ascontiguousarray(M.T).reshape(-1)
+    wr, wi, V = np.zeros(n), np.zeros(n), np.zeros(n * n)
+    if L.load().hgm_eig(n, _dp(Mf), _dp(wr), _dp(wi), _dp(V)) != L.HGM_OK:
+        raise HgmError("hgm_eig: QR iteration did not converge")
+    V = V.reshape(n, n).T
+    W = V.astype(np.complex128)
+    j = 0
+    while j < n:
+        if wi[j] > 0 and j + 1 < n:
+            W[:, j] = V[:, j] + 1j * V[:, j + 1]
+            W[:, j + 1] = V[:, j] - 1j * V[:, j + 1]
+            j += 2
+        else:
+            j += 1
+    return wr + 1j * wi, W
+
+
+def filter_factors(H, k, dK, mu, dmu, lambda_, side, hybrid):
+    """phi / dphi of iteration k of the ``*_bounds.m`` files (``:42-78``) from H ((k+1) x k
+    leading part), dK = Qk' DeltaM Qk, the k leading eigenvalues mu of M and dmu."""
+    H = np.asarray(H, dtype=np.float64)
+    Hf = np.ascontiguousarray(H.T).reshape(-1)
+    dK = np.asarray(dK, dtype=np.float64)
+    dKf = np.ascontiguousarray(dK.T).reshape(-1)
+    mu = np.ascontiguousarray(mu, dtype=np.float64)
+    dmu = np.ascontiguousarray(dmu, dtype=np.float64)
+    phi, dphi = np.zeros(k), np.zeros(k)
+    sd = L.HGM_SIDE_AB if side == "ab" else L.HGM_SIDE_BA
+    rc = L.load().hgm_filter_factors(_dp(Hf), H.shape[0], int(k), _dp(dKf), dK.shape[0], _dp(mu), _dp(dmu),
+                                     float(lambda_), sd, int(bool(hybrid)), _dp(phi), _dp(dphi))
+    if rc != L.HGM_OK:
+        raise ValueError("hgm_filter_factors: invalid arguments")
+    return phi, dphi
+
+
+def ritz(Hp, h_next, G, nev):
+    """Leading Ritz pairs of a p-step Arnoldi: (mu, dmu, resid) (descending real part)."""
+    Hp = np.asarray(Hp, dtype=np.float64)
+    p = Hp.shape[1]
+    Hf = np.ascontiguousarray(Hp.T).reshape(-1)
+    G = np.asarray(G, dtype=np.float64)
+    Gf = np.ascontiguousarray(G.T).reshape(-1)
+    mu, dmu, rr = np.zeros(nev), np.zeros(nev), np.zeros(nev)
+    rc = L.load().hgm_ritz(_dp(Hf), Hp.shape[0], p, float(h_next), _dp(Gf), G.shape[0], int(nev), _dp(mu),
+                           _dp(dmu), _dp(rr))
+    if rc != L.HGM_OK:
+        raise ValueError("hgm_ritz: invalid arguments")
+    return mu, dmu, rr

@@ -19,6 +19,8 @@
  *   hgm_gcv_function         <- gcv_function.m:1          gcv_val
  *   hgm_arnoldi / hgm_gcv_from_H  <- gcv_function.m:18-33 / :35-58 split (Arnoldi once, lambda on H;
  *                               pattern of plot_gcv_surface.m:58-122)
+ *   hgm_gmres_bounds_filter  <- outputs 5-8 of the four *_bounds.m (phi/dphi filter-factor bounds,
+ *                               eig(M) of :4-9 replaced by device Ritz pairs)
  *   hgm_mat_create_csc       <- MATLAB sparse (CSC, jc/ir/pr) operand hand-over
  *   hgm_spmv                 <- the `A*v` / `B*u` / `A'*u` mtimes inside every solver
  *
@@ -266,6 +268,38 @@ HGM_API int hgm_gcv_function(hgm_ctx* ctx, double lambda, const hgm_mat* A, cons
 /* fminbnd (Brent) over λ ∈ [lo, hi] of GCV on one cached Arnoldi (analyze_regularization.m:37-46). */
 HGM_API int hgm_gcv_fminbnd(const double* H, int k, double beta, double trace_m, double lo,
                             double hi, double tolx, double* lambda_opt, double* gcv_opt);
+
+/* ---- filter-factor / perturbation bounds (outputs 5-8 of *_bounds.m) ---------
+ * ABgmres_hybrid_bounds.m:1-2, ABgmres_nonhybrid_bounds.m:1-2, BAgmres_hybrid_bounds.m:1-2,
+ * BAgmres_nonhybrid_bounds.m:1-2: [x, err, res, niters, phi_final, dphi_final, phi_iter, dphi_iter].
+ * The dense eig(M) of *_bounds.m:4-9 is replaced by the Ritz pairs of a ritz_steps-step Arnoldi
+ * on M = A*B (AB) / B*A (BA) with CGS2 (ritz_steps = dim reproduces eig(M); 0 = automatic,
+ * max(2 niters + 10, 20) capped at dim).  DeltaM = dM_left (dim x dim), or dM_left * dM_right
+ * when dM_right != NULL (e.g. A*E / E*A of analyze_regularization.m:14-15, never formed).
+ * phi_iter / dphi_iter: maxit x maxit column-major, column k-1 holds iteration k's k values
+ * (phi_final = column niters-1).  mu (optional, niters): the Ritz values used (mu_full(1:k));
+ * ritz_resid (optional, niters): ||M u_i - mu_i u_i||.  Complex Ritz pairs: the real parts, as
+ * the reference's real(diag(D)); their dMu is the phase-invariant Re(y^H G y).  Single rank. */
+HGM_API int hgm_gmres_bounds_filter(hgm_ctx* ctx, const hgm_opts* opts, const hgm_mat* A, const hgm_mat* B,
+                                    const double* b, const double* x_true, double tol, int maxit, double lambda,
+                                    int side, int hybrid, const hgm_mat* dM_left, const hgm_mat* dM_right,
+                                    int ritz_steps, double* x, double* error_norm, double* residual_norm,
+                                    int* niters, double* phi_iter, double* dphi_iter, double* mu,
+                                    double* ritz_resid);
+/* Host only: phi / dphi of iteration k (*_bounds.m:42-78) from H ((k+1) x k leading part of a
+ * column-major array with leading dimension ldh), dK = Qk' DeltaM Qk (k x k, lddk), the k
+ * leading eigenvalues mu of M (descending) and dmu_i = u_i' DeltaM u_i. */
+HGM_API int hgm_filter_factors(const double* H, int ldh, int k, const double* dK, int lddk, const double* mu,
+                               const double* dmu, double lambda, int side, int hybrid, double* phi, double* dphi);
+/* Host only: the nev leading Ritz pairs (descending real part) of a p-step Arnoldi (Hp: p x p,
+ * ldh; h_next = H(p+1,p)) with dmu_i = y_i' G y_i (G = Qp' DeltaM Qp, p x p, ldg) and
+ * resid_i = |h_next| |e_p' y_i| (optional). */
+HGM_API int hgm_ritz(const double* Hp, int ldh, int p, double h_next, const double* G, int ldg, int nev, double* mu,
+                     double* dmu, double* resid);
+/* Host only: MATLAB eig of a real n x n column-major matrix: eigenvalues wr + i wi, unit 2-norm
+ * eigenvectors in V (optional, LAPACK dgeev layout: a complex pair j, j+1 with wi[j] > 0 has
+ * V(:,j) +- i V(:,j+1)).  HGM_E_ARG when the QR iteration does not converge. */
+HGM_API int hgm_eig(int n, const double* A, double* wr, double* wi, double* V);
 
 /* ---- timing hooks used by bench.py ---------------------------------------- */
 /* Average device time (ms) of the named kernel class over the calls since the

@@ -639,11 +639,81 @@ def hybrid_lsmr_solver(A, b, x_true, tol, maxit, lam):
     return x, error_norm[:niters], residual_norm[:niters], niters
 
 
-def _gmres_ptr(A, B, b, x_true, tol, maxit, lam, side, hybrid, explicit_BA=False, return_H=False):
+def _dense(M):
+    return M.toarray() if sp.issparse(M) else np.asarray(M, dtype=np.float64)
+
+
+def _spectrum(A, B, side):
+    """``M = A*B`` / ``B*A``; ``[U,D] = eig(M)``; real parts sorted descending with the
+    eigenvector columns (*_bounds.m:4-9).  Dense: small problems only."""
+    M = _dense(A) @ _dense(B) if side == "ab" else _dense(B) @ _dense(A)   # :4
+    D, U = np.linalg.eig(M)                      # :6-7 (LAPACK dgeev: unit 2-norm vectors)
+    mu_full = np.real(D)                         # :8 / :7
+    order = np.argsort(-mu_full, kind="stable")  # sort(mu_full, 'descend')
+    return mu_full[order], U[:, order]
+
+
+def _filter_iteration(H, Q, k, mu_full, UA, DeltaM, lam, side, hybrid):
+    """phi / dphi of iteration k (1-based): ABgmres_hybrid_bounds.m:43-78,
+    ABgmres_nonhybrid_bounds.m:42-73, BAgmres_hybrid_bounds.m:42-74,
+    BAgmres_nonhybrid_bounds.m:42-74."""
+    Qk = Q[:, :k]                                # :43 / :42
+    DM = _dense(DeltaM)
+    dK = Qk.T @ (DM @ Qk)                        # :44 / :43  Qk'*DeltaM*Qk
+    Hs = H[:k, :k]                               # :46 / :43-45
+    ek = np.zeros(k)
+    ek[-1] = 1.0                                 # :47
+    if side == "ba" and hybrid:
+        Hf = H[: k + 1, :k]                      # BA hybrid :44
+        Th, W = sla.eig(Hf.T @ Hf, Hs)           # :46  eig(Hk_full'*Hk_full, Hk_small)
+    else:
+        X = np.zeros((k, k))
+        X[:, -1] = mldivide(Hs.T, ek)            # Hk_small' \ (ek*ek'): only the last column
+        P = Hs + (H[k, k - 1] ** 2) * X          # AB :48 / nonhybrid :48 / :47
+        if hybrid:
+            P = P + lam * np.eye(k)              # AB hybrid :49
+        Th, W = np.linalg.eig(P)                 # :50 / :49 / :48
+    Theta = np.real(Th)                          # :51 / :50 / :49
+    p_sort = np.argsort(Theta, kind="stable")    # :52  sort(Theta)
+    Theta = Theta[p_sort]
+    W = W[:, p_sort]                             # :53
+    dTheta = np.real(np.einsum("ij,ik,kj->j", W.conj(), dK, W))   # :55  real(diag(W'*dK*W))
+    dMu = np.sum(UA[:, :k] * (DM @ UA[:, :k]), axis=0).conj()     # :56  sum(UA.*(DeltaM*UA),1)'
+    mu = mu_full[:k]                             # :58
+    s2l = mu + lam if hybrid else mu             # :60 (hybrid); nonhybrid uses mu
+    eps0 = EPS                                   # :61
+    Clog = np.zeros(k)
+    P_excl = np.zeros((k, k))
+    for i in range(k):                           # :64-71
+        terms = np.maximum(1 - s2l[i] / Theta, eps0)
+        Clog[i] = np.sum(np.log(terms))
+        for j in range(k):
+            denom = max(1 - s2l[i] / Theta[j], eps0)
+            P_excl[i, j] = np.exp(Clog[i] - np.log(denom))
+    P_final = np.exp(Clog)                       # :72
+    if hybrid:
+        phi = (mu / s2l) * (1 - P_final)         # :73
+        term1 = -mu * np.sum((dTheta / Theta ** 2) * P_excl, axis=1)            # :75
+        term2 = (lam / s2l ** 2) * (1 - P_final) * dMu                           # :76
+        term3 = (mu / s2l) * np.sum((1 / Theta) * P_excl, axis=1) * dMu          # :77
+        dphi = term1 + term2 + term3             # :78
+    else:
+        phi = 1 - P_final                        # nonhybrid :69
+        term1 = -mu * np.sum((dTheta / Theta ** 2) * P_excl, axis=1)            # :71
+        term2 = np.sum((1 / Theta) * P_excl, axis=1) * dMu                      # :72
+        dphi = term1 + term2                     # :73
+    return phi, dphi
+
+
+def _gmres_ptr(A, B, b, x_true, tol, maxit, lam, side, hybrid, explicit_BA=False, return_H=False,
+               DeltaM=None, return_Q=False):
     """Arnoldi + projected-solve part of ``{AB,BA}gmres_{hybrid,nonhybrid}_bounds.m``
-    (lines cited per variant below).  The spectral-bound outputs
-    (``phi_*``/``dphi_*``) are out of scope."""
+    (lines cited per variant below).  With ``DeltaM`` the spectral-bound outputs 5-8
+    (``phi_final, dphi_final, phi_iter, dphi_iter``) follow the reference's dense
+    ``eig(M)`` (small problems only); the GPU computes them from Ritz pairs at scale."""
     m, n = A.shape
+    spec = _spectrum(A, B, side) if DeltaM is not None else None
+    phi_iter, dphi_iter = [], []
     if side == "ab":
         r0 = b - A @ (B @ np.zeros(B.shape[1]))  # AB*_bounds.m:11-12
         dim = m
@@ -687,35 +757,52 @@ def _gmres_ptr(A, B, b, x_true, tol, maxit, lam, side, hybrid, explicit_BA=False
         xk = B @ zk if side == "ab" else zk      # AB :38 ; BA :37
         res[k] = _norm(b - A @ xk) / nb          # :40 / :39
         err[k] = _norm(xk - x_true) / nxt        # :41 / :40
+        if spec is not None:                     # :42-81
+            ph, dph = _filter_iteration(H, Q, k + 1, spec[0], spec[1], DeltaM, lam, side, hybrid)
+            phi_iter.append(ph)
+            dphi_iter.append(dph)
         if res[k] <= tol:                        # :83 / :78 / :79
             break
     if xk is None:
         raise OutputNotAssigned('Output argument "x" not assigned (*gmres_*_bounds)')
     niters = k + 1
     out = (xk, err[:niters], res[:niters], niters)
-    return out + (H,) if return_H else out
+    if spec is not None:
+        # phi_final = phi_iter{k}: empty when iteration k broke down before :80
+        last = phi_iter[-1] if len(phi_iter) == niters else np.zeros(0)
+        dlast = dphi_iter[-1] if len(dphi_iter) == niters else np.zeros(0)
+        out = out + (last, dlast, phi_iter, dphi_iter)
+    if return_H:
+        out = out + (H,)
+    if return_Q:
+        out = out + (Q,)
+    return out
 
 
-def ABgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lam, DeltaM=None, return_H=False):
-    """``ABgmres_hybrid_bounds.m:11-41,83-88`` (first four outputs)."""
-    return _gmres_ptr(A, B, b, x_true, tol, maxit, lam, "ab", True, return_H=return_H)
+def ABgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lam, DeltaM=None, return_H=False, return_Q=False):
+    """``ABgmres_hybrid_bounds.m:1-96`` (outputs 5-8 when ``DeltaM`` is given)."""
+    return _gmres_ptr(A, B, b, x_true, tol, maxit, lam, "ab", True, return_H=return_H, DeltaM=DeltaM,
+                      return_Q=return_Q)
 
 
-def ABgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, return_H=False):
-    """``ABgmres_nonhybrid_bounds.m:12-40,78-83``."""
-    return _gmres_ptr(A, B, b, x_true, tol, maxit, 0.0, "ab", False, return_H=return_H)
+def ABgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, return_H=False, return_Q=False):
+    """``ABgmres_nonhybrid_bounds.m:1-91``."""
+    return _gmres_ptr(A, B, b, x_true, tol, maxit, 0.0, "ab", False, return_H=return_H, DeltaM=DeltaM,
+                      return_Q=return_Q)
 
 
-def BAgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lam, DeltaM=None, return_H=False):
-    """``BAgmres_hybrid_bounds.m:11-40,79-84``."""
-    return _gmres_ptr(A, B, b, x_true, tol, maxit, lam, "ba", True, return_H=return_H)
+def BAgmres_hybrid_bounds(A, B, b, x_true, tol, maxit, lam, DeltaM=None, return_H=False, return_Q=False):
+    """``BAgmres_hybrid_bounds.m:1-92``."""
+    return _gmres_ptr(A, B, b, x_true, tol, maxit, lam, "ba", True, return_H=return_H, DeltaM=DeltaM,
+                      return_Q=return_Q)
 
 
-def BAgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, explicit_BA=True, return_H=False):
-    """``BAgmres_nonhybrid_bounds.m:4,12-40,79-84`` — uses the explicit product
+def BAgmres_nonhybrid_bounds(A, B, b, x_true, tol, maxit, DeltaM=None, explicit_BA=True, return_H=False,
+                             return_Q=False):
+    """``BAgmres_nonhybrid_bounds.m:1-92`` — uses the explicit product
     ``M = B*A`` as the reference does (``:4,25``)."""
     return _gmres_ptr(A, B, b, x_true, tol, maxit, 0.0, "ba", False,
-                      explicit_BA=explicit_BA, return_H=return_H)
+                      explicit_BA=explicit_BA, return_H=return_H, DeltaM=DeltaM, return_Q=return_Q)
 
 
 def arnoldi(A, B, b, k_gcv, gcv_type, breakdown_tol=1e-12, orth="mgs"):

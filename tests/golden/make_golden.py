@@ -83,9 +83,41 @@ def dump_c3(name="c3_2048.npz", k=5):
           np.max(np.abs(d["hba_mgs_H"] - d["hba_cgs2_H"])) / np.max(np.abs(d["hba_mgs_H"])))
 
 
+def dump_shaw_pipeline(name="shaw32_pipeline.npz"):
+    """analyze_regularization.m on shaw(32) (restated, hgmres.regtools) with numpy noise and
+    mismatch (MATLAB's randn stream cannot be reproduced): inputs, the oracle's outputs in the
+    default (LAPACK/BLAS) order with dense operands as the reference has them, and the same
+    pipeline in the fixed summation order.  Their difference is the pipeline's own rounding
+    sensitivity (it is large: the 32-step Arnoldi on shaw(32) runs far past the numerical rank),
+    stored as `spread_<key>` (normwise: max|default - fixed| / max|fixed|) for the production-path
+    test's envelope."""
+    import warnings
+    import scipy.sparse as sp
+    from hgmres.analysis import regularization_problem
+    from oracle import pipeline
+    P = regularization_problem(32)
+    d = {"A": P.A, "b": P.b, "b_exact": P.b_exact, "x_true": P.x_true, "E": P.E}
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        o = pipeline.analyze_regularization(P.A, P.b, P.x_true, P.B_pert, P.DeltaM_AB, P.DeltaM_BA)
+        with R.fixed_order():
+            f = pipeline.analyze_regularization(sp.csr_matrix(P.A), P.b, P.x_true, sp.csr_matrix(P.B_pert),
+                                                P.DeltaM_AB, P.DeltaM_BA, bounds_outputs=False, explicit_BA=False)
+    for k, v in o.items():
+        d[f"out_{k}"] = np.asarray(v)
+    for k, v in f.items():
+        a, b = np.asarray(o[k], dtype=np.float64), np.asarray(v, dtype=np.float64)
+        d[f"spread_{k}"] = np.max(np.abs(a - b), initial=0.0) / max(np.max(np.abs(b), initial=0.0), 1e-300)
+    np.savez_compressed(os.path.join(OUT, name), **d)
+    print("wrote", name, {k: float(np.max(v)) for k, v in d.items() if k.startswith("spread_")})
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["c3"]:
         dump_c3()
+        sys.exit(0)
+    if sys.argv[1:] == ["shaw"]:
+        dump_shaw_pipeline()
         sys.exit(0)
     # matched back-projector B = A^T (run_equivalence_plots.m:5 style), 24^2 phantom, 12 angles
     dump("tomo24_matched.npz", tomo_problem(24, 12, noise=1e-2, seed=0, backprojector="matched"), maxit=12, lam=1e-2)

@@ -1,0 +1,235 @@
+"""The MATLAB mex gateway (matlab/hgmres_mex.c) driven through a stand-in of the
+mx API (tests/mexmock: test infrastructure; MATLAB is absent from this image and the GPU box).
+
+CPU: the gateway compiles against the mx API subset it uses, dispatches by name, validates its
+arguments with MATLAB-style error identifiers, and fails loudly without a HIP device.
+GPU: every dispatched entry point returns what the Python binding of the same C-ABI call returns,
+bit for bit, with the reference's output shapes (histories truncated to 1:niters, phi_iter as a
+cell of growing columns) and MATLAB's own error for an unassigned x.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import ROOT, golden_problem, load_golden
+import hgmres
+
+MOCK_DIR = os.path.join(ROOT, "tests", "mexmock")
+MOCK = os.path.join(MOCK_DIR, "libhgmres_mex_mock.so")
+
+
+class MexError(Exception):
+    def __init__(self, ident, msg):
+        super().__init__(f"{ident}: {msg}")
+        self.ident = ident
+
+
+class Mex:
+    """mexFunction through the stand-in: Python values in, numpy arrays / lists (cells) out."""
+
+    def __init__(self):
+        hgmres.load_library()                       # libhgmres (and the HIP runtime) first
+        if not os.path.exists(MOCK):
+            subprocess.run(["make", "-s"], cwd=MOCK_DIR, check=True)
+        L = C.CDLL(MOCK)
+        vp, sz = C.c_void_p, C.c_size_t
+        for name, res, args in (
+                ("mock_double", vp, [sz, sz, C.POINTER(C.c_double)]),
+                ("mock_sparse", vp, [sz, sz, sz, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
+                ("mock_string", vp, [C.c_char_p]),
+                ("mock_call", C.c_int, [C.c_int, C.POINTER(vp), C.c_int, C.POINTER(vp), C.c_char_p, C.c_char_p, C.c_int]),
+                ("mxGetM", sz, [vp]), ("mxGetN", sz, [vp]), ("mxIsCell", C.c_int, [vp]),
+                ("mxGetDoubles", C.POINTER(C.c_double), [vp]), ("mxGetCell", vp, [vp, sz]),
+                ("mxDestroyArray", None, [vp]), ("mock_exit", None, [])):
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        self.L = L
+
+    def _arg(self, v):
+        L = self.L
+        if isinstance(v, str):
+            return L.mock_string(v.encode())
+        if sp.issparse(v):
+            M = sp.csc_matrix(v)
+            M.sort_indices()
+            jc = np.ascontiguousarray(M.indptr, dtype=np.int64)
+            ir = np.ascontiguousarray(M.indices, dtype=np.int64)
+            pr = np.ascontiguousarray(M.data, dtype=np.float64)
+            return L.mock_sparse(M.shape[0], M.shape[1], M.nnz, jc.ctypes.data_as(C.POINTER(C.c_int64)),
+                                 ir.ctypes.data_as(C.POINTER(C.c_int64)), pr.ctypes.data_as(C.POINTER(C.c_double)))
+        a = np.asarray(v, dtype=np.float64)
+        if a.ndim == 0:
+            a = a.reshape(1, 1)
+        elif a.ndim == 1:
+            a = a.reshape(-1, 1)
+        f = np.asfortranarray(a).reshape(-1, order="F").copy()
+        return L.mock_double(a.shape[0], a.shape[1], f.ctypes.data_as(C.POINTER(C.c_double)))
+
+    def _out(self, p):
+        L = self.L
+        m, n = L.mxGetM(p), L.mxGetN(p)
+        if L.mxIsCell(p):
+            return [self._out(L.mxGetCell(p, i)) for i in range(m * n)]
+        d = L.mxGetDoubles(p)
+        a = np.array([d[i] for i in range(m * n)], dtype=np.float64).reshape((m, n), order="F")
+        return a[:, 0].copy() if n == 1 else a
+
+    def __call__(self, nlhs, *args):
+        ins = [self._arg(a) for a in args]
+        prhs = (C.c_void_p * max(len(ins), 1))(*ins)
+        plhs = (C.c_void_p * max(nlhs, 1))()
+        ident, msg = C.create_string_buffer(512), C.create_string_buffer(512)
+        rc = self.L.mock_call(nlhs, plhs, len(ins), prhs, ident, msg, 512)
+        for p in ins:
+            self.L.mxDestroyArray(p)
+        if rc:
+            raise MexError(ident.value.decode(), msg.value.decode())
+        outs = []
+        for i in range(nlhs):
+            outs.append(self._out(plhs[i]) if plhs[i] else None)
+            if plhs[i]:
+                self.L.mxDestroyArray(plhs[i])
+        return outs
+
+
+@pytest.fixture(scope="module")
+def mex():
+    return Mex()
+
+
+def test_gateway_builds_and_exports_mexfunction(mex):
+    assert hasattr(mex.L, "mexFunction")
+
+
+@pytest.mark.parametrize("args,ident", [
+    ((), "hgmres:nargin"),
+    ((3.0,), "hgmres:nargin"),
+    (("no_such_solver",), "hgmres:unknown"),
+    (("hybrid_ab_gmres_rtp", 1.0), "hgmres:nargin"),
+    (("lsqr_solver", 1.0, 2.0, 3.0, 4.0, 5.0, 6.0), "hgmres:nargin"),
+    (("gmres_bounds", "ab", 1.0), "hgmres:nargin"),
+])
+def test_gateway_argument_errors(mex, args, ident):
+    with pytest.raises(MexError) as e:
+        mex(1, *args)
+    assert e.value.ident == ident
+
+
+def test_gateway_without_device_fails_loudly(mex):
+    """No HIP device (this container): a solver call raises hgmres:device -- no CPU fallback."""
+    if _devices() > 0:
+        pytest.skip("a HIP device is visible")
+    A = sp.random(8, 6, density=0.5, random_state=0, format="csc")
+    with pytest.raises(MexError) as e:
+        mex(4, "lsqr_solver", A, np.ones(8), np.ones(6), 0.0, 3.0)
+    assert e.value.ident == "hgmres:device"
+
+
+def _devices():
+    c = C.c_int(0)
+    hgmres.load_library().hgm_device_count(C.byref(c))
+    return c.value
+
+
+# ------------------------------------------------------------------ GPU: bit-identical dispatch
+@pytest.fixture(scope="module")
+def tomo(gpu_ctx):
+    A, B, b, xt, g = golden_problem("tomo24_pixel.npz")
+    return A.tocsc(), B.tocsc(), b, xt
+
+
+def _ops(ctx, *Ms):
+    return [hgmres.SparseOperator.from_csc(M, ctx) for M in Ms]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fn", ["hybrid_ab_gmres_rtp", "hybrid_ba_gmres_rtp"])
+def test_gateway_gmres_rtp(mex, gpu_ctx, tomo, fn):
+    A, B, b, xt = tomo
+    x, e, r, k = mex(4, fn, A, B, b, xt, 1e-3, 12.0, 1e-2)
+    Ao, Bo = _ops(gpu_ctx, A, B)
+    ref = getattr(hgmres, fn)(Ao, Bo, b, xt, 1e-3, 12, 1e-2, ctx=gpu_ctx)
+    assert int(k) == ref[3] and e.shape == (ref[3],)          # error_norm(1:niters)
+    np.testing.assert_array_equal(x, ref[0])
+    np.testing.assert_array_equal(e, ref[1])
+    np.testing.assert_array_equal(r, ref[2])
+
+
+@pytest.mark.gpu
+def test_gateway_golub_kahan(mex, gpu_ctx, tomo):
+    A, B, b, xt = tomo
+    Ao, = _ops(gpu_ctx, A)
+    At = Ao.T
+    out = mex(4, "lsqr_solver", A, b, xt, 0.0, 10.0)
+    ref = hgmres.lsqr_solver(Ao, b, xt, 0.0, 10, ctx=gpu_ctx, At=At)
+    for a, r_ in zip(out[:3], ref[:3]):
+        np.testing.assert_array_equal(a, r_)
+    out = mex(5, "lsmr_solver", A, b, np.zeros(0), 1e-6, 10.0)           # x_true = [] -> err_hist NaN
+    ref = hgmres.lsmr_solver(Ao, b, None, 1e-6, 10, ctx=gpu_ctx, At=At)
+    for a, r_ in zip(out[:4], ref[:4]):
+        np.testing.assert_array_equal(a, r_)
+    assert np.all(np.isnan(out[1]))
+    for fn in ("hybrid_lsqr_solver", "hybrid_lsmr_solver"):
+        out = mex(4, fn, A, b, xt, 0.0, 8.0, 1e-2)
+        ref = getattr(hgmres, fn)(Ao, b, xt, 0.0, 8, 1e-2, ctx=gpu_ctx, At=At)
+        for a, r_ in zip(out[:3], ref[:3]):
+            np.testing.assert_array_equal(a, r_)
+
+
+@pytest.mark.gpu
+def test_gateway_gcv(mex, gpu_ctx, tomo):
+    A, B, b, xt = tomo
+    Ao, Bo = _ops(gpu_ctx, A, B)
+    m = A.shape[0]
+    for side in ("ab", "ba"):
+        g, = mex(1, "gcv_function", 1e-3, A, B, b, float(m), 8.0, side)
+        assert g[0] == hgmres.gcv_function(1e-3, Ao, Bo, b, m, 8, side, ctx=gpu_ctx)
+        H, beta, kd = mex(3, "arnoldi", A, B, b, 8.0, side)
+        Hr, br, kr = hgmres.arnoldi(Ao, Bo, b, 8, side, ctx=gpu_ctx)
+        np.testing.assert_array_equal(H, Hr)
+        assert beta[0] == br and int(kd[0]) == kr
+        tm = m if side == "ab" else A.shape[1]
+        lam, gv = mex(2, "gcv_fminbnd", H, beta[0], float(tm), 1e-9, 1e-1, 1e-8)
+        assert (lam[0], gv[0]) == hgmres.gcv_fminbnd(Hr, br, tm, 1e-9, 1e-1, 1e-8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("side,hybrid", [("ab", 1), ("ba", 0)])
+def test_gateway_bounds_eight_outputs(mex, gpu_ctx, side, hybrid):
+    """The reference's dense n = 32 setting (shaw, analyze_regularization.m:5-15): dense operands,
+    the formed DeltaM, eight outputs with phi_iter / dphi_iter as cells."""
+    g = load_golden("shaw32_pipeline.npz")
+    A, E = g["A"], g["E"]
+    Bp = A.T + E
+    dm = A @ E if side == "ab" else E @ A
+    outs = mex(8, "gmres_bounds", side, float(hybrid), A, Bp, g["b"], g["x_true"], 1e-6, 8.0, 1e-4, dm)
+    full = lambda M: sp.csr_matrix((M.reshape(-1), np.tile(np.arange(M.shape[1]), M.shape[0]),
+                                    np.arange(0, M.size + 1, M.shape[1])), shape=M.shape)   # every entry stored
+    Ao, Bo, Do = (hgmres.SparseOperator.from_scipy(full(M), gpu_ctx) for M in (A, Bp, dm))
+    fn = getattr(hgmres, {("ab", 1): "ABgmres_hybrid_bounds", ("ba", 0): "BAgmres_nonhybrid_bounds"}[(side, hybrid)])
+    args = (Ao, Bo, g["b"], g["x_true"], 1e-6, 8) + ((1e-4,) if hybrid else ())
+    ref = fn(*args, Do, ctx=gpu_ctx)
+    k = int(outs[3][0])
+    assert k == ref[3] and len(outs[6]) == k and [len(c) for c in outs[6]] == list(range(1, k + 1))
+    for a, r_ in zip(outs[:3] + outs[4:6], ref[:3] + ref[4:6]):
+        np.testing.assert_array_equal(a, r_)
+    for j in range(k):
+        np.testing.assert_array_equal(outs[6][j], ref[6][j])
+        np.testing.assert_array_equal(outs[7][j], ref[7][j])
+    with pytest.raises(MexError) as e:             # outputs 5-8 without DeltaM
+        mex(8, "gmres_bounds", side, float(hybrid), A, Bp, g["b"], g["x_true"], 1e-6, 8.0, 1e-4)
+    assert e.value.ident == "hgmres:nargout"
+
+
+@pytest.mark.gpu
+def test_gateway_unassigned_x_is_matlabs_error(mex, gpu_ctx):
+    """Breakdown at k = 1 (hybrid_ab_gmres_rtp.m:4,25,33 never assigns x): MATLAB's own error id."""
+    n = 16
+    I = sp.identity(n, format="csc")
+    with pytest.raises(MexError) as e:
+        mex(4, "hybrid_ab_gmres_rtp", I, I, np.ones(n), np.ones(n), 0.0, 5.0, 1e-2)
+    assert e.value.ident == "MATLAB:unassignedOutputs"
