@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="sharded-solve transport: RCCL, or the host all-reduce hook (single-device emulation)")
     ap.add_argument("--same-device", action="store_true", help="run every rank on GPU 0 (shard emulation)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="experiment: per-context numerics option (hgm_ctx_set_option), e.g. mgs_fused=0")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP-event timing")
     # default A: the roofline kernel; timing both classes costs ~11% of the C2 step, A alone ~4%
@@ -167,6 +169,9 @@ def main():
             B.close()
             B = hgmres.SparseOperator.pixel_backprojector(wl["N"], wl["angles"], ctx=ctx, dtype=A.dtype)
         lo, hi, full = 0, A.shape[1], A.shape
+    for o in args.opt:
+        name, val = o.split("=", 1)
+        ctx.set_option(name, float(val))
     for M, t in ((A, args.tune_a), (B, args.tune_b)):
         if t:
             v, g = t.split(":")

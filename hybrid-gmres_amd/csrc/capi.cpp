@@ -484,6 +484,7 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             if (!(v >= 1.0 && v <= 8.0) || v != (double)(int)v) return bad("mgs1 ppl is 1..8");
             n.mgs1_ppl = (int)v;
             break;
+        case HGM_OPT_MGS_FUSED: n.mgs_fused = v != 0.0; break;
         default: return bad("unknown option");
     }
     return HGM_OK;
@@ -506,6 +507,7 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_SYNC_EVENT_FENCE: *v = n.sync_event_fence; break;
         case HGM_OPT_MGS_PPL: *v = n.mgs_ppl; break;
         case HGM_OPT_MGS1_PPL: *v = n.mgs1_ppl; break;
+        case HGM_OPT_MGS_FUSED: *v = n.mgs_fused; break;
         default: return HGM_E_ARG;
     }
     return HGM_OK;

@@ -73,6 +73,7 @@ struct Numerics {
     bool sync_event_fence = false;
     int mgs_ppl = 1;
     int mgs1_ppl = 2;
+    bool mgs_fused = true;          // one-reduction MGS: solve folded into the update kernel
 };
 
 }  // namespace hgm

@@ -815,6 +815,36 @@ __global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* Q, int64_t
     if (t <= 2 * MGS1_CG && row_ok(t)) row_ptr(t)[rb] = (sh[0][t] + sh[1][t]) + (sh[2][t] + sh[3][t]);
 }
 
+// The partial rows of k_mgs1_dots reduced exactly as k_mgs1_solve reduces them (16 lanes per
+// row, the same loads and additions in the same order, so the same bits), NT threads per block.
+template <typename T, int NT>
+__device__ __forceinline__ T mgs1_row_sum(const T* p, int npr, bool ok, int sub) {
+    T acc = 0;
+    for (int base = 0; base < npr; base += 256) {
+        T pv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int i = base + sub + 16 * u;
+            pv[u] = (ok && i < npr) ? p[i] : T(0);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += pv[u];
+    }
+    return row16_sum(acc);
+}
+
+// Arguments of the fused form of k_mgs1_update (HGM_OPT_MGS_FUSED): the update blocks run
+// k_mgs1_solve's reduction and substitution themselves, redundantly per block, so the sweep is
+// two dependent launches (dots, update) instead of three.
+template <typename T>
+struct Mgs1Fused {
+    const T* pr = nullptr;   // partial rows r_0..r_k (npr each)
+    const T* pg = nullptr;   // partial rows of the Gram row k (+ q_k'q_k, q_k'x_true)
+    int npr = 0;
+    T* Gt = nullptr;         // packed Gram triangle kept across the steps (block 0 appends row k)
+    int ngx = 0;             // 2: Gram error monitor rows
+};
+
 // One 1024-thread workgroup.  MODE 0: sum the partial rows and solve.  MODE 1: sum only,
 // red = [r_0..r_k | g_0..g_{k-1}] (multi-GPU all-reduces it).  MODE 2: solve from red.
 // Row c < k+1 is r_c (pr), row k+1+c is g_c (pg); 16 lanes (one DPP row) per partial row.
@@ -849,18 +879,7 @@ __global__ __launch_bounds__(MGS1_SBS) void k_mgs1_solve(int kk, const T* __rest
             const int row = row0 + (t >> 4);
             const bool ok = row < nrow;
             const T* p = row <= kk ? pr + (int64_t)row * npr : pg + (int64_t)(row - kk - 1) * npr;
-            T acc = 0;
-            for (int base = 0; base < npr; base += 256) {
-                T pv[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    const int i = base + sub + 16 * u;
-                    pv[u] = (ok && i < npr) ? p[i] : T(0);
-                }
-#pragma unroll
-                for (int u = 0; u < 16; ++u) acc += pv[u];
-            }
-            acc = row16_sum(acc);
+            const T acc = mgs1_row_sum<T, MGS1_SBS>(p, npr, ok, sub);
             if (sub == 0 && ok) {
                 if (MODE == 1) red[row] = acc;
                 else put(row, acc);
@@ -874,13 +893,14 @@ __global__ __launch_bounds__(MGS1_SBS) void k_mgs1_solve(int kk, const T* __rest
     if ((t >> 6) == 0) mgs1_substitute(kk, sr, sG, hdev);
 }
 
-template <typename T>
+template <typename T, bool FUSED>
 // hpend: Q(:,k) still holds v_k (pending normalisation): q_k = v_k / *hpend is used for the
 // last term and written back (each element by the one thread that updates it).
 __global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, T* Q, int64_t ldq, int kk,
                                                     const T* w, T* v, const T* __restrict__ hdev, T* Hcol,
                                                     T* __restrict__ pout, MdotStage<T> side, const T* hpend,
-                                                    const T* __restrict__ grow, const T* __restrict__ gx, T* qg) {
+                                                    const T* __restrict__ grow, const T* __restrict__ gx, T* qg,
+                                                    Mgs1Fused<T> fz) {
     using T2 = typename V2<T>::t;
     __shared__ T hs[MGS1_MAXC];
     __shared__ T sh[4];
@@ -888,14 +908,49 @@ __global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, T* Q, int
         mdot_side(side, (int)blockIdx.x - nb, sh);
         return;
     }
-    for (int j = threadIdx.x; j <= kk; j += BS) {
-        const T h = hdev[j];
-        hs[j] = h;
-        if (blockIdx.x == 0) st_sys(Hcol + j, h);   // H(0:k, k) -> host ring
+    if (FUSED) {
+        extern __shared__ unsigned char mgs1u_smem[];
+        T* sG = reinterpret_cast<T*>(mgs1u_smem);
+        __shared__ T sr[MGS1_MAXC];
+        __shared__ T sgx[2];
+        const int t = threadIdx.x, sub = t & 15;
+        const int rowk = kk * (kk - 1) / 2;
+        const int nrow = 2 * kk + 1 + fz.ngx;
+        for (int e = t; e < rowk; e += BS) sG[e] = fz.Gt[e];
+        for (int row0 = 0; row0 < nrow; row0 += BS / 16) {
+            const int row = row0 + (t >> 4);
+            const bool ok = row < nrow;
+            const T* p = row <= kk ? fz.pr + (int64_t)row * fz.npr : fz.pg + (int64_t)(row - kk - 1) * fz.npr;
+            const T acc = mgs1_row_sum<T, BS>(p, fz.npr, ok, sub);
+            if (sub == 0 && ok) {
+                if (row <= kk) {
+                    sr[row] = acc;
+                } else if (row > 2 * kk) {
+                    sgx[row - 2 * kk - 1] = acc;
+                } else {
+                    sG[rowk + row - kk - 1] = acc;
+                    if (blockIdx.x == 0) fz.Gt[rowk + row - kk - 1] = acc;
+                }
+            }
+        }
+        __syncthreads();
+        if ((t >> 6) == 0) mgs1_substitute(kk, sr, sG, hs);
+        __syncthreads();
+        if (blockIdx.x == 0) {
+            for (int j = t; j <= kk; j += BS) st_sys(Hcol + j, hs[j]);   // H(0:k, k) -> host ring
+            if (qg)                                                      // Gram error monitor row
+                for (int j = t; j <= kk + 1; j += BS) st_sys(qg + j, j < kk ? sG[rowk + j] : sgx[j - kk]);
+        }
+    } else {
+        for (int j = threadIdx.x; j <= kk; j += BS) {
+            const T h = hdev[j];
+            hs[j] = h;
+            if (blockIdx.x == 0) st_sys(Hcol + j, h);   // H(0:k, k) -> host ring
+        }
+        if (qg && blockIdx.x == 0)                      // Gram error monitor row -> host ring
+            for (int j = threadIdx.x; j <= kk + 1; j += BS) st_sys(qg + j, j < kk ? grow[j] : gx[j - kk]);
+        __syncthreads();
     }
-    if (qg && blockIdx.x == 0)                      // Gram error monitor row -> host ring
-        for (int j = threadIdx.x; j <= kk + 1; j += BS) st_sys(qg + j, j < kk ? grow[j] : gx[j - kk]);
-    __syncthreads();
     const int64_t n2 = n >> 1, stride = (int64_t)nb * BS;
     const T2* w2 = reinterpret_cast<const T2*>(w);
     T2* v2 = reinterpret_cast<T2*>(v);
@@ -1047,7 +1102,20 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
         T* hdev = c->buf<T>("mgs1_h", MGS1_MAXC + 2);
         const size_t lds = sizeof(T) * ((size_t)kk * (kk + 1) / 2 + 1);
         k_mgs1_dots<T><<<npr * ncg + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1, pend_h, xe);
-        if (dist) {
+        const int nb = gemv_blocks(n, mgs_ppl(c));
+        T* pout = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
+        const bool fused = !dist && c->num.mgs_fused;
+        Mgs1Fused<T> fz;
+        if (fused) {
+            fz.pr = pr;
+            fz.pg = pg;
+            fz.npr = npr;
+            fz.Gt = Gt;
+            fz.ngx = xe ? 2 : 0;
+            k_mgs1_update<T, true><<<nb + s2.blocks(), BS, lds, st>>>(n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout,
+                                                                      s2, pend_h, nullptr, nullptr, xe ? qg : nullptr,
+                                                                      fz);
+        } else if (dist) {
             T* redd = c->buf<T>("mgs1_red", 2 * MGS1_MAXC + 2);
             k_mgs1_solve<T, 1><<<1, MGS1_SBS, 0, st>>>(kk, pr, pg, npr, redd, Gt, hdev, nullptr);
             allreduce(c, redd, 2 * kk + 1);
@@ -1055,10 +1123,10 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
         } else {
             k_mgs1_solve<T, 0><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, nullptr, Gt, hdev, gx);
         }
-        const int nb = gemv_blocks(n, mgs_ppl(c));
-        T* pout = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
-        k_mgs1_update<T><<<nb + s2.blocks(), BS, 0, st>>>(n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout, s2, pend_h,
-                                                        Gt + (size_t)kk * (kk - 1) / 2, gx, xe ? qg : nullptr);
+        if (!fused)
+            k_mgs1_update<T, false><<<nb + s2.blocks(), BS, 0, st>>>(n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout, s2,
+                                                                     pend_h, Gt + (size_t)kk * (kk - 1) / 2, gx,
+                                                                     xe ? qg : nullptr, fz);
         if (defer && !dist && kk + 2 <= MGS1_MAXC) {   // the next step must be one-reduction too
             // the next step's SpMVs divide by H(kk+1,kk) in their epilogues
             HGM_HIP(hipGetLastError());

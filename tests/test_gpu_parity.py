@@ -505,6 +505,21 @@ def test_mgs_one_reduction_form(gpu_ctx, N, na, maxit):
         assert np.array_equal(res[form]["hba_H"], again["hba_H"])
 
 
+@pytest.mark.parametrize("N,na,maxit", [(64, 91, 80), (512, 30, 20)])
+def test_mgs_fused_solve_is_bitwise(gpu_ctx, N, na, maxit):
+    """HGM_OPT_MGS_FUSED (default): the one-reduction sweep's partial-row reduction and
+    triangular solve run redundantly in every update block (2 launches per step) instead of in
+    a one-block solve kernel (3).  Same summation code, so x, H and both histories are bitwise
+    those of the unfused form -- with the Gram error monitor, the pending normalisation (n-space)
+    and the kept m-space products (abn), up to 80 steps (both substitution rows per lane)."""
+    P = tomo_problem(N, na, noise=1e-2, seed=0)
+    tags = ("hab", "hba", "abn")
+    a = _gm_solve(gpu_ctx, P, maxit, tags, mgs_single=0, mgs_fused=1)
+    b = _gm_solve(gpu_ctx, P, maxit, tags, mgs_single=0, mgs_fused=0)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+
+
 @pytest.mark.parametrize("N,na,maxit,stop", [(64, 90, 20, False), (64, 91, 80, False), (64, 90, 20, True)])
 def test_gram_error_monitor(gpu_ctx, N, na, maxit, stop):
     """Gram error monitor: the error history as x_true'x_true - 2y'(Q'x_true)
