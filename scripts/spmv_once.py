@@ -2,7 +2,8 @@
 PMC passes (FETCH_SIZE / WRITE_SIZE / TCC_HIT / TCC_MISS) in scripts/profile_spmv.sh.
 Prints the launch order so counter rows can be matched to cases.
 usage: python scripts/spmv_once.py CFG [A:v:g[:band_w:band_group] ...] [--reps 3]
-(stored pixel order of the generated operator: env HGM_SIDDON_TILE / HGM_SIDDON_SUPER)
+(stored pixel order of the generated operator: env HGM_SIDDON_TILE / HGM_SIDDON_SUPER;
+ HGM_DTYPE=f32 for the fp32 operator)
 """
 import ctypes as C
 import os
@@ -29,17 +30,19 @@ def main():
     ctx = hgmres.Context(0)
     N, na = CONFIGS[cfg]
     order = (int(os.environ.get("HGM_SIDDON_TILE", "1")), int(os.environ.get("HGM_SIDDON_SUPER", "0")))
-    A = hgmres.SparseOperator.siddon(N, na, ctx=ctx, order=order)
+    f32 = os.environ.get("HGM_DTYPE") == "f32"
+    es = 4 if f32 else 8
+    A = hgmres.SparseOperator.siddon(N, na, ctx=ctx, order=order, dtype=L.HGM_F32 if f32 else L.HGM_F64)
     B = A.T
     ops = {"A": A, "B": B}
     bufs = {}
     for nm, M in ops.items():
         rows, cols = M.shape
         xd, yd = C.c_void_p(), C.c_void_p()
-        lib.hgm_dev_alloc(ctx.handle, 8 * cols, C.byref(xd))
-        lib.hgm_dev_alloc(ctx.handle, 8 * rows, C.byref(yd))
-        ones = np.ones(cols)
-        lib.hgm_memcpy_h2d(ctx.handle, xd, ones.ctypes.data_as(C.c_void_p), 8 * cols)
+        lib.hgm_dev_alloc(ctx.handle, es * cols, C.byref(xd))
+        lib.hgm_dev_alloc(ctx.handle, es * rows, C.byref(yd))
+        ones = np.ones(cols, dtype=np.float32 if f32 else np.float64)
+        lib.hgm_memcpy_h2d(ctx.handle, xd, ones.ctypes.data_as(C.c_void_p), es * cols)
         bufs[nm] = (xd, yd)
     for case in cases:
         parts = case.split(":")
