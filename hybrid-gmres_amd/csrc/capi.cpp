@@ -485,6 +485,7 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             n.mgs1_ppl = (int)v;
             break;
         case HGM_OPT_MGS_FUSED: n.mgs_fused = v != 0.0; break;
+        case HGM_OPT_LSQR_DEV: n.lsqr_dev = v != 0.0; break;
         default: return bad("unknown option");
     }
     return HGM_OK;
@@ -508,6 +509,7 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_MGS_PPL: *v = n.mgs_ppl; break;
         case HGM_OPT_MGS1_PPL: *v = n.mgs1_ppl; break;
         case HGM_OPT_MGS_FUSED: *v = n.mgs_fused; break;
+        case HGM_OPT_LSQR_DEV: *v = n.lsqr_dev; break;
         default: return HGM_E_ARG;
     }
     return HGM_OK;

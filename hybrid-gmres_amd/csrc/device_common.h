@@ -155,6 +155,12 @@ __device__ __forceinline__ T apply_epi_zv(T t, T a, T zi, int64_t i, const PendN
     return t;
 }
 
+// The epilogue coefficient: the host's scalar, or sqrt of a device sum of squares (PendNorm::asq)
+template <typename T>
+__device__ __forceinline__ T pn_coef(const PendNorm<T>& pn, T a) {
+    return pn.asq ? (T)sqrt((double)*pn.asq) : a;
+}
+
 // h of the pending normalisation, in two halves so that its loads are issued at kernel
 // start and overlap the product: pn_pre returns this thread's share (EPI_DIVH: its
 // strided partial sum, the order of reduce_parts; EPI_ADDQ: h itself), pn_fin the value.

@@ -74,6 +74,7 @@ struct Numerics {
     int mgs_ppl = 1;
     int mgs1_ppl = 2;
     bool mgs_fused = true;          // one-reduction MGS: solve folded into the update kernel
+    bool lsqr_dev = true;           // LSQR: device-resident beta/alpha/rotation (no host round trip)
 };
 
 }  // namespace hgm
@@ -228,6 +229,9 @@ struct PendNorm {
     T* hdev = nullptr;
     T* hring = nullptr;
     T* q = nullptr;
+    // device-resident epilogue coefficient (EPI_ADD / EPI_SUB): a = (T)sqrt((double)*asq), the
+    // bits the host computes from the same sum of squares (device-side Golub-Kahan scalars)
+    const T* asq = nullptr;
 };
 
 int pick_group(int64_t rows, int64_t nnz);
@@ -306,6 +310,17 @@ template <typename T> void div_scalar(hgm_ctx* c, int64_t n, const T* in, T* out
 // v = v / norm(v) on the device, *nrm_out = norm(v) (system-scope store, e.g. the host ring)
 template <typename T> void normalize_to(hgm_ctx* c, int64_t n, T* v, T* nrm_out);
 template <typename T> void lsqr_update(hgm_ctx* c, int64_t n, T* x, T* w, const T* v, T a, T b);
+// Device-resident LSQR scalars (kernels.hip): the Givens rotation from the sums of squares *ssb
+// (beta^2) and *ssa (alpha^2) in one thread (st = [rho_bar, phi_bar, stop]); the step
+// v /= alpha, x += coef0 w, w = v - coef1 w (skipped after the stop), with ||x - x_true||^2 fused
+// into err_out when xt != NULL; out = in / sqrt(*ss).
+template <typename T>
+void lsqr_rot(hgm_ctx* c, const T* ssb, const T* ssa, double* st, T* coef, double* phib_hist, int k, double nb,
+              double tol);
+template <typename T>
+void lsqr_step(hgm_ctx* c, int64_t n, T* x, T* w, T* v, const T* ssa, const T* coef, const double* st, int k,
+               const T* xt, T* err_out);
+template <typename T> void div_sqrt(hgm_ctx* c, int64_t n, const T* in, T* out, const T* ss);
 template <typename T>
 void lsmr_update(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, const T* v, T c_hbar, T c_x, T c_h,
                  bool first);

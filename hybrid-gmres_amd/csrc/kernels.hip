@@ -1314,6 +1314,101 @@ template <typename T> void lsqr_update(hgm_ctx* c, int64_t n, T* x, T* w, const 
     HGM_HIP(hipGetLastError());
 }
 
+// ------------------------------------------------------------------------------
+// Device-resident LSQR scalars (lsqr_solver.m:22-46 without host round trips): the Givens
+// rotation of :31-38 in one thread, in double, exactly as the host loop computes it from the
+// same sums of squares, and the stop test of :44-46 as a flag the update kernel honours.
+// st: [rho_bar, phi_bar, stop] (stop = iteration+1 of the first res <= tol, 0 while running).
+// ------------------------------------------------------------------------------
+template <typename T>
+__global__ void k_lsqr_rot(const T* ssb, const T* ssa, double* st, T* coef, double* phib_hist, int k, double nb,
+                           double tol) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const double beta = sqrt((double)*ssb);                  // :23
+    const double alpha = sqrt((double)*ssa);                 // :27
+    const double rho_bar = st[0], phi_bar = st[1];
+    const double rho = sqrt(rho_bar * rho_bar + beta * beta);   // :31
+    const double cs = rho_bar / rho;                         // :32
+    const double sn = beta / rho;                            // :33
+    const double theta = sn * alpha;                         // :34
+    st[0] = -cs * alpha;                                     // :35
+    const double phi = cs * phi_bar;                         // :37
+    const double pb = sn * phi_bar;                          // :38
+    st[1] = pb;
+    coef[0] = (T)(phi / rho);                                // :40
+    coef[1] = (T)(theta / rho);                              // :41
+    phib_hist[k] = pb;
+    if (st[2] == 0.0 && fabs(pb) / nb <= tol) st[2] = (double)(k + 1);   // :44-46
+}
+
+// v = v_hat / alpha (alpha = sqrt(*ssa)), then x += (phi/rho) w ; w = v - (theta/rho) w
+// (lsqr_solver.m:28,40-41), skipped once an earlier iteration met the stop test; with parts,
+// also the partials of ||x - x_true||^2 (:43) in k_reduce_partial<T, 2>'s order (same bits).
+template <typename T>
+__global__ __launch_bounds__(BS) void k_lsqr_step(int64_t n, T* __restrict__ x, T* __restrict__ w, T* __restrict__ v,
+                                                  const T* ssa, const T* coef, const double* st, int k,
+                                                  const T* __restrict__ xt, T* __restrict__ parts) {
+    __shared__ T sh[4];
+    const T alpha = (T)sqrt((double)*ssa);
+    const bool live = !(st[2] != 0.0 && st[2] < (double)(k + 1));
+    const T a = coef[0], b = coef[1];
+    T acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+        const T vi = v[i] / alpha;
+        v[i] = vi;
+        T xi = x[i];
+        if (live) {
+            const T wi = w[i];
+            const T p = a * wi;
+            xi = xi + p;
+            x[i] = xi;
+            const T q = b * wi;
+            w[i] = vi - q;
+        }
+        if (parts) {
+            const T d = xi - xt[i];
+            acc += d * d;
+        }
+    }
+    if (parts) {
+        const T tot = block_sum_all(acc, sh);
+        if (threadIdx.x == 0) parts[blockIdx.x] = tot;
+    }
+}
+
+// out = in / (T)sqrt((double)*ss)
+template <typename T>
+__global__ __launch_bounds__(BS) void k_div_sqrt(int64_t n, const T* __restrict__ in, T* __restrict__ out, const T* ss) {
+    const T s = (T)sqrt((double)*ss);
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = in[i] / s;
+}
+
+template <typename T>
+void lsqr_rot(hgm_ctx* c, const T* ssb, const T* ssa, double* st, T* coef, double* phib_hist, int k, double nb,
+              double tol) {
+    k_lsqr_rot<T><<<1, 64, 0, c->stream>>>(ssb, ssa, st, coef, phib_hist, k, nb, tol);
+    HGM_HIP(hipGetLastError());
+}
+
+template <typename T>
+void lsqr_step(hgm_ctx* c, int64_t n, T* x, T* w, T* v, const T* ssa, const T* coef, const double* st, int k,
+               const T* xt, T* err_out) {
+    // the error partials keep reduce_to's layout: one launch for short vectors stays separate
+    const bool fuse = xt && n > SINGLE_MAX && !c->num.parity;
+    const int np = fuse ? parts_for(n) : grid_for(n);
+    T* parts = fuse ? c->buf<T>("red_parts", MAX_PARTS) : nullptr;
+    k_lsqr_step<T><<<np, BS, 0, c->stream>>>(n, x, w, v, ssa, coef, st, k, xt, parts);
+    if (fuse) k_finalize<T><<<1, BS, 0, c->stream>>>(parts, np, err_out);
+    HGM_HIP(hipGetLastError());
+    if (xt && !fuse) sumsq_diff<T>(c, n, x, xt, err_out);
+}
+
+template <typename T>
+void div_sqrt(hgm_ctx* c, int64_t n, const T* in, T* out, const T* ss) {
+    k_div_sqrt<T><<<grid_for(n), BS, 0, c->stream>>>(n, in, out, ss);
+    HGM_HIP(hipGetLastError());
+}
+
 // lsmr_solver.m:61-67
 template <typename T, bool FIRST>
 __global__ __launch_bounds__(BS) void k_lsmr_update(int64_t n, T* __restrict__ x, T* __restrict__ h,
@@ -1453,6 +1548,9 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
     template void gemv<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, int);       \
     template void div_scalar<T>(hgm_ctx*, int64_t, const T*, T*, T);                           \
     template void lsqr_update<T>(hgm_ctx*, int64_t, T*, T*, const T*, T, T);                   \
+    template void lsqr_rot<T>(hgm_ctx*, const T*, const T*, double*, T*, double*, int, double, double); \
+    template void lsqr_step<T>(hgm_ctx*, int64_t, T*, T*, T*, const T*, const T*, const double*, int, const T*, T*); \
+    template void div_sqrt<T>(hgm_ctx*, int64_t, const T*, T*, const T*);                     \
     template void lsmr_update<T>(hgm_ctx*, int64_t, T*, T*, T*, const T*, T, T, T, bool);      \
     template void lsmr_monitor<T>(hgm_ctx*, int64_t, const T*, const T*, double, double, double*, double*, \
                                   double*, const T*, double, double, double, bool, double*);   \

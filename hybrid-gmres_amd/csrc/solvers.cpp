@@ -734,7 +734,49 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     // device and is read once after the loop instead of once per iteration
     T* errh = hybrid ? nullptr : c->buf<T>("lsqr_errh", maxit);
     int k = 0;
-    for (k = 0; k < maxit; ++k) {
+    // Device-resident scalars (single rank, production kernels): beta and alpha stay on the
+    // device as sums of squares, the SpMV epilogues read them there (PendNorm::asq), and the
+    // Givens rotation (:31-38) and the stop test (:44-46) run in a one-thread kernel, in the same
+    // double arithmetic as the host loop below -- the same bits, with no host round trip per
+    // iteration.  The host reads the stop flag once per batch of iterations (none when tol <= 0
+    // cannot stop early); an iteration enqueued past the stop leaves x and w untouched.
+    const bool dev_scalars = !hybrid && !parity && !dist_n(c) && c->num.lsqr_dev;
+    if (dev_scalars) {
+        double* st = c->buf<double>("lsqr_st", 4);
+        double* phib = c->buf<double>("lsqr_phib", maxit);
+        T* coef = c->buf<T>("lsqr_coef", 2);
+        const double st0[4] = {rho_bar, phi_bar, 0.0, 0.0};
+        h2d(c, st, st0, sizeof(st0));
+        PendNorm<T> pa, pb;
+        pa.asq = sl + S_ALPHA;                     // A*v - alpha*u
+        pb.asq = sl + S_BETA;                      // A'*u - beta*v
+        const int batch = tol > 0 ? 8 : maxit;
+        int stop = 0;
+        for (k = 0; k < maxit && stop == 0;) {
+            const int kend = std::min(maxit, k + batch);
+            for (; k < kend; ++k) {
+                spmv<T>(c, A, v, t, EPI_SUB, T(0), u, KC_SPMV_A, nullptr, &pa);     // :22
+                sumsq<T>(c, m, t, sl + S_BETA);                                      // :23
+                div_sqrt<T>(c, m, t, u, sl + S_BETA);                                // :24
+                spmv<T>(c, At, u, v, EPI_SUB, T(0), v, KC_SPMV_B, nullptr, &pb);     // :26
+                sumsq<T>(c, n, v, sl + S_ALPHA);                                     // :27
+                lsqr_rot<T>(c, sl + S_BETA, sl + S_ALPHA, st, coef, phib, k, nb, tol);   // :31-38, :44-46
+                lsqr_step<T>(c, n, x, w, v, sl + S_ALPHA, coef, st, k, xt, errh + k);     // :28, :40-41, :43
+            }
+            double sv = 0;
+            Reader rs(c);
+            rs.add(&sv, st + 2, sizeof(double));
+            rs.go();
+            stop = (int)sv;
+        }
+        k = stop > 0 ? stop - 1 : maxit;
+        std::vector<double> pbh(maxit);
+        Reader rh(c);
+        rh.add(pbh.data(), phib, sizeof(double) * maxit);
+        rh.go();
+        for (int i = 0; i < maxit && i <= k; ++i) res[i] = std::fabs(pbh[i]) / nb;   // :44
+    }
+    for (; !dev_scalars && k < maxit; ++k) {
         // :22-24  u_hat = A*v - alpha*u ; beta = norm(u_hat) ; u = u_hat / beta
         apply_A<T>(c, A, v, t, EPI_SUB, (T)alpha, u);
         sumsq<T>(c, m, t, sl + S_BETA);

@@ -119,6 +119,7 @@ __global__ __launch_bounds__(BS) void k_spmv(int64_t rows, const int64_t* __rest
     const int64_t row = blk * RPB + threadIdx.x / G;
     const int gl = threadIdx.x & (G - 1);
     const T hpre = pn_pre<T, EPI>(pn);
+    if constexpr (EPI == EPI_ADD || EPI == EPI_SUB) a = pn_coef<T>(pn, a);
     T zr = T(0);   // epilogue operand, loaded up front
     if constexpr (EPI != EPI_NONE && EPI != EPI_DIVH) {
         if (gl == 0 && row < rows) zr = z[row];
@@ -247,6 +248,7 @@ __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, c
     T h = T(1);
     auto bookkeeping = [&]() {
         h = pn_pre<T, EPI>(pn);
+        if constexpr (EPI == EPI_ADD || EPI == EPI_SUB) a = pn_coef<T>(pn, a);
         s_begin = fo[k];
         s_end = fo[k + 1];
         q = s_begin + gid;
@@ -393,6 +395,7 @@ __global__ __launch_bounds__(BS) void k_stream_fixup(int64_t nnz, int64_t nchunk
                                                      const T* __restrict__ tail, PendNorm<T> pn) {
     static_assert(EPI != EPI_DIVH, "EPI_DIVH is applied by the band reduction or the row kernel");
     const T h = pn_pre<T, EPI>(pn);
+    if constexpr (EPI == EPI_ADD || EPI == EPI_SUB) a = pn_coef<T>(pn, a);
     for (int64_t k = (int64_t)blockIdx.x * BS + threadIdx.x; k < nchunks; k += (int64_t)gridDim.x * BS) {
         const int64_t s_begin = fo[k], s_end = fo[k + 1];
         if (s_end <= s_begin) continue;
@@ -422,6 +425,7 @@ __global__ __launch_bounds__(BS) void k_band_reduce(int64_t rows, int nbands, co
                                                     PendNorm<T> pn) {
     __shared__ T hsh[4];
     const T h = pn_fin<T, EPI>(pn, pn_pre<T, EPI>(pn), hsh);
+    if constexpr (EPI == EPI_ADD || EPI == EPI_SUB) a = pn_coef<T>(pn, a);
     for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BS) {
         T s = 0;
         for (int b = 0; b < nbands; ++b) s += ypart[(int64_t)b * rows + r];

@@ -107,9 +107,11 @@ enum hgm_ctx_option {
     HGM_OPT_SYNC_EVENT_FENCE = 11, /* system-scope release on the pipeline events [0] */
     HGM_OPT_MGS_PPL = 12,          /* row pairs per lane of the MGS update / pass kernels [1] */
     HGM_OPT_MGS1_PPL = 13,         /* row pairs per lane of the one-reduction dots kernel [2] */
-    HGM_OPT_MGS_FUSED = 14         /* one-reduction MGS (single rank): the partial-row reduction and the
+    HGM_OPT_MGS_FUSED = 14,        /* one-reduction MGS (single rank): the partial-row reduction and the
                                       triangular solve run in the update kernel's prologue, redundantly per
                                       block (2 launches per sweep), instead of a one-block solve kernel [1] */
+    HGM_OPT_LSQR_DEV = 15          /* lsqr_solver (single rank): beta, alpha, the Givens rotation and the stop
+                                      test stay on the device (same bits, no host round trip per iteration) [1] */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for

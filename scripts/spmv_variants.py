@@ -2,7 +2,8 @@
 variant:group; give the creation default explicitly, e.g. C2 A 1:16, B 0:8), HIP events on the library stream,
 alternating the choices `rounds` times.  Prints per-choice averages and whether each choice's
 product is bitwise the auto one.
-usage: python scripts/spmv_variants.py c2 reps rounds A=1:16,26:4,24:8 B=0:8,26:4"""
+usage: python scripts/spmv_variants.py c2 reps rounds A=1:16,26:4,24:8 B=0:8,26:4
+(v:g:band_width:band_group also re-bands the operator first)"""
 import ctypes as C
 import json
 import os
@@ -40,8 +41,10 @@ def main():
         ys = {}
         for r in range(rounds):
             for o in opts:
-                v, g = (int(t) for t in o.split(":"))
-                M.tune(v, g)
+                parts = [int(t) for t in o.split(":")]
+                if len(parts) >= 4:                      # v:g:band_width:band_group
+                    M.set_bands(parts[2], parts[3])
+                M.tune(parts[0], parts[1])
                 for _ in range(3):
                     lib.hgm_spmv(ctx.handle, M._h, xd, yd)
                 ctx.kernel_timing(True)

@@ -505,6 +505,32 @@ def test_mgs_one_reduction_form(gpu_ctx, N, na, maxit):
         assert np.array_equal(res[form]["hba_H"], again["hba_H"])
 
 
+@pytest.mark.parametrize("N,na,dtype,stop", [(64, 90, "f64", False), (64, 90, "f64", True), (512, 30, "f64", True),
+                                             (512, 30, "f32", False), (24, 12, "f64", True)])
+def test_lsqr_device_scalars_are_bitwise(gpu_ctx, N, na, dtype, stop):
+    """HGM_OPT_LSQR_DEV (default): beta, alpha, the Givens rotation and the stop test of
+    lsqr_solver.m:22-46 on the device (SpMV epilogues read the coefficients there) give bitwise
+    the host-driven loop's x and histories -- including a `tol` stop mid-batch (the iterations
+    enqueued past it must leave x alone), fp32, and a vector short enough for the one-launch
+    error reduction."""
+    P = tomo_problem(N, na, noise=1e-2, seed=0)
+    dt = hgmres._lib.HGM_F32 if dtype == "f32" else hgmres._lib.HGM_F64
+    A = hgmres.SparseOperator.from_scipy(P.A, gpu_ctx, dtype=dt)
+    maxit = 20
+    tol = 0.0
+    if stop:
+        with gpu_ctx.options(lsqr_dev=0):
+            r = hgmres.lsqr_solver(A, P.b, P.x_true, 0.0, maxit, ctx=gpu_ctx)[2]
+        tol = float(r[10]) * (1 + 1e-12)      # stops at iteration 11 (inside the second batch of 8)
+    out = {}
+    for mode in (1, 0):
+        with gpu_ctx.options(lsqr_dev=mode):
+            out[mode] = hgmres.lsqr_solver(A, P.b, P.x_true, tol, maxit, ctx=gpu_ctx)
+    assert out[1][3] == out[0][3] and (not stop or out[1][3] == 11)
+    for a, b in zip(out[1][:3], out[0][:3]):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("N,na,maxit", [(64, 91, 80), (512, 30, 20)])
 def test_mgs_fused_solve_is_bitwise(gpu_ctx, N, na, maxit):
     """HGM_OPT_MGS_FUSED (default): the one-reduction sweep's partial-row reduction and
