@@ -330,7 +330,12 @@ int64_t auto_band_width(const hgm_mat* M) {
     if ((double)M->cols * vs <= 4.0 * 1024 * 1024) return 0;
     // only long-row operators benefit (the short pixel-major rows of B gather an L2-resident y)
     if (M->rows > 0 && (double)M->nnz / (double)M->rows < 64) return 0;
-    // tiled pixel order: 256 Ki pixels (2 MiB fp64 x-slice: compact tile strips / blocks)
+    // tiled pixel order (tile-column-major): a strip of 64 pixel columns, 64 N pixels.  The paged
+    // stream kernel's sweeps (profiles/r2_c{3,4}_bands*.log) put the optimum there at both sizes:
+    // C4 (N = 4096) 262,144 pixels, 2.20 ms against 2.25 (128 Ki) and 2.38 (512 Ki); C3
+    // (N = 2048) 131,072 pixels, 254-257 us against 269 (256 Ki) and 259 (64 Ki).
+    if (!M->col_order.trivial() && M->col_order.super == 0) return (int64_t)64 * M->col_order.N;
+    // super-blocks: 256 Ki pixels (2 MiB fp64 x-slice)
     if (!M->col_order.trivial()) return (int64_t)(1 << 18);
     return (int64_t)(1 << 17);   // 128 Ki pixels = 1 MiB fp64 x-slice per band
 }
