@@ -75,6 +75,7 @@ struct Numerics {
     int mgs1_ppl = 2;
     bool mgs_fused = true;          // one-reduction MGS: solve folded into the update kernel
     bool lsqr_dev = true;           // LSQR: device-resident beta/alpha/rotation (no host round trip)
+    bool paged16 = true;            // streaming SpMV: paged gathers also for 16-bit-index operators
 };
 
 }  // namespace hgm

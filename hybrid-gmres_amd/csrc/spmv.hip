@@ -677,7 +677,9 @@ static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int ep
         band_reduce<T>(c, M, yp, y, epi, a, z, pn);
     } else {
         SegIndex si{M->nnz, M->rows, stream_chunks(M->nnz), M->rp, M->cfo};
-        if (M->ci16)
+        // 16-bit column indices (<= 65,536 columns) unless the paged gathers are on: those read
+        // 16-bit page-local indices instead, and only chunks past the page limit read M->ci
+        if (M->ci16 && !(pg.pptr && c->num.paged16))
             spmv_stream<T, uint16_t>(c, true, si, M->sgroup, nt, M->ci16, reinterpret_cast<const T*>(M->val), x, y,
                                      epi, a, z, pn);
         else

@@ -207,6 +207,10 @@ def test_paged_stream_spmv_bitwise(gpu_ctx, P64, group, dtype):
             Mo.tune(8 | 2 | 16, group)
             y1 = Mo @ x
             assert np.array_equal(y0, y1), (M.shape, bands, dtype)
+            if M.shape[1] <= 65536 and not bands:     # 16-bit-index operators: paged16 on / off
+                with gpu_ctx.options(paged16=0):
+                    y2 = Mo @ x
+                assert np.array_equal(y1, y2), (M.shape, dtype)
     if dtype == 0:
         Ao = hgmres.SparseOperator.from_scipy(P64.A, gpu_ctx)
         Bo = hgmres.SparseOperator.from_scipy(P64.B, gpu_ctx)
