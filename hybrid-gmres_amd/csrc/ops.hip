@@ -42,7 +42,8 @@ __global__ __launch_bounds__(BS) void k_rebase(int64_t n, const int64_t* __restr
 // rows [lo, hi) of M as a new operator (same columns): B_g = B(P_g,:) of a pixel shard
 hgm_mat* row_slice(hgm_ctx* c, const hgm_mat* M, int64_t lo, int64_t hi) {
     HGM_REQUIRE(0 <= lo && lo <= hi && hi <= M->rows, "row_slice: need 0 <= lo <= hi <= rows");
-    HGM_REQUIRE(M->row_order.trivial(), "row_slice: rows must be stored in the reference order");
+    // tiled rows: [lo, hi) are STORED positions, and the slice numbers its rows in that stored
+    // order (a shard-local index space, reported as the trivial order)
     hipStream_t st = c->stream;
     int64_t b[2];
     HGM_HIP(hipMemcpy(&b[0], M->rp + lo, sizeof(int64_t), hipMemcpyDeviceToHost));

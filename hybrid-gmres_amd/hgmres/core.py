@@ -180,6 +180,25 @@ def auto_pixel_order(N):
     return (4 if N % 4 == 0 else 1), 0
 
 
+def stored_pixel_index(N, tile, super_block=0):
+    """Stored position of every reference pixel p = r + c*N of an N x N image in the tiled
+    order (N, tile, super_block) (csrc/ops.hip pixel_index): super x super blocks column-major,
+    tile x tile tiles inside in tile-column-major order, column-major inside a tile."""
+    p = np.arange(N * N, dtype=np.int64)
+    r, c = p % N, p // N
+
+    def tiled(S, rr, cc):
+        if tile <= 1:
+            return rr + cc * S
+        tr, tc = rr // tile, cc // tile
+        return ((tc * (S // tile) + tr) * tile + (cc % tile)) * tile + (rr % tile)
+
+    if super_block <= 1:
+        return tiled(N, r, c)
+    S = super_block
+    return ((c // S) * (N // S) + (r // S)) * S * S + tiled(S, r % S, c % S)
+
+
 class SparseOperator:
     """A CSR operator resident in HBM (``hgm_mat``)."""
 

@@ -158,7 +158,10 @@ HGM_API int hgm_mat_create_csc(hgm_ctx* ctx, int64_t rows, int64_t cols, int64_t
 HGM_API int hgm_mat_transpose(hgm_ctx* ctx, const hgm_mat* in, hgm_mat** out);
 /* Rows [lo, hi) of `in` as a new device operator with the same columns (the pixel
  * shard B_g = B(P_g,:) of SURVEY.md §8(e); A_g = A(:,P_g) is then hgm_mat_transpose of
- * it).  `in`'s rows must be stored in the reference order. */
+ * it).  When `in`'s rows are stored tiled (hgm_mat_create_siddon_ordered), [lo, hi) are
+ * STORED positions and the slice keeps their stored order as its own (reference) row order:
+ * a shard of whole tile columns keeps the tiled gather locality (hgmres.core.stored_pixel_index
+ * maps reference pixels to stored positions). */
 HGM_API int hgm_mat_row_slice(hgm_ctx* ctx, const hgm_mat* in, int64_t lo, int64_t hi, hgm_mat** out);
 /* Parallel-beam Siddon projector generated on the device (ray-major CSR,
  * bit-compatible geometry with hgmres.problems.siddon_projector). */

@@ -69,7 +69,22 @@ def main():
     B32 = hgmres.SparseOperator.from_scipy(B_g, ctx, dtype=1)
     x, e, r, k = hgmres.lsqr_solver(A32, P.b, xt, 0.0, 4, ctx=ctx, At=B32)
     res.update(lsqr32_x=x, lsqr32_res=r, lsqr32_err=e)
-    np.savez(os.path.join(out, f"rank{rank}_of{world}.npz"), lo=lo, hi=hi, **res)
+    # the device-generated 4 x 4-tiled operator sharded in STORED order (bench.py build_shard):
+    # B_g = hgm_mat_row_slice of the tiled B over whole tile columns, A_g its transpose
+    from hgmres.core import stored_pixel_index
+    Af = hgmres.SparseOperator.siddon(64, 90, ctx=ctx, order=(4, 0))
+    n, col = Af.shape[1], 4 * 64
+    bounds = [0] + [int(round(g * (n // col) / world)) * col for g in range(1, world)] + [n]
+    tlo, thi = bounds[rank], bounds[rank + 1]
+    B2 = Af.T.row_slice(tlo, thi)
+    A2 = B2.T
+    xs = np.empty(n)
+    xs[stored_pixel_index(64, 4, 0)] = P.x_true
+    out_ = hgmres.ABgmres_nonhybrid_bounds(A2, B2, P.b, xs[tlo:thi], 0.0, 12, ctx=ctx, return_H=True)
+    res.update(tabn_x=out_[0], tabn_res=out_[2], tabn_err=out_[1], tabn_H=out_[-1])
+    x, e, r, k, H = hgmres.hybrid_ba_gmres_rtp(A2, B2, P.b, xs[tlo:thi], 0.0, 15, 1e-2, ctx=ctx, return_H=True)
+    res.update(thba_x=x, thba_res=r, thba_err=e, thba_H=H)
+    np.savez(os.path.join(out, f"rank{rank}_of{world}.npz"), lo=lo, hi=hi, tlo=tlo, thi=thi, **res)
     if conn is not None:
         conn.close()
     ctx.close()

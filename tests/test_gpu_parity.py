@@ -803,3 +803,14 @@ def test_shard_emulation_two_ranks(tmp_path):
     for tag in ("hba", "abn", "hab"):
         H_ok(o[0][f"{tag}_H"], s[f"{tag}_H"])
         assert np.array_equal(o[0][f"{tag}_H"], o[1][f"{tag}_H"])
+    # tiled shards in stored order (bench.py build_shard): the 2-rank solves match the
+    # 1-rank solve of the same tiled operator, whose x (stored order) is the reference-order solve's
+    from hgmres.core import stored_pixel_index
+    perm = stored_pixel_index(64, 4, 0)
+    for tag, ref in (("tabn", "abn"), ("thba", "hba")):
+        x = np.concatenate([o[0][f"{tag}_x"], o[1][f"{tag}_x"]])
+        assert rel(x, s[f"{tag}_x"]) < TOL, tag
+        assert rel(s[f"{tag}_x"][perm], s[f"{ref}_x"]) < TOL, tag
+        assert np.array_equal(o[0][f"{tag}_res"], o[1][f"{tag}_res"])
+        hist_ok(o[0][f"{tag}_res"], s[f"{ref}_res"], TOL)
+        H_ok(o[0][f"{tag}_H"], s[f"{ref}_H"])
