@@ -110,3 +110,18 @@ def test_gloo_two_rank_sharded_gmres_matches_oracle():
         # every rank holds the same (replicated) Hessenberg matrix
         np.testing.assert_allclose(out[r]["H"], Hr, rtol=0, atol=1e-10 * np.abs(Hr).max())
     assert np.linalg.norm(x - xr) <= 1e-10 * np.linalg.norm(xr)
+
+
+def test_stored_pixel_index_is_the_tiled_permutation():
+    """hgmres.core.stored_pixel_index mirrors csrc/ops.hip pixel_index: a permutation; 4 x 4
+    tiles in tile-column-major order, column-major inside a tile; super-blocks contiguous."""
+    from hgmres.core import stored_pixel_index
+    N = 8
+    s = stored_pixel_index(N, 4, 0)
+    assert sorted(s.tolist()) == list(range(N * N))
+    assert s[1 + 5 * N] == ((1 * 2 + 0) * 4 + 1) * 4 + 1      # (r=1, c=5): tile (0,1), (col 1, row 1) inside
+    assert list(s[:4]) == [0, 1, 2, 3] and s[N] == 4            # first tile column-major
+    t = stored_pixel_index(16, 4, 8)
+    assert sorted(t.tolist()) == list(range(256))
+    assert t[0 + 8 * 16] == 2 * 64                              # (r=0, c=8): third super-block (column-major)
+    np.testing.assert_array_equal(stored_pixel_index(8, 1, 0), np.arange(64))
