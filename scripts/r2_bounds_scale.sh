@@ -1,0 +1,5 @@
+#!/bin/bash
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -u scripts/bounds_scale.py 512 30 20 60 > gpurun_out/bounds_scale_c2.log 2>&1 || exit $?
