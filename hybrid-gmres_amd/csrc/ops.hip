@@ -304,6 +304,10 @@ void finalize_operator(hgm_ctx* c, hgm_mat* M) {
             // 2.90 ms vs 3.31 ms at 16 lanes; reference order 2.96 ms vs 4.18 ms at 32 lanes)
             M->variant = SPMV_STREAM | SPMV_NT;
             M->bsgroup = 4;
+            // XCD-contiguous chunk order: each XCD streams its own bands, so a band's x-slice is
+            // fetched into one L2 instead of eight (paged kernel, alternating runs: C4 A 2.36 ->
+            // 2.31 ms, C3 A 252 -> 238 us, bitwise equal; profiles/r2_c{3,4}_xcd.log)
+            M->variant |= SPMV_XCD;
         } else {
             // C2 A (460-entry rays, x L2-resident): 16 lanes per row beats 32 in the solve
             // (33.0 vs 34.6 us, alternating runs, scripts/ab_compare.sh)

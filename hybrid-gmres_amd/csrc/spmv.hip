@@ -203,6 +203,7 @@ struct Paged {
     const int32_t* pids = nullptr;
     const uint16_t* lidx = nullptr;
     int64_t xlen = 0;
+    int xcd = 0;   // SPMV_XCD: workgroups of one XCD take one contiguous eighth of the chunks
 };
 
 // 16 bytes of page `pid` for lane `pl` of the page's loaders, zero past the end of x
@@ -234,7 +235,10 @@ __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, c
     using IV4 = std::conditional_t<sizeof(IX) == 2, nus4, ni4>;
     __shared__ __attribute__((aligned(16))) unsigned char smem[stream_lds_bytes<T>(PG)];
     T* prod = reinterpret_cast<T*>(smem);
-    const int64_t k = blockIdx.x;
+    // chunk of this workgroup: in launch order, or (pg.xcd) XCD-contiguous -- workgroups are
+    // dispatched to the 8 XCDs round-robin, so XCD j then streams the j-th eighth of the chunks
+    // (band-major: its own bands, whose x-slices only its L2 fetches)
+    const int64_t k = pg.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
     const int64_t c0 = k * SCH;
     const int64_t c1 = (c0 + SCH < nnz) ? c0 + SCH : nnz;
     const int n = (int)(c1 - c0);
@@ -663,6 +667,7 @@ static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int ep
     const bool nt = M->variant & SPMV_NT;
     // paged x gathers need the page index and a 16-B aligned x (vector page loads)
     Paged<T> pg;
+    pg.xcd = (M->variant & SPMV_XCD) ? 1 : 0;
     if ((M->variant & SPMV_PAGED) && M->pg_ptr && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
         pg.pptr = M->pg_ptr;
         pg.pids = M->pg_ids;
@@ -681,7 +686,7 @@ static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int ep
         // 16-bit page-local indices instead, and only chunks past the page limit read M->ci
         if (M->ci16 && !(pg.pptr && c->num.paged16))
             spmv_stream<T, uint16_t>(c, true, si, M->sgroup, nt, M->ci16, reinterpret_cast<const T*>(M->val), x, y,
-                                     epi, a, z, pn);
+                                     epi, a, z, pn, pg);
         else
             spmv_stream<T>(c, true, si, M->sgroup, nt, M->ci, reinterpret_cast<const T*>(M->val), x, y, epi, a, z, pn,
                            pg);
