@@ -138,29 +138,44 @@ int gmres_bounds_filter(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const h
         normalize_to<double>(c, dim, Qp, nrm);
         std::vector<double> Hp((size_t)(p + 1) * p, 0.0);
         double hmax = 0.0;
-        for (int j = 0; j < p; ++j) {
-            const double* qj = Qp + (int64_t)j * ldp;
-            double* v = Qp + (int64_t)(j + 1) * ldp;
-            if (nspace) {                                    // M = B*A
-                spmv<double>(c, A, qj, tm, EPI_NONE, 0.0, nullptr, KC_SPMV_A);
-                spmv<double>(c, B, tm, v, EPI_NONE, 0.0, nullptr, KC_SPMV_B);
-            } else {                                         // M = A*B
-                spmv<double>(c, B, qj, tm, EPI_NONE, 0.0, nullptr, KC_SPMV_B);
-                spmv<double>(c, A, tm, v, EPI_NONE, 0.0, nullptr, KC_SPMV_A);
+        // The steps are enqueued back to back and their H columns read once; the scan then applies
+        // the per-step breakdown test with the running max.  After an invariant subspace at step j
+        // (rare) the fresh vector is made and the steps from j+1 are enqueued again, so the result is
+        // that of a per-step test.
+        int j0 = 0;
+        while (j0 < p) {
+            for (int j = j0; j < p; ++j) {
+                const double* qj = Qp + (int64_t)j * ldp;
+                double* v = Qp + (int64_t)(j + 1) * ldp;
+                if (nspace) {                                    // M = B*A
+                    spmv<double>(c, A, qj, tm, EPI_NONE, 0.0, nullptr, KC_SPMV_A);
+                    spmv<double>(c, B, tm, v, EPI_NONE, 0.0, nullptr, KC_SPMV_B);
+                } else {                                         // M = A*B
+                    spmv<double>(c, B, qj, tm, EPI_NONE, 0.0, nullptr, KC_SPMV_B);
+                    spmv<double>(c, A, tm, v, EPI_NONE, 0.0, nullptr, KC_SPMV_A);
+                }
+                cgs2<double>(c, dim, Qp, ldp, j, Hd + (size_t)j * (p + 1), false);
             }
-            cgs2<double>(c, dim, Qp, ldp, j, Hd + (size_t)j * (p + 1), false);
             Reader rd(c);
-            rd.add(&Hp[(size_t)j * (p + 1)], Hd + (size_t)j * (p + 1), sizeof(double) * (j + 2));
+            rd.add(&Hp[(size_t)j0 * (p + 1)], Hd + (size_t)j0 * (p + 1), sizeof(double) * (size_t)(p - j0) * (p + 1));
             rd.go();
-            for (int i = 0; i < j + 2; ++i) hmax = std::max(hmax, std::fabs(Hp[(size_t)j * (p + 1) + i]));
-            double& hsub = Hp[(size_t)j * (p + 1) + j + 1];
-            if (j + 1 < p && !(hsub > 1e-12 * hmax)) {
-                // invariant subspace found: continue from a fresh vector orthogonal to it
-                // (H(j+1,j) = 0 keeps Hp block upper triangular, so its eigenvalues stay M's)
-                hsub = 0.0;
-                fill_hash<double>(c, dim, v, seed + 0x1000 + (uint64_t)j);
-                cgs2<double>(c, dim, Qp, ldp, j, hsink, false);
+            int restart = p;
+            for (int j = j0; j < p; ++j) {
+                for (int i = 0; i < j + 2; ++i) hmax = std::max(hmax, std::fabs(Hp[(size_t)j * (p + 1) + i]));
+                for (int i = j + 2; i <= p; ++i) Hp[(size_t)j * (p + 1) + i] = 0.0;
+                double& hsub = Hp[(size_t)j * (p + 1) + j + 1];
+                if (j + 1 < p && !(hsub > 1e-12 * hmax)) {
+                    // invariant subspace found: continue from a fresh vector orthogonal to it
+                    // (H(j+1,j) = 0 keeps Hp block upper triangular, so its eigenvalues stay M's)
+                    hsub = 0.0;
+                    double* v = Qp + (int64_t)(j + 1) * ldp;
+                    fill_hash<double>(c, dim, v, seed + 0x1000 + (uint64_t)j);
+                    cgs2<double>(c, dim, Qp, ldp, j, hsink, false);
+                    restart = j + 1;
+                    break;
+                }
             }
+            j0 = restart;
         }
         const double h_next = Hp[(size_t)(p - 1) * (p + 1) + p];
         const std::vector<double> G = projected_delta(c, dm, Qp, ldp, dim, p);
