@@ -84,17 +84,19 @@ def _fsum(p):
 
 
 def _norm(v):
+    # numpy scalars, not Python floats: a division by a zero norm gives MATLAB's Inf / NaN
+    # (e.g. beta = 0 for b = 0, norm(x_true) = 0) instead of raising ZeroDivisionError
     if _FIXED:
         v = np.asarray(v, dtype=np.float64)
-        return float(np.sqrt(_fsum(v * v)))
-    return float(np.linalg.norm(v))
+        return np.float64(np.sqrt(_fsum(v * v)))
+    return np.float64(np.linalg.norm(v))
 
 
 def _dot(a, b):
     """Inner product a'*b (``Q(:,j)'*v``)."""
     if _FIXED:
-        return _fsum(np.asarray(a, dtype=np.float64) * np.asarray(b, dtype=np.float64))
-    return float(a @ b)
+        return np.float64(_fsum(np.asarray(a, dtype=np.float64) * np.asarray(b, dtype=np.float64)))
+    return np.float64(a @ b)
 
 
 def _gemv(Q, y):
