@@ -24,7 +24,9 @@ def main():
     lib = L.load()
     ctx = hgmres.Context(0)
     N, na = CONFIGS[cfg]
-    A = hgmres.SparseOperator.siddon(N, na, ctx=ctx)
+    f32 = os.environ.get("HGM_DTYPE") == "f32"
+    es = 4 if f32 else 8
+    A = hgmres.SparseOperator.siddon(N, na, ctx=ctx, dtype=L.HGM_F32 if f32 else L.HGM_F64)
     B = A.T
     res = {"cfg": cfg}
     for nm, M in (("A", A), ("B", B)):
@@ -32,10 +34,10 @@ def main():
             continue
         rows, cols = M.shape
         xd, yd = C.c_void_p(), C.c_void_p()
-        lib.hgm_dev_alloc(ctx.handle, 8 * cols, C.byref(xd))
-        lib.hgm_dev_alloc(ctx.handle, 8 * rows, C.byref(yd))
-        xs = np.random.default_rng(0).standard_normal(cols)
-        lib.hgm_memcpy_h2d(ctx.handle, xd, xs.ctypes.data_as(C.c_void_p), 8 * cols)
+        lib.hgm_dev_alloc(ctx.handle, es * cols, C.byref(xd))
+        lib.hgm_dev_alloc(ctx.handle, es * rows, C.byref(yd))
+        xs = np.random.default_rng(0).standard_normal(cols).astype(np.float32 if f32 else np.float64)
+        lib.hgm_memcpy_h2d(ctx.handle, xd, xs.ctypes.data_as(C.c_void_p), es * cols)
         opts = choices[nm].split(",")
         acc = {o: [] for o in opts}
         ys = {}
@@ -53,8 +55,8 @@ def main():
                 ms, calls, by = ctx.kernel_timing_read(0)
                 ctx.kernel_timing(False)
                 acc[o].append(ms / calls)
-                y = np.empty(rows)
-                lib.hgm_memcpy_d2h(ctx.handle, y.ctypes.data_as(C.c_void_p), yd, 8 * rows)
+                y = np.empty(rows, dtype=xs.dtype)
+                lib.hgm_memcpy_d2h(ctx.handle, y.ctypes.data_as(C.c_void_p), yd, es * rows)
                 ys[o] = y
                 res.setdefault("bytes_" + nm, by / calls)
         base = ys[opts[0]]
