@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="sharded-solve transport: RCCL, or the host all-reduce hook (single-device emulation)")
     ap.add_argument("--same-device", action="store_true", help="run every rank on GPU 0 (shard emulation)")
+    ap.add_argument("--shard1", action="store_true",
+                    help="N=1: the sharded code path on a one-rank RCCL communicator (transport rehearsal)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="experiment: per-context numerics option (hgm_ctx_set_option), e.g. mgs_fused=0")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -164,12 +166,15 @@ def main():
     from hgmres.core import _check
 
     wl = WORKLOADS[args.workload]
-    shard = world > 1 and not args.replicas
+    shard = (world > 1 and not args.replicas) or args.shard1
     if shard:
         # one global problem, pixel-sharded: RCCL context (or the host
         # all-reduce hook for the single-device emulation)
         from hgmres.dist import host_allreduce_context, init_context
-        ctx = host_allreduce_context(local, rank, world) if args.comm == "host" else init_context(local, rank, world)
+        if args.comm == "host":
+            ctx = host_allreduce_context(local, rank, world)
+        else:
+            ctx = init_context(local, rank, world, one_rank_comm=args.shard1)
         A, B, b, x_true, (lo, hi), full = build_shard(ctx, wl, rank, world)
     else:
         ctx = hgmres.Context(local)

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <set>
 #include <vector>
@@ -248,12 +249,13 @@ void pipe_wait(hgm_ctx* c) {
 
 template <typename T>
 static void allreduce_t(hgm_ctx* c, T* dev, int64_t count, ncclDataType_t dt) {
-    if (c->world <= 1 || count <= 0) return;
-    if (c->nccl) {
+    if (count <= 0) return;
+    if (c->nccl) {              // includes a one-rank communicator (hgm_ctx_create_dist)
         if (ncclAllReduce(dev, dev, (size_t)count, dt, ncclSum, c->nccl, c->stream) != ncclSuccess)
             throw Error{HGM_E_COMM, "ncclAllReduce failed"};
         return;
     }
+    if (c->world <= 1) return;
     if (!c->host_ar) throw Error{HGM_E_COMM, "world > 1 but no communicator"};
     // host all-reduce hook (shard emulation / tests): always exchanged as doubles
     ensure_stage(c, sizeof(double) * count + sizeof(T) * count);
@@ -399,7 +401,11 @@ HGM_API int hgm_ctx_create_dist(int device, int rank, int world, const void* uni
     hgm_ctx* c = *out;
     c->rank = rank;
     c->world = world;
-    if (world > 1) {
+    // world 1 with a non-zero id: a one-rank communicator, so the solve takes the sharded code
+    // path with real RCCL all-reduces (rehearses the transport on one GPU)
+    const unsigned char* u = static_cast<const unsigned char*>(unique_id);
+    const bool one_rank = world == 1 && std::any_of(u, u + sizeof(ncclUniqueId), [](unsigned char x) { return x != 0; });
+    if (world > 1 || one_rank) {
         ncclUniqueId id;
         std::memcpy(&id, unique_id, sizeof(id));
         if (ncclCommInitRank(&c->nccl, world, id, rank) != ncclSuccess) {
@@ -904,7 +910,7 @@ HGM_API int hgm_gcv_function(hgm_ctx* c, double lambda, const hgm_mat* A, const 
     // gcv_function.m:33 k = size(H,2) = k_gcv; trace term m ('ab') or n ('ba') (:46-50)
     const double trace_m = side == HGM_SIDE_AB ? (double)m : (double)A->cols * 1.0;
     double tm = trace_m;
-    if (side == HGM_SIDE_BA && c->world > 1) {
+    if (side == HGM_SIDE_BA && (c->world > 1 || c->nccl)) {
         double nloc = (double)A->cols;
         std::vector<double> v{nloc};
         HGM_TRY(c, {

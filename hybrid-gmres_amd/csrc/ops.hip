@@ -298,12 +298,10 @@ void finalize_operator(hgm_ctx* c, hgm_mat* M) {
     set_bands(c, M, auto_band_width(M));
     if (avg >= 64) {
         if (M->nbands > 1) {
-            // band segments are short ray chords (tens to hundreds of entries): 4 lanes per
-            // segment keeps every lane busy; with the super-block order the wider bands also
-            // gain from nontemporal val/col loads (C4 sweeps, profiles/r1_spmv_sweep_c4_*.jsonl:
-            // 2.90 ms vs 3.31 ms at 16 lanes; reference order 2.96 ms vs 4.18 ms at 32 lanes)
+            // the streaming kernel over the (band,row) segments, 4 lanes per segment (set_bands);
+            // the wider bands also gain from nontemporal val/col loads (C4 sweeps,
+            // profiles/r1_spmv_sweep_c4_*.jsonl; reference order 2.96 ms vs 4.18 ms at 32 lanes)
             M->variant = SPMV_STREAM | SPMV_NT;
-            M->bsgroup = 4;
             // XCD-contiguous chunk order: each XCD streams its own bands, so a band's x-slice is
             // fetched into one L2 instead of eight (paged kernel, alternating runs: C4 A 2.36 ->
             // 2.31 ms, C3 A 252 -> 238 us, bitwise equal; profiles/r2_c{3,4}_xcd.log)
@@ -391,8 +389,14 @@ void set_bands(hgm_ctx* c, hgm_mat* M, int64_t W) {
     // streaming index over the (band,row) segments; ~2/3 of them are non-empty for a
     // parallel-beam operator, hence the 1.5 factor in the average segment length
     M->bcfo = build_chunk_index(c, M->brp, nseg, M->nnz);
-    M->bsgroup = stream_group((double)M->nnz / (double)(M->rows > 0 ? M->rows : 1) /
-                              (double)(nb > 0 ? nb : 1) * 1.5);
+    const double row_avg = (double)M->nnz / (double)(M->rows > 0 ? M->rows : 1);
+    M->bsgroup = stream_group(row_avg / (double)(nb > 0 ? nb : 1) * 1.5);
+    // long-row (ray-major) operators: band segments are short ray chords (tens to hundreds of
+    // entries), and 4 lanes per segment keeps every lane busy (C4 sweeps,
+    // profiles/r1_spmv_sweep_c4_*.jsonl: 2.90 ms vs 3.31 ms at 16 lanes).  Set here so that
+    // hgm_mat_set_bands keeps it too (a 64-column re-band at 8/16 lanes cost the C4 shards
+    // 2.57 vs 2.27 ms, profiles/r2_shard_order.log)
+    if (row_avg >= 64) M->bsgroup = 4;
     HGM_HIP(hipStreamSynchronize(st));
 }
 

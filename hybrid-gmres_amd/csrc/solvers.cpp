@@ -36,7 +36,8 @@ T* dslot(hgm_ctx* c, int i) {
     return reinterpret_cast<T*>(c->dscal) + i;
 }
 
-inline bool dist_n(hgm_ctx* c) { return c->world > 1; }
+// sharded code path: world > 1, or a one-rank RCCL communicator (hgm_ctx_create_dist)
+inline bool dist_n(hgm_ctx* c) { return c->world > 1 || c->nccl != nullptr; }
 
 // y = A x (+epilogue) where the output is an m-vector assembled across ranks.
 template <typename T>

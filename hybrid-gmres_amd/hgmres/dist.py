@@ -62,9 +62,14 @@ def unique_id() -> bytes:
     return bytes(buf)
 
 
-def init_context(device: int, rank: int, world: int, uid: bytes | None = None, group=None) -> Context:
+def init_context(device: int, rank: int, world: int, uid: bytes | None = None, group=None,
+                 one_rank_comm: bool = False) -> Context:
     """RCCL-backed context.  If ``uid`` is None it is created on rank 0 and
-    broadcast with ``torch.distributed.broadcast_object_list`` over ``group``."""
+    broadcast with ``torch.distributed.broadcast_object_list`` over ``group``.
+    ``one_rank_comm`` (world 1): a one-rank communicator, so the solve runs the sharded
+    code path with real RCCL all-reduces on one GPU."""
+    if world == 1 and one_rank_comm and uid is None:
+        uid = unique_id()
     if world > 1 and uid is None:
         import torch.distributed as dist
         obj = [unique_id() if rank == 0 else None]

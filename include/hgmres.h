@@ -130,6 +130,10 @@ HGM_API int hgm_runtime_check(char* msg, int len);
 HGM_API int hgm_device_count(int* count);
 HGM_API int hgm_ctx_create(int device, hgm_ctx** ctx);
 HGM_API int hgm_comm_unique_id(void* id_out /* HGM_UNIQUE_ID_BYTES */);
+/* RCCL context: rank `rank` of `world` on `device`, the id from hgm_comm_unique_id on rank 0.
+ * world == 1 with an all-zero id is a plain context; world == 1 with a real id makes a one-rank
+ * communicator, so the solvers take the sharded code path with real RCCL all-reduces (the whole
+ * operator is the one shard) — rehearses the transport on a single GPU. */
 HGM_API int hgm_ctx_create_dist(int device, int rank, int world, const void* unique_id, hgm_ctx** ctx);
 HGM_API int hgm_ctx_set_host_allreduce(hgm_ctx* ctx, int rank, int world, hgm_allreduce_fn fn, void* user);
 HGM_API void hgm_ctx_destroy(hgm_ctx* ctx);

@@ -1,4 +1,5 @@
-"""Worker for test_gpu_parity.py::test_shard_emulation_two_ranks.
+"""Worker for test_gpu_parity.py::test_shard_emulation_two_ranks (and, through
+solve_all, test_gpu_rccl.py's one-rank RCCL run).
 
 Runs the pixel-sharded solvers as ``world`` processes on ONE device with the
 cross-rank sums routed through the library's host all-reduce hook (a fixed-order
@@ -21,7 +22,6 @@ from hgmres.problems import tomo_problem  # noqa: E402
 
 def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
-    P = tomo_problem(64, 90, noise=1e-2, seed=0)
     ctx = hgmres.Context(0)
     conn = None
     if world > 1:
@@ -49,6 +49,16 @@ def main():
                 arr[:] = conn.recv()
 
         ctx.set_host_allreduce(rank, world, allreduce)
+    res = solve_all(ctx, rank, world)
+    np.savez(os.path.join(out, f"rank{rank}_of{world}.npz"), **res)
+    if conn is not None:
+        conn.close()
+    ctx.close()
+
+
+def solve_all(ctx, rank, world):
+    """Every sharded solve of the test on rank `rank`'s shard; returns the arrays by tag."""
+    P = tomo_problem(64, 90, noise=1e-2, seed=0)
     lo, hi = plan_pixel_shards(P.A, world, P.B)[rank]
     A_g, B_g = shard_operators(P.A, P.B, lo, hi)
     xt = P.x_true[lo:hi]
@@ -84,10 +94,8 @@ def main():
     res.update(tabn_x=out_[0], tabn_res=out_[2], tabn_err=out_[1], tabn_H=out_[-1])
     x, e, r, k, H = hgmres.hybrid_ba_gmres_rtp(A2, B2, P.b, xs[tlo:thi], 0.0, 15, 1e-2, ctx=ctx, return_H=True)
     res.update(thba_x=x, thba_res=r, thba_err=e, thba_H=H)
-    np.savez(os.path.join(out, f"rank{rank}_of{world}.npz"), lo=lo, hi=hi, tlo=tlo, thi=thi, **res)
-    if conn is not None:
-        conn.close()
-    ctx.close()
+    res.update(lo=lo, hi=hi, tlo=tlo, thi=thi)
+    return res
 
 
 if __name__ == "__main__":
