@@ -156,6 +156,9 @@ struct hgm_mat {
     int group = 64;          // lanes per row in the SpMV kernel
     int variant = 0;         // SpmvVariant bits
     double fro = -1.0;       // cached ||M||_F (lsmr_solver.m:71 is loop-invariant)
+    // identity (operators are immutable once built): transpose_of = the uid of the operator
+    // this one is the device transpose of, value for value (hgm_mat_transpose)
+    uint64_t uid = 0, transpose_of = 0;
     // Column-banded copy (cache blocking of the x gather): the columns are
     // cut into nbands contiguous bands of band_w pixels; segment (b, r) of row r that lies
     // in band b is [brp[b*rows + r], brp[b*rows + r + 1]) of bci/bval (band-major order).

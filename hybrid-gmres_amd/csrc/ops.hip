@@ -5,6 +5,7 @@
 //    hgmres/problems.py so the two generators agree bit for bit).
 #include <hipcub/hipcub.hpp>
 
+#include <atomic>
 #include <climits>
 #include <cmath>
 #include <cstdlib>
@@ -14,7 +15,9 @@
 namespace hgm {
 
 hgm_mat* mat_alloc(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, int dtype) {
+    static std::atomic<uint64_t> next_uid{0};
     hgm_mat* M = new hgm_mat();
+    M->uid = ++next_uid;
     M->ctx = c;
     M->rows = rows;
     M->cols = cols;
@@ -449,6 +452,7 @@ hgm_mat* transpose(hgm_ctx* c, const hgm_mat* M) {
     hgm_mat* T = mat_alloc(c, M->cols, M->rows, nnz, M->dtype);
     T->row_order = M->col_order;
     T->col_order = M->row_order;
+    T->transpose_of = M->uid;
     if (nnz == 0) {
         HGM_HIP(hipMemsetAsync(T->rp, 0, sizeof(int64_t) * (T->rows + 1), st));
         HGM_HIP(hipStreamSynchronize(st));

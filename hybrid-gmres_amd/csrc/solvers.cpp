@@ -284,8 +284,17 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // Gram error monitor: step k's MGS sweep appends [Q(:,k)'Q(:,0:k-1),
     // Q(:,k)'Q(:,k), Q(:,k)'x_true] to the ring (LQ doubles) and the host evaluates
     // ||Q y_k - x_true||^2 from them, so an iteration's reconstruction reads only the kept A*Q.
-    const bool gem = aq_res && zc && c->num.ring_poll && orth == HGM_MGS && mgs_gram_ok(c, ldq, maxit, dist) &&
-                     c->num.gram_err;
+    const bool gem_ok = zc && c->num.ring_poll && orth == HGM_MGS && mgs_gram_ok(c, ldq, maxit, dist) &&
+                        c->num.gram_err;
+    const bool gem_n = aq_res && gem_ok;
+    // m-space side (AB-GMRES, x = (B*Q) y = Z y): when B is A' value for value (a device
+    // transpose), Z'Z = Q'(A*B*Q) are the sweep's own dots Q'w_k = (I + L) H(0:k,k) (one-reduction
+    // form, L the strictly lower Q'Q), and Z'x_true = x_true'(B*q_k) is one dot per step riding on
+    // the sweep as a side job, so an iteration's reconstruction reads no n-vector: the kept B*Q
+    // columns are combined once, at the end (C4: the 0.3 ms GEMV per iteration)
+    const bool pair_t = B && (B->transpose_of == A->uid || A->transpose_of == B->uid);
+    const bool gem_ab = bq_res && gem_ok && sp.proj != PROJ_ABRTP && pair_t;
+    const bool gem = gem_n || gem_ab;
     const double gem_min = c->num.gram_err_min;
     const size_t LQ = (size_t)maxit + 2, offQG = offS + 4;
     const size_t ring_n = offQG + (gem ? (size_t)maxit * LQ : 0);
@@ -370,7 +379,9 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     std::vector<double> y, rhs, M;
     std::vector<double> G((size_t)maxit * maxit, 0.0), cvec(maxit, 0.0);
     // Gram error monitor: Q'Q, Q'x_true and the errors it produced (-1: formed explicitly)
+    // (m-space: the Gram of Z = B*Q, from H and the strictly lower Q'Q in SQ)
     std::vector<double> GQ(gem ? (size_t)maxit * maxit : 0), cq(maxit, 0.0), gerr(maxit, -1.0);
+    std::vector<double> SQ(gem_ab ? (size_t)maxit * maxit : 0);
     // Pending normalisation (single GPU, n-space, one-reduction MGS): step k
     // leaves v_{k+1} = Q(:,k+1) undivided and step k+1 applies q = v / H(k+1,k) where it reads
     // it — A: (A*v)/h, which also publishes h = H(k+1,k); B: B*(A*q) + lambda*q; the MGS dots
@@ -438,9 +449,17 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         } else {
             PendNorm<T>* defer = (pn_ok && kq + 1 < maxit) ? &pend : nullptr;
             if (!defer) pend.np = 0;
-            mgs<T>(c, dim, Q, ldq, kq, Hcol, dist, (!nspace && ABQ) ? ABQ + (int64_t)kq * ldaq : nullptr, side,
-                   defer, pending_in ? (const T*)pn_h : nullptr, gem ? xt : nullptr,
-                   gem ? dr + offQG + (size_t)kq * LQ : nullptr);
+            MdotJob<T> zx;                                // gem_ab: x_true'(B*q_k) -> row entry k+2
+            if (gem_ab) {
+                zx.n = n;
+                zx.w = BQ + (int64_t)kq * ldbq;
+                zx.e = xt;
+                zx.out = dr + offQG + (size_t)kq * LQ + kq + 2;
+            }
+            // the Gram row's extra dot: x_true (n-space) or b (m-space, unused: the row is for L)
+            mgs<T>(c, dim, Q, ldq, kq, Hcol, dist, (!nspace && ABQ) ? ABQ + (int64_t)kq * ldaq : nullptr,
+                   gem_ab ? &zx : side, defer, pending_in ? (const T*)pn_h : nullptr,
+                   gem ? (gem_n ? xt : b) : nullptr, gem ? dr + offQG + (size_t)kq * LQ : nullptr);
         }
         // Step kq-1's column is complete (H(kq,kq-1) came from this step's A product).  The
         // event goes at the end of the step: a marker between two kernels costs a bubble.
@@ -480,7 +499,9 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         if (bq_res) {
             // xk = B*(Q(:,1:k)*yk) = (B*Q(:,1:k))*yk with ||xk - x_true||^2, and
             // ||b - A*xk||^2 = ||b - (A*B*Q(:,1:k))*yk||^2 (*_bounds.m:37-40), one launch
-            recon<T>(c, n, kk, BQ, ldbq, yk, x, xt, eslot, m, ABQ, ldaq, b, rslot);
+            // (want_x false: the m-space Gram error monitor has the error, x is formed at the end)
+            recon<T>(c, n, kk, BQ, ldbq, yk, want_x ? x : nullptr, xt, eslot, m, ABQ, ldaq, b, rslot);
+            x_pending = want_x ? -1 : kq;
             if (dist_n(c)) allreduce(c, eslot, 1);
             publish(offM + 2 * (size_t)kq, 2);
             pipe_record(c);
@@ -524,6 +545,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             for (int i = 0; i < kq + 2; ++i) idx.push_back((size_t)kq * LH + (maxit + 2) + i);
         if (gem)
             for (int i = 0; i < kq + 2; ++i) idx.push_back(offQG + (size_t)kq * LQ + i);
+        if (gem_ab) idx.push_back(offQG + (size_t)kq * LQ + kq + 2);
         ring_wait(c, hr, idx);
     };
     // the monitors of reconstruction R_kq (the error slot is not written when the Gram error
@@ -574,11 +596,22 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             for (int i = 0; i <= k; ++i) G[(size_t)k * maxit + i] = hk[(maxit + 2) + i];
             cvec[k] = hk[(maxit + 2) + k + 1];
         }
-        if (gem) {
+        if (gem_n) {
             const double* gk = hr + offQG + (size_t)k * LQ;
             for (int i = 0; i < k; ++i) GQ[(size_t)k * maxit + i] = GQ[(size_t)i * maxit + k] = gk[i];
             GQ[(size_t)k * maxit + k] = gk[k];
             cq[k] = gk[k + 1];
+        } else if (gem_ab) {
+            // z_j'z_k = q_j'(A*B*q_k) = H(j,k) + sum_{i<j} (q_j'q_i) H(i,k): the sweep solved
+            // (I + L) h = Q'w_k for h = H(0:k,k), so this is its right-hand side again
+            const double* gk = hr + offQG + (size_t)k * LQ;
+            for (int i = 0; i < k; ++i) SQ[(size_t)k * maxit + i] = gk[i];
+            for (int j = 0; j <= k; ++j) {
+                long double g = Hh(j, k);
+                for (int i = 0; i < j; ++i) g += (long double)SQ[(size_t)j * maxit + i] * Hh(i, k);
+                GQ[(size_t)k * maxit + j] = GQ[(size_t)j * maxit + k] = (double)g;
+            }
+            cq[k] = gk[k + 2];
         }
         if (Hh(k + 1, k) == 0) {                         // :25  if H(k+1,k) == 0, break
             done = true;
@@ -643,7 +676,9 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         // the last reconstruction left x unformed (Gram error monitor): x = Q(:,0:k) y_k
         // behind it, on the same stream
         StreamScope scope(c, rs_stream, "aux:");
-        gemv<T>(c, n, x_pending + 1, Q, ldq, c->hring_dev + offY + (size_t)x_pending * maxit, x, 0);
+        const T* yk = c->hring_dev + offY + (size_t)x_pending * maxit;
+        if (nspace) gemv<T>(c, n, x_pending + 1, Q, ldq, yk, x, 0);
+        else gemv<T>(c, n, x_pending + 1, BQ, ldbq, yk, x, 0);          // x = (B*Q) y
         x_pending = -1;
     }
     bool staged = false;

@@ -97,7 +97,8 @@ enum hgm_ctx_option {
     HGM_OPT_PARITY = 1,
     HGM_OPT_MGS_FORM = 2,          /* MGS for long vectors: 1 one-reduction form [1], 0 one launch per pass */
     HGM_OPT_MGS_SINGLE = 3,        /* one-workgroup MGS sweep for short bases [1] */
-    HGM_OPT_GRAM_ERR = 4,          /* Gram error monitor of the n-space GMRES solvers [1] */
+    HGM_OPT_GRAM_ERR = 4,          /* Gram error monitor of the n-space GMRES solvers, and of the
+                                      AB *_bounds solvers when B is the device transpose of A [1] */
     HGM_OPT_GRAM_ERR_MIN = 5,      /* ... used while ||x-x_true||^2/||x_true||^2 >= this [0.01] */
     HGM_OPT_RING_POLL = 6,         /* single GPU: host polls the pinned ring instead of events [1] */
     HGM_OPT_PEND_NORM = 7,         /* pending normalisation of the Krylov vector [1] */

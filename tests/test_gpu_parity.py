@@ -415,6 +415,31 @@ def test_residual_monitor_forms_agree(gpu_ctx, P64, tag, fn, haslam):
     hist_ok(o1[2], ref[2], TOL)
 
 
+@pytest.mark.parametrize("tag,fn,haslam", [g for g in GM if g[0] in ("abp", "abn")])
+@pytest.mark.parametrize("N,na", [(64, 90), (64, 91)])
+def test_ab_gram_error_monitor(gpu_ctx, tag, fn, haslam, N, na):
+    """AB *_bounds with B the device transpose of A (B = None): the error history comes from
+    the Gram of Z = B*Q, Z'Z = Q'(A*B*Q) = (I + L) H (the sweep's own dots) and Z'x_true (a dot
+    riding on the sweep), and x = (B*Q) y is formed once at the end (solvers.cpp gem_ab).
+    Against the explicit per-iteration reconstruction (HGM_OPT_GRAM_ERR = 0) to 1e-12 and the
+    oracle to 1e-10 (north_star).  mgs_single = 0: the unpadded multi-block basis it needs."""
+    P = tomo_problem(N, na, noise=1e-2, seed=0)
+    args = (1e-2,) if haslam else ()
+    with gpu_ctx.options(mgs_single=0):
+        og = fn(P.A, None, P.b, P.x_true, 0.0, 20, *args, ctx=gpu_ctx, return_H=True)
+        with gpu_ctx.options(gram_err=0):
+            oe = fn(P.A, None, P.b, P.x_true, 0.0, 20, *args, ctx=gpu_ctx, return_H=True)
+    assert og[3] == oe[3] == 20 and np.array_equal(og[-1], oe[-1])   # the Arnoldi part is shared
+    assert rel(og[0], oe[0]) < 1e-13
+    hist_ok(og[2], oe[2], 1e-13)
+    hist_ok(og[1], oe[1], 1e-12)
+    assert not np.array_equal(og[1], oe[1])          # the Gram form ran (its rounding differs)
+    ref = getattr(R, fn.__name__)(P.A, P.A.T.tocsr(), P.b, P.x_true, 0.0, 20, *args)
+    assert rel(og[0], ref[0]) < TOL
+    hist_ok(og[1], ref[1], TOL)
+    hist_ok(og[2], ref[2], TOL)
+
+
 def test_gmres_determinism(gpu_ctx, P64):
     o1 = hgmres.hybrid_ab_gmres_rtp(P64.A, P64.B, P64.b, P64.x_true, 0.0, 15, 1e-2, ctx=gpu_ctx, return_H=True)
     o2 = hgmres.hybrid_ab_gmres_rtp(P64.A, P64.B, P64.b, P64.x_true, 0.0, 15, 1e-2, ctx=gpu_ctx, return_H=True)
