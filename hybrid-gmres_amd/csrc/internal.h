@@ -200,8 +200,11 @@ constexpr int SCH = HGM_SCH;
 #ifndef HGM_PG_MAX64
 #define HGM_PG_MAX64 256
 #endif
+#ifndef HGM_PG_MAX32
+#define HGM_PG_MAX32 (SCH * 4 / 128)
+#endif
 constexpr int PG_BYTES = 128;
-template <typename T> constexpr int pg_max() { return sizeof(T) == 8 ? HGM_PG_MAX64 : SCH * (int)sizeof(T) / PG_BYTES; }
+template <typename T> constexpr int pg_max() { return sizeof(T) == 8 ? HGM_PG_MAX64 : HGM_PG_MAX32; }
 template <typename T> constexpr int stream_lds_bytes(bool paged) {
     return paged && pg_max<T>() * PG_BYTES > SCH * (int)sizeof(T) ? pg_max<T>() * PG_BYTES : SCH * (int)sizeof(T);
 }

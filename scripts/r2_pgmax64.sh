@@ -1,7 +1,6 @@
 #!/bin/bash
-# LDS page budget per chunk: fp64 256/320/384 pages at C4, fp32 128/192/256 at C5.
+# LDS page budget per chunk, fp64 at C4: 256 / 320 / 384 pages.
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 : > gpurun_out/lib_sweep.jsonl
 bash scripts/lib_sweep.sh c4 exp/lib_base.so exp/lib_p64_320.so exp/lib_p64_384.so || exit $?
-bash scripts/lib_sweep.sh c5 exp/lib_base.so exp/lib_p32_192.so exp/lib_p32_256.so || exit $?
