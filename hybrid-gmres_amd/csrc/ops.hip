@@ -112,8 +112,9 @@ void build_stream_index(hgm_ctx* c, hgm_mat* M) {
 // --------------------------------------------------------------------------
 // x-page index of the paged streaming kernel (spmv.hip).  One 256-thread block per chunk of
 // SCH entries: block radix sort of (page, position) pairs, head flags, block scan -> slots.
-// Pass 0 counts the distinct pages (0 when more than PG_MAX: the chunk keeps the 32-bit
-// gathers); pass 1 writes the page list and the page-local 16-bit indices.
+// Pass 0 counts the distinct pages (0 when more than PGMAX, the LDS budget times pg_rounds: the
+// chunk keeps the 32-bit gathers); pass 1 writes the page list and the page-local 16-bit indices
+// (slot x values per page + offset; the kernel stages slots [0, pg_max) first, then the rest).
 // --------------------------------------------------------------------------
 template <int PGV, int PGMAX, bool FILL>
 __global__ __launch_bounds__(256) void k_page_index(int64_t nnz, const int32_t* __restrict__ ci,
@@ -221,8 +222,9 @@ void build_page_index(hgm_ctx* c, hgm_mat* M) {
     free_page_index(M);
     HGM_REQUIRE(stream_chunks(M->nnz) < (int64_t)INT32_MAX, "page index: too many chunks");
     if (M->nnz < SCH) return;
-    if (M->dtype == HGM_F32) build_page_index_t<PG_BYTES / 4, pg_max<float>()>(c, M);
-    else build_page_index_t<PG_BYTES / 8, pg_max<double>()>(c, M);
+    // (PGMAX: the pages a chunk may touch, over all its LDS rounds)
+    if (M->dtype == HGM_F32) build_page_index_t<PG_BYTES / 4, pg_max<float>() * pg_rounds<float>()>(c, M);
+    else build_page_index_t<PG_BYTES / 8, pg_max<double>() * pg_rounds<double>()>(c, M);
     M->variant |= SPMV_PAGED;
 }
 

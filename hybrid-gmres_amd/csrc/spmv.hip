@@ -302,16 +302,67 @@ __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, c
             for (int i = 0; i < NPASS; ++i)
                 if (pid[i] >= 0) pages[(ps + i * PPP) * LPP + pl] = pv[i];
             __syncthreads();
-            T pr[U * VE];
+            if constexpr (pg_rounds<T>() == 1) {
+                T pr[U * VE];
 #pragma unroll
-            for (int u = 0; u < U; ++u)
+                for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int e = 0; e < VE; ++e) pr[u * VE + e] = vv[u][e] * prod[lc[u][e]];
-            __syncthreads();                                          // pages no longer read
+                    for (int e = 0; e < VE; ++e) pr[u * VE + e] = vv[u][e] * prod[lc[u][e]];
+                __syncthreads();                                      // pages no longer read
 #pragma unroll
-            for (int u = 0; u < U; ++u)
+                for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int e = 0; e < VE; ++e) prod[VE * threadIdx.x + u * VE * BS + e] = pr[u * VE + e];
+                    for (int e = 0; e < VE; ++e) prod[VE * threadIdx.x + u * VE * BS + e] = pr[u * VE + e];
+            } else {
+                // (a one-round fast path beside this loop measured slower: 66 vs 62 VGPRs,
+                // C5 A 1.33-1.35 vs 1.32-1.33 ms, profiles/r2_tworound_c5.jsonl)
+                // more than PGM pages: later rounds restage the buffer with the next PGM pages;
+                // each entry is multiplied in its page's round (products: the same bits)
+                constexpr int PGM = pg_max<T>(), LIM = PGM * (PG_BYTES / (int)sizeof(T));
+                T pr[U * VE];
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int e = 0; e < VE; ++e) pr[u * VE + e] = vv[u][e];
+                const int nround = (npg + PGM - 1) / PGM;             // block-uniform
+#pragma unroll 1
+                for (int r = 0; r < nround; ++r) {
+                    if (r > 0) {
+                        // in quarters: the products and the segment bookkeeping are live here
+                        constexpr int NQ = NPASS >= 4 ? NPASS / 4 : 1;
+                        __syncthreads();                              // the previous round's pages no longer read
+#pragma unroll 1
+                        for (int i0 = 0; i0 < NPASS; i0 += NQ) {
+                            int qid[NQ];
+                            V16 qv[NQ];
+#pragma unroll
+                            for (int i = 0; i < NQ; ++i) {
+                                const int sl = r * PGM + ps + (i0 + i) * PPP;
+                                qid[i] = sl < npg ? pg.pids[pp0 + sl] : -1;
+                            }
+#pragma unroll
+                            for (int i = 0; i < NQ; ++i)
+                                if (qid[i] >= 0) qv[i] = load_page16<V16>(x, qid[i], pl, pg.xlen);
+#pragma unroll
+                            for (int i = 0; i < NQ; ++i)
+                                if (qid[i] >= 0) pages[(ps + (i0 + i) * PPP) * LPP + pl] = qv[i];
+                        }
+                        __syncthreads();
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+#pragma unroll
+                        for (int e = 0; e < VE; ++e) {
+                            const int li = lc[u][e] - r * LIM;
+                            if (li >= 0 && li < LIM) pr[u * VE + e] = pr[u * VE + e] * prod[li];
+                        }
+                }
+                __syncthreads();                                      // pages no longer read
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int e = 0; e < VE; ++e) prod[VE * threadIdx.x + u * VE * BS + e] = pr[u * VE + e];
+            }
             staged = true;
         }
     }

@@ -158,6 +158,19 @@ def _ragged_matrix():
     return sp.vstack(rows).tocsr()
 
 
+def _page_heavy_matrix():
+    """Rows of 2048 entries drawn from column windows of 3000-12000: 4096-entry chunks touching
+    ~190-750 distinct 128-B pages of x, i.e. one and two LDS rounds of the paged kernel (256
+    pages fp64 / 128 fp32 per round) and the 32-bit fallback beyond two."""
+    rng = np.random.default_rng(7)
+    rows, W, n = [], 1500, 64 * 1500 + 12000
+    for i in range(64):
+        span = (3000, 5000, 7000, 12000)[i % 4]
+        cols = np.sort(rng.choice(span, size=2048, replace=False)) + i * W
+        rows.append(sp.csr_matrix((rng.standard_normal(cols.size), (np.zeros(cols.size, int), cols)), shape=(1, n)))
+    return sp.vstack(rows).tocsr()
+
+
 @pytest.mark.parametrize("variant,group", [(8, 8), (8, 16), (10, 32), (8, 64), (9, 4)])
 def test_stream_spmv(gpu_ctx, P64, variant, group):
     """nnz-balanced streaming kernel (chunked, LDS-staged, fixed-order fix-up) on the
@@ -194,9 +207,10 @@ def test_paged_stream_spmv_bitwise(gpu_ctx, P64, group, dtype):
     """Paged x gathers (variant bit 16: the chunk's x pages staged in LDS, 16-bit page-local
     indices) give exactly the unpaged streaming kernel's bits -- plain and banded, fp64 and
     fp32, every epilogue through a solve -- on the tomography operators and a ragged matrix
-    (empty rows, rows spanning several chunks, a final partial chunk)."""
+    (empty rows, rows spanning several chunks, a final partial chunk), and on chunks that stage
+    their pages in two LDS rounds (or fall back to 32-bit gathers beyond two)."""
     rng = np.random.default_rng(11)
-    for M in (P64.A, P64.B, _ragged_matrix()):
+    for M in (P64.A, P64.B, _ragged_matrix(), _page_heavy_matrix()):
         Mo = hgmres.SparseOperator.from_scipy(M, gpu_ctx, dtype=dtype)
         x = rng.standard_normal(M.shape[1])
         for bands in ((0,) if M.shape[1] <= 2000 else (0, M.shape[1] // 5 + 1)):
