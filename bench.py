@@ -293,7 +293,8 @@ def main():
         d = spmv[dom_name]
         traffic = None
         tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
-        if os.path.exists(tf):
+        # the committed PMC traffic is the single-GPU operator's: not a shard's
+        if os.path.exists(tf) and not shard:
             try:
                 traffic = json.load(open(tf)).get(dom_name)
             except Exception:   # noqa: BLE001
