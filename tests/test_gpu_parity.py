@@ -454,6 +454,33 @@ def test_ab_gram_error_monitor(gpu_ctx, tag, fn, haslam, N, na):
     hist_ok(og[2], ref[2], TOL)
 
 
+def test_ab_gram_error_monitor_stops(gpu_ctx):
+    """The m-space Gram error monitor through a tol stop (x formed from the last accepted y at
+    the end) and an Arnoldi breakdown, against the explicit reconstruction (gram_err = 0)."""
+    P = tomo_problem(64, 90, noise=1e-2, seed=0)
+    with gpu_ctx.options(mgs_single=0):
+        full = hgmres.ABgmres_nonhybrid_bounds(P.A, None, P.b, P.x_true, 0.0, 12, ctx=gpu_ctx)
+        tol = float(full[2][4]) * (1 + 1e-9)                 # `<=` stops at k = 5 (*_bounds.m:79-83)
+        runs = []
+        for ge in (1, 0):
+            with gpu_ctx.options(gram_err=ge):
+                runs.append(hgmres.ABgmres_nonhybrid_bounds(P.A, None, P.b, P.x_true, tol, 12, ctx=gpu_ctx))
+    (xg, eg, rg, kg), (xe, ee, re_, ke) = (r[:4] for r in runs)
+    assert kg == ke == 5 and np.array_equal(rg, re_)
+    assert rel(xg, xe) < 1e-13
+    hist_ok(eg, ee, 1e-12)
+    ref = R.ABgmres_nonhybrid_bounds(P.A, P.A.T.tocsr(), P.b, P.x_true, tol, 12)
+    assert ref[3] == 5 and rel(xg, ref[0]) < TOL
+    # breakdown at k = 1 (A*A'*e1 = e1, H(2,1) = 0): x is never assigned (*_bounds.m), either form
+    A = sp.csr_matrix(np.diag([1.0, 2.0, 2.0, 1.0]))
+    b, xt = np.array([1.0, 0.0, 0.0, 0.0]), np.ones(4)
+    with pytest.raises(R.OutputNotAssigned):
+        R.ABgmres_nonhybrid_bounds(A, A.T.tocsr(), b, xt, 0.0, 4)
+    for ge in (1, 0):
+        with gpu_ctx.options(gram_err=ge), pytest.raises(hgmres.OutputNotAssigned):
+            hgmres.ABgmres_nonhybrid_bounds(A, None, b, xt, 0.0, 4, ctx=gpu_ctx)
+
+
 def test_gmres_determinism(gpu_ctx, P64):
     o1 = hgmres.hybrid_ab_gmres_rtp(P64.A, P64.B, P64.b, P64.x_true, 0.0, 15, 1e-2, ctx=gpu_ctx, return_H=True)
     o2 = hgmres.hybrid_ab_gmres_rtp(P64.A, P64.B, P64.b, P64.x_true, 0.0, 15, 1e-2, ctx=gpu_ctx, return_H=True)
