@@ -482,8 +482,17 @@ __global__ __launch_bounds__(BS) void k_band_reduce(int64_t rows, int nbands, co
     const T h = pn_fin<T, EPI>(pn, pn_pre<T, EPI>(pn), hsh);
     if constexpr (EPI == EPI_ADD || EPI == EPI_SUB) a = pn_coef<T>(pn, a);
     for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BS) {
+        // eight independent (read-once, nontemporal) loads in flight, summed in band order
         T s = 0;
-        for (int b = 0; b < nbands; ++b) s += ypart[(int64_t)b * rows + r];
+        int b = 0;
+        for (; b + 8 <= nbands; b += 8) {
+            T v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = __builtin_nontemporal_load(ypart + (int64_t)(b + i) * rows + r);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s += v[i];
+        }
+        for (; b < nbands; ++b) s += ypart[(int64_t)b * rows + r];
         y[r] = apply_epi_pn<T, EPI>(s, a, z, r, pn, h);
     }
 }
