@@ -293,7 +293,10 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // the sweep as a side job, so an iteration's reconstruction reads no n-vector: the kept B*Q
     // columns are combined once, at the end (C4: the 0.3 ms GEMV per iteration)
     const bool pair_t = B && (B->transpose_of == A->uid || A->transpose_of == B->uid);
-    const bool gem_ab = bq_res && gem_ok && sp.proj != PROJ_ABRTP && pair_t;
+    // (multi-GPU too: the m-space sweep is replicated, the side dot is all-reduced and the
+    // Gram row published with the H column; a shard pair A_g = B_g' qualifies)
+    const bool gem_ab = bq_res && orth == HGM_MGS && mgs_gram_ok(c, ldq, maxit, dist) && c->num.gram_err &&
+                        (zc ? c->num.ring_poll : true) && sp.proj != PROJ_ABRTP && pair_t;
     const bool gem = gem_n || gem_ab;
     const double gem_min = c->num.gram_err_min;
     const size_t LQ = (size_t)maxit + 2, offQG = offS + 4;
@@ -370,6 +373,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         read_scalars(c, 0, 3);
         nb = std::sqrt(c->hscal[S_NB]);
         nxt = std::sqrt(c->hscal[S_NXT]);
+        xt2 = c->hscal[S_NXT];
         beta = std::sqrt(c->hscal[S_BETA]);               // :10  beta = norm(r0)
         div_scalar<T>(c, dim, q0, q0, (T)beta);           // :13  Q(:,1) = r0 / beta
     }
@@ -460,6 +464,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             mgs<T>(c, dim, Q, ldq, kq, Hcol, dist, (!nspace && ABQ) ? ABQ + (int64_t)kq * ldaq : nullptr,
                    gem_ab ? &zx : side, defer, pending_in ? (const T*)pn_h : nullptr,
                    gem ? (gem_n ? xt : b) : nullptr, gem ? dr + offQG + (size_t)kq * LQ : nullptr);
+            if (gem_ab && dist_n(c)) allreduce(c, zx.out, 1);   // x_true'(B*q_k) over the pixel shards
         }
         // Step kq-1's column is complete (H(kq,kq-1) came from this step's A product).  The
         // event goes at the end of the step: a marker between two kernels costs a bubble.
@@ -470,6 +475,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         }
         if (pend.np == 0) {                               // else: recorded at the end of step kq+1
             publish((size_t)kq * LH, LH);
+            if (gem_ab) publish(offQG + (size_t)kq * LQ, (size_t)kq + 3);   // the Gram row (m-space)
             step_record(c, kq);
         }
     };
@@ -502,7 +508,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             // (want_x false: the m-space Gram error monitor has the error, x is formed at the end)
             recon<T>(c, n, kk, BQ, ldbq, yk, want_x ? x : nullptr, xt, eslot, m, ABQ, ldaq, b, rslot);
             x_pending = want_x ? -1 : kq;
-            if (dist_n(c)) allreduce(c, eslot, 1);
+            if (dist_n(c) && want_x) allreduce(c, eslot, 1);
             publish(offM + 2 * (size_t)kq, 2);
             pipe_record(c);
             return;
