@@ -1,20 +1,23 @@
-"""Median gap between consecutive kernels on the main queue of a rocprofv3 kernel trace.
-usage: python scripts/trace_gaps.py <kernel_trace.csv>"""
-import collections
-import csv
-import sys
-
-rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-q = collections.Counter(r["Queue_Id"] for r in rows if "k_spmv" in r["Kernel_Name"]).most_common(1)[0][0]
-main = [r for r in rows if r["Queue_Id"] == q]
-short = lambda r: r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").replace("hgm::", "")  # noqa: E731
-gaps = collections.defaultdict(list)
-for a, b in zip(main, main[1:]):
-    gaps[(short(a), short(b))].append((int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1000)
-for k, v in sorted(gaps.items(), key=lambda x: -len(x[1]))[:10]:
-    v.sort()
-    print(f"{k[0]:>16} -> {k[1]:<16} n={len(v):4d} median {v[len(v) // 2]:7.2f} us  p10 {v[len(v) // 10]:6.2f}")
-durs = collections.defaultdict(list)
-for r in main:
-    durs[short(r)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000)
-print({k: round(sorted(v)[len(v) // 2], 2) for k, v in durs.items() if len(v) > 20})
+"""Kernel time and inter-kernel gaps over the second half of a rocprofv3 kernel trace (the steady
+solves of a bench run).  usage: python scripts/trace_gaps.py <trace_kernel_trace.csv>"""
+import csv, sys, collections
+f=sys.argv[1]
+v=[]
+for r in csv.DictReader(open(f)):
+    v.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'].split('(')[0][-60:], r.get('Stream_Id', '')))
+v.sort()
+# steady region: last solve = kernels after the last-but-one k_spmv_stream burst... take last 40% of spmv kernels
+sp=[i for i,x in enumerate(v) if 'spmv_stream' in x[2]]
+lo=sp[len(sp)//2]; hi=sp[-1]
+seg=v[lo:hi+1]
+span=(seg[-1][1]-seg[0][0])/1e3
+busy=sum((x[1]-x[0]) for x in seg)/1e3
+print('span us',span,'busy us',busy,'frac',busy/span, 'spmv', len([x for x in seg if 'spmv_stream' in x[2]]))
+gaps=collections.defaultdict(float); cnt=collections.Counter()
+for a,b in zip(seg,seg[1:]):
+    g=(b[0]-a[1])/1e3
+    if g>0: gaps[(a[2],b[2])]+=g; cnt[(a[2],b[2])]+=1
+for k,g in sorted(gaps.items(), key=lambda t:-t[1])[:12]: print(round(g,1), cnt[k], k)
+tot=collections.defaultdict(float)
+for x in seg: tot[x[2]]+=(x[1]-x[0])/1e3
+for k,t in sorted(tot.items(), key=lambda t:-t[1])[:14]: print(round(t,1), k)
