@@ -493,6 +493,7 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
         case HGM_OPT_MGS_FUSED: n.mgs_fused = v != 0.0; break;
         case HGM_OPT_LSQR_DEV: n.lsqr_dev = v != 0.0; break;
         case HGM_OPT_PAGED16: n.paged16 = v != 0.0; break;
+        case HGM_OPT_BAND_DUAL: n.band_dual = v != 0.0; break;
         default: return bad("unknown option");
     }
     return HGM_OK;
@@ -518,6 +519,7 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_MGS_FUSED: *v = n.mgs_fused; break;
         case HGM_OPT_LSQR_DEV: *v = n.lsqr_dev; break;
         case HGM_OPT_PAGED16: *v = n.paged16; break;
+        case HGM_OPT_BAND_DUAL: *v = n.band_dual; break;
         default: return HGM_E_ARG;
     }
     return HGM_OK;

@@ -76,6 +76,7 @@ struct Numerics {
     bool mgs_fused = true;          // one-reduction MGS: solve folded into the update kernel
     bool lsqr_dev = true;           // LSQR: device-resident beta/alpha/rotation (no host round trip)
     bool paged16 = true;            // streaming SpMV: paged gathers also for 16-bit-index operators
+    bool band_dual = true;          // banded tiled ray-major operators: steep rows in row strips
 };
 
 }  // namespace hgm
@@ -162,8 +163,12 @@ struct hgm_mat {
     // Column-banded copy (cache blocking of the x gather): the columns are
     // cut into nbands contiguous bands of band_w pixels; segment (b, r) of row r that lies
     // in band b is [brp[b*rows + r], brp[b*rows + r + 1]) of bci/bval (band-major order).
+    // band_dual: rows whose pixel-row span exceeds their pixel-column span (steeper than 45
+    // deg) are cut into strips of band_w / N pixel ROWS instead (same band count, tiled N x N
+    // grid), so both kinds of ray cross their strips in short chords.
     int64_t band_w = 0;
     int nbands = 0;
+    bool band_dual = false;
     int bgroup = 16;         // lanes per segment in the banded kernel
     int64_t* brp = nullptr;
     int32_t* bci = nullptr;

@@ -239,6 +239,7 @@ static void free_bands(hgm_mat* M) {
     M->bval = nullptr;
     M->nbands = 0;
     M->band_w = 0;
+    M->band_dual = false;
 }
 
 void mat_free(hgm_mat* M) {
@@ -256,23 +257,56 @@ void mat_free(hgm_mat* M) {
 // --------------------------------------------------------------------------
 // column bands (cache blocking of the x gather for long-row operators)
 // --------------------------------------------------------------------------
+// Band of a stored column.  Column strips: s / W.  Dual (tiled N x N grid): a
+// steep row (pixel-row span > pixel-column span) takes the strip of h = W / N pixel ROWS its
+// pixel lies in instead; in the tile-column-major order that is (s mod tile*N) / (h*tile).
+struct BandKey {
+    int64_t W = 0;
+    int dual = 0, tile = 1;
+    int64_t N = 0, tN = 0, rdiv = 1;
+};
+
+__device__ __forceinline__ bool row_steep(const BandKey& k, const int64_t* __restrict__ rp,
+                                          const int32_t* __restrict__ ci, int64_t r) {
+    if (!k.dual) return false;
+    const int64_t t = k.tile, Nt = k.N / t;
+    int64_t rmin = INT64_MAX, rmax = -1, cmin = INT64_MAX, cmax = -1;
+    for (int64_t i = rp[r]; i < rp[r + 1]; ++i) {
+        const int64_t s = ci[i], q = s / (t * t);
+        const int64_t pr = (q % Nt) * t + s % t, pc = (q / Nt) * t + (s / t) % t;
+        rmin = pr < rmin ? pr : rmin;
+        rmax = pr > rmax ? pr : rmax;
+        cmin = pc < cmin ? pc : cmin;
+        cmax = pc > cmax ? pc : cmax;
+    }
+    return rmax >= 0 && rmax - rmin > cmax - cmin;
+}
+
+__device__ __forceinline__ int64_t band_of(const BandKey& k, int64_t s, bool steep) {
+    return steep ? (s % k.tN) / k.rdiv : s / k.W;
+}
+
 // one thread per row, sequential over the row (each row is owned by one thread: no races)
-__global__ void k_band_count(int64_t rows, int64_t W, const int64_t* __restrict__ rp,
+__global__ void k_band_count(int64_t rows, BandKey key, const int64_t* __restrict__ rp,
                              const int32_t* __restrict__ ci, int64_t* __restrict__ cnt) {
-    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BS)
-        for (int64_t i = rp[r]; i < rp[r + 1]; ++i) cnt[(int64_t)(ci[i] / W) * rows + r] += 1;
+    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BS) {
+        const bool steep = row_steep(key, rp, ci, r);
+        for (int64_t i = rp[r]; i < rp[r + 1]; ++i) cnt[band_of(key, ci[i], steep) * rows + r] += 1;
+    }
 }
 
 template <typename T>
-__global__ void k_band_fill(int64_t rows, int64_t W, const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+__global__ void k_band_fill(int64_t rows, BandKey key, const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
                             const T* __restrict__ val, int64_t* __restrict__ cur, int32_t* __restrict__ bci,
                             T* __restrict__ bval) {
-    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BS)
+    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < rows; r += (int64_t)gridDim.x * BS) {
+        const bool steep = row_steep(key, rp, ci, r);
         for (int64_t i = rp[r]; i < rp[r + 1]; ++i) {
-            const int64_t p = cur[(int64_t)(ci[i] / W) * rows + r]++;
+            const int64_t p = cur[band_of(key, ci[i], steep) * rows + r]++;
             bci[p] = ci[i];
             bval[p] = val[i];
         }
+    }
 }
 
 // Kernel defaults from the gfx950 sweep (profiles/):
@@ -357,6 +391,21 @@ void set_bands(hgm_ctx* c, hgm_mat* M, int64_t W) {
     hipStream_t st = c->stream;
     const size_t vs = M->dtype == HGM_F32 ? 4 : 8;
     const int64_t nseg = nb * M->rows;
+    // dual strips: a whole tiled N x N grid cut into square-count strips (h rows = W / N columns)
+    BandKey key;
+    key.W = W;
+    const PixOrder& o = M->col_order;
+    if (c->num.band_dual && !o.trivial() && o.super <= 1 && o.N > 0 && M->cols == (int64_t)o.N * o.N &&
+        W % o.N == 0) {
+        const int64_t h = W / o.N, t = o.tile > 1 ? o.tile : 1;
+        if (h % t == 0 && o.N % h == 0 && o.N % t == 0) {
+            key.dual = 1;
+            key.tile = (int)t;
+            key.N = o.N;
+            key.tN = t * o.N;
+            key.rdiv = h * t;
+        }
+    }
     int64_t* cnt = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
@@ -367,16 +416,16 @@ void set_bands(hgm_ctx* c, hgm_mat* M, int64_t W) {
         HGM_HIP(hipMalloc(&cnt, sizeof(int64_t) * (nseg + 1)));
         HGM_HIP(hipMemsetAsync(cnt, 0, sizeof(int64_t) * (nseg + 1), st));
         const int g = grid_cap(M->rows);
-        k_band_count<<<g, BS, 0, st>>>(M->rows, W, M->rp, M->ci, cnt);
+        k_band_count<<<g, BS, 0, st>>>(M->rows, key, M->rp, M->ci, cnt);
         HGM_HIP(hipGetLastError());
         HGM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, M->brp, (int)(nseg + 1), st));
         HGM_HIP(hipMalloc(&tmp, tmp_bytes));
         HGM_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, M->brp, (int)(nseg + 1), st));
         HGM_HIP(hipMemcpyAsync(cnt, M->brp, sizeof(int64_t) * (nseg + 1), hipMemcpyDeviceToDevice, st));
         if (M->dtype == HGM_F32)
-            k_band_fill<float><<<g, BS, 0, st>>>(M->rows, W, M->rp, M->ci, (const float*)M->val, cnt, M->bci, (float*)M->bval);
+            k_band_fill<float><<<g, BS, 0, st>>>(M->rows, key, M->rp, M->ci, (const float*)M->val, cnt, M->bci, (float*)M->bval);
         else
-            k_band_fill<double><<<g, BS, 0, st>>>(M->rows, W, M->rp, M->ci, (const double*)M->val, cnt, M->bci, (double*)M->bval);
+            k_band_fill<double><<<g, BS, 0, st>>>(M->rows, key, M->rp, M->ci, (const double*)M->val, cnt, M->bci, (double*)M->bval);
         HGM_HIP(hipGetLastError());
         HGM_HIP(hipStreamSynchronize(st));
     } catch (...) {
@@ -389,6 +438,7 @@ void set_bands(hgm_ctx* c, hgm_mat* M, int64_t W) {
     (void)hipFree(tmp);
     M->band_w = W;
     M->nbands = (int)nb;
+    M->band_dual = key.dual != 0;
     const double avg = (double)M->nnz / (double)nseg;
     M->bgroup = avg >= 96 ? 32 : (avg >= 24 ? 16 : 8);
     // streaming index over the (band,row) segments; ~2/3 of them are non-empty for a

@@ -113,8 +113,12 @@ enum hgm_ctx_option {
                                       block (2 launches per sweep), instead of a one-block solve kernel [1] */
     HGM_OPT_LSQR_DEV = 15,         /* lsqr_solver (single rank): beta, alpha, the Givens rotation and the stop
                                       test stay on the device (same bits, no host round trip per iteration) [1] */
-    HGM_OPT_PAGED16 = 16           /* streaming SpMV: LDS-paged x gathers also for operators with <= 65,536
+    HGM_OPT_PAGED16 = 16,          /* streaming SpMV: LDS-paged x gathers also for operators with <= 65,536
                                       columns (instead of their 16-bit column indices) [1] */
+    HGM_OPT_BAND_DUAL = 17         /* banded ray-major operators over a whole tiled N x N grid: rows steeper
+                                      than 45 deg are cut into 64-pixel-row strips instead of 64-column strips,
+                                      so every ray crosses its strips [1]; read when an operator is banded
+                                      (creation, hgm_mat_set_bands) */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for

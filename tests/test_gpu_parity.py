@@ -240,6 +240,47 @@ def test_paged_stream_spmv_bitwise(gpu_ctx, P64, group, dtype):
                 assert np.array_equal(np.asarray(u), np.asarray(w))
 
 
+@pytest.mark.parametrize("dtype", [0, 1])
+def test_dual_strip_bands(gpu_ctx, dtype):
+    """Dual strips (HGM_OPT_BAND_DUAL): on a tiled ray-major operator over the
+    whole N x N grid, rows steeper than 45 deg are banded in 64-pixel-row strips instead of
+    64-column strips.  Every entry is still multiplied once: the product equals the CSR product
+    to rounding, repeats bitwise, its paged and unpaged streaming gathers agree bitwise, and a
+    solve through it stays within the parity bar of the column-strip banding."""
+    N, na = 256, 30
+    A = hgmres.SparseOperator.siddon(N, na, ctx=gpu_ctx, dtype=dtype)
+    assert A.pixel_order("cols")[1] == 4
+    As = A.to_scipy()
+    x = np.random.default_rng(5).standard_normal(N * N)
+    scale = np.abs(As) @ np.abs(x) + 1e-300
+    tol = 1e-14 if dtype == 0 else 2e-5
+    ys = {}
+    for dual in (0, 1):
+        with gpu_ctx.options(band_dual=dual):
+            A.set_bands(64 * N, 0)
+        for v in (8 | 2 | 4, 8 | 2 | 4 | 16):
+            A.tune(v, 4)
+            y = A @ x
+            assert np.array_equal(y, A @ x), (dual, v)
+            assert np.max(np.abs(y - As @ x) / scale) < tol, (dual, v)
+            ys[dual, v] = y
+        assert np.array_equal(ys[dual, 8 | 2 | 4], ys[dual, 8 | 2 | 4 | 16]), dual
+    # steep rows are split at other pixels: the two bandings differ in rounding only
+    assert not np.array_equal(ys[0, 14], ys[1, 14])
+    if dtype == 0:
+        B = A.T
+        b = As @ np.random.default_rng(6).random(N * N)
+        xt = np.ones(N * N)
+        outs = []
+        for dual in (0, 1):
+            with gpu_ctx.options(band_dual=dual):
+                A.set_bands(64 * N, 0)
+            outs.append(hgmres.hybrid_ab_gmres_rtp(A, B, b, xt, 0.0, 10, 1e-2, ctx=gpu_ctx, return_H=True))
+        H_ok(outs[1][-1], outs[0][-1], 1e-12)
+        assert rel(outs[1][0], outs[0][0]) < 1e-12
+        hist_ok(outs[1][2], outs[0][2], 1e-12)
+
+
 @pytest.mark.parametrize("width,group", [(512, 8), (1000, 16), (1 << 11, 32), (333, 64)])
 def test_banded_spmv(gpu_ctx, P64, width, group):
     """Column-banded A (cache-blocked x gather) equals the plain CSR product; bands are
