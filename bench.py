@@ -186,8 +186,8 @@ def main():
     for o in args.opt:
         name, val = o.split("=", 1)
         ctx.set_option(name, float(val))
-        if name == "band_dual" and not shard:
-            A.set_bands(-1)            # the option is read when an operator is banded: re-band A
+        if name == "band_dual":        # read when an operator is banded: re-band A
+            A.set_bands(64 * wl["N"] if shard else -1)
     for M, t in ((A, args.tune_a), (B, args.tune_b)):
         if t:
             v, g = t.split(":")

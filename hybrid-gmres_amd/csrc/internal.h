@@ -149,6 +149,9 @@ struct hgm_mat {
     int64_t rows = 0, cols = 0, nnz = 0;
     // index-space orders of the rows / columns (pixel spaces may be stored tiled)
     hgm::PixOrder row_order, col_order;
+    // grid of a trivially-ordered index space that is a window of whole tile columns of a tiled
+    // N x N grid (a pixel shard: hgm_mat_row_slice / transpose); only the band geometry reads it
+    hgm::PixOrder row_grid, col_grid;
     int dtype = HGM_F64;
     int64_t* rp = nullptr;   // rows+1
     int32_t* ci = nullptr;   // nnz

@@ -53,6 +53,9 @@ hgm_mat* row_slice(hgm_ctx* c, const hgm_mat* M, int64_t lo, int64_t hi) {
     HGM_HIP(hipMemcpy(&b[1], M->rp + hi, sizeof(int64_t), hipMemcpyDeviceToHost));
     hgm_mat* S = mat_alloc(c, hi - lo, M->cols, b[1] - b[0], M->dtype);
     S->col_order = M->col_order;
+    // a window of whole tile columns keeps the grid's strip geometry (dual bands of A_g = S')
+    const PixOrder& ro = !M->row_order.trivial() ? M->row_order : M->row_grid;
+    if (!ro.trivial() && ro.super <= 1 && lo % ((int64_t)std::max(ro.tile, 1) * ro.N) == 0) S->row_grid = ro;
     try {
         k_rebase<<<grid_cap(hi - lo + 1), BS, 0, st>>>(hi - lo + 1, M->rp + lo, b[0], S->rp);
         HGM_HIP(hipGetLastError());
@@ -386,26 +389,30 @@ void set_bands(hgm_ctx* c, hgm_mat* M, int64_t W) {
     free_page_index(M);   // it indexes the stream the bands replace; the caller rebuilds it
     free_bands(M);
     if (W <= 0 || W >= M->cols || M->nnz == 0) return;
-    const int64_t nb = (M->cols + W - 1) / W;
+    // dual strips: the columns are a window of whole tile columns of a tiled
+    // N x N grid (the full grid, or a pixel shard's slice of it).  Steep rows take strips of h
+    // pixel rows of the same pixel count as a column strip: h = W N / cols (64 on the full grid).
+    BandKey key;
+    key.W = W;
+    int64_t nb = (M->cols + W - 1) / W;
+    const PixOrder& o = !M->col_order.trivial() ? M->col_order : M->col_grid;
+    if (c->num.band_dual && !o.trivial() && o.super <= 1 && o.N > 0) {
+        const int64_t t = o.tile > 1 ? o.tile : 1, tN = t * o.N;
+        int64_t h = (int64_t)((double)W * o.N / (double)M->cols + 0.5);
+        h = (h + t - 1) / t * t;
+        if (o.N % t == 0 && M->cols % tN == 0 && M->cols <= (int64_t)o.N * o.N && h >= t && h < o.N) {
+            key.dual = 1;
+            key.tile = (int)t;
+            key.N = o.N;
+            key.tN = tN;
+            key.rdiv = h * t;
+            nb = std::max(nb, (o.N + h - 1) / h);
+        }
+    }
     HGM_REQUIRE(nb * M->rows + 1 < (int64_t)INT32_MAX, "set_bands: too many (band,row) segments");
     hipStream_t st = c->stream;
     const size_t vs = M->dtype == HGM_F32 ? 4 : 8;
     const int64_t nseg = nb * M->rows;
-    // dual strips: a whole tiled N x N grid cut into square-count strips (h rows = W / N columns)
-    BandKey key;
-    key.W = W;
-    const PixOrder& o = M->col_order;
-    if (c->num.band_dual && !o.trivial() && o.super <= 1 && o.N > 0 && M->cols == (int64_t)o.N * o.N &&
-        W % o.N == 0) {
-        const int64_t h = W / o.N, t = o.tile > 1 ? o.tile : 1;
-        if (h % t == 0 && o.N % h == 0 && o.N % t == 0) {
-            key.dual = 1;
-            key.tile = (int)t;
-            key.N = o.N;
-            key.tN = t * o.N;
-            key.rdiv = h * t;
-        }
-    }
     int64_t* cnt = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
@@ -504,6 +511,8 @@ hgm_mat* transpose(hgm_ctx* c, const hgm_mat* M) {
     hgm_mat* T = mat_alloc(c, M->cols, M->rows, nnz, M->dtype);
     T->row_order = M->col_order;
     T->col_order = M->row_order;
+    T->row_grid = M->col_grid;
+    T->col_grid = M->row_grid;
     T->transpose_of = M->uid;
     if (nnz == 0) {
         HGM_HIP(hipMemsetAsync(T->rp, 0, sizeof(int64_t) * (T->rows + 1), st));

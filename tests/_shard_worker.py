@@ -88,6 +88,8 @@ def solve_all(ctx, rank, world):
     tlo, thi = bounds[rank], bounds[rank + 1]
     B2 = Af.T.row_slice(tlo, thi)
     A2 = B2.T
+    A2.set_bands(16 * 64, 0)       # 16-column strips; steep rays in the shard's dual row strips
+    A2.tune(8 | 2 | 4 | 16, 4)     # the paged streaming kernel of the C4 shards
     xs = np.empty(n)
     xs[stored_pixel_index(64, 4, 0)] = P.x_true
     out_ = hgmres.ABgmres_nonhybrid_bounds(A2, B2, P.b, xs[tlo:thi], 0.0, 12, ctx=ctx, return_H=True)

@@ -267,6 +267,23 @@ def test_dual_strip_bands(gpu_ctx, dtype):
         assert np.array_equal(ys[dual, 8 | 2 | 4], ys[dual, 8 | 2 | 4 | 16]), dual
     # steep rows are split at other pixels: the two bandings differ in rounding only
     assert not np.array_equal(ys[0, 14], ys[1, 14])
+    # a pixel shard (whole tile columns of the stored order, bench.py build_shard): A_g = B_g'
+    # keeps the grid's strip geometry, with row strips of the column strips' pixel count
+    col = 4 * N
+    B_s = A.T.row_slice(3 * col, 35 * col)
+    A_s = B_s.T
+    Ss = A_s.to_scipy()
+    xl = x[: Ss.shape[1]]
+    sc = np.abs(Ss) @ np.abs(xl) + 1e-300
+    yl = {}
+    for dual in (0, 1):
+        with gpu_ctx.options(band_dual=dual):
+            A_s.set_bands(16 * N, 0)
+        A_s.tune(8 | 2 | 4 | 16, 4)
+        yl[dual] = A_s @ xl
+        assert np.array_equal(yl[dual], A_s @ xl)
+        assert np.max(np.abs(yl[dual] - Ss @ xl) / sc) < tol, dual
+    assert not np.array_equal(yl[0], yl[1])
     if dtype == 0:
         B = A.T
         b = As @ np.random.default_rng(6).random(N * N)
