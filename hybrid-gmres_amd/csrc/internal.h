@@ -205,8 +205,11 @@ constexpr int SCH = HGM_SCH;
 // x pages per streaming chunk that the paged kernel stages in LDS (one 128-B line each).  The
 // chunk's product buffer (SCH values) is reused for them, extended to HGM_PG_MAX64 pages in fp64
 // (C4 A chunks touch 235 pages on average, up to 272: scripts/page_stats.py); fp32: 128 pages.
+// With the dual strips the fp64 chunks over 256 pages are the axis-aligned angles' (256-269):
+// 272 pages (34 KB of LDS) took C4 A from 2.07-2.10 to 2.05-2.06 ms, C3 A equal within noise
+// (alternating builds, profiles/r2_pgmax272_ab.jsonl); 320 / 384 were slower (r2_pgmax_sweep.txt).
 #ifndef HGM_PG_MAX64
-#define HGM_PG_MAX64 256
+#define HGM_PG_MAX64 272
 #endif
 #ifndef HGM_PG_MAX32
 #define HGM_PG_MAX32 (SCH * 4 / 128)
