@@ -125,3 +125,33 @@ def test_stored_pixel_index_is_the_tiled_permutation():
     assert sorted(t.tolist()) == list(range(256))
     assert t[0 + 8 * 16] == 2 * 64                              # (r=0, c=8): third super-block (column-major)
     np.testing.assert_array_equal(stored_pixel_index(8, 1, 0), np.arange(64))
+
+
+@pytest.mark.parametrize("N,tile", [(64, 4), (256, 4), (128, 1)])
+def test_dual_strip_band_key_is_the_pixel_strip(N, tile):
+    """The band key of the dual strips (csrc/ops.hip BandKey) restated on the host:
+    in the tile-column-major stored order, s / (64 N) is the 64-pixel COLUMN strip and
+    (s mod tile*N) / (64 tile) the 64-pixel ROW strip of the pixel; the coordinates row_steep
+    recovers from s are the pixel's own; and a shard window of whole tile columns keeps both
+    keys, with row strips of h = W N / cols rows (the column strips' pixel count)."""
+    from hgmres.core import stored_pixel_index
+    p = np.arange(N * N, dtype=np.int64)
+    r, c = p % N, p // N
+    s = stored_pixel_index(N, tile, 0)
+    W, t, Nt = 64 * N if N >= 128 else 16 * N, tile, N // tile
+    h = W // N
+    np.testing.assert_array_equal(s // W, c // h)
+    np.testing.assert_array_equal((s % (t * N)) // (h * t), r // h)
+    q = s // (t * t)
+    np.testing.assert_array_equal((q % Nt) * t + s % t, r)          # pixel row from s
+    np.testing.assert_array_equal((q // Nt) * t + (s // t) % t, c)  # pixel column from s
+    # a shard of tile columns [4, 4 + k): local stored positions s - lo
+    k = N // (2 * t)
+    lo, hi = 4 * t * N, (4 + k) * t * N
+    sel = (s >= lo) & (s < hi)
+    sl = s[sel] - lo
+    cols = hi - lo
+    hs = W * N // cols
+    assert hs % t == 0 and N % hs == 0
+    np.testing.assert_array_equal((sl % (t * N)) // (hs * t), r[sel] // hs)
+    assert N // hs == -(-cols // W)            # as many row strips as column strips
