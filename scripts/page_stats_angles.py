@@ -1,7 +1,10 @@
 """Pages of x per 4096-entry chunk of the banded ray-major A (64-column strips of the 4 x 4-tiled
 order), per projection angle: which chunks exceed the LDS page budget (256 pages fp64, 512 fp32)
 and fall back to 32-bit gathers.  Host-only; N = 2048 with C4's 47 angles (a chunk's page count
-depends on the strip width and the angle, not on N).  usage: python scripts/page_stats_angles.py"""
+depends on the strip width and the angle, not on N).  --dual: the dual strips (HGM_OPT_BAND_DUAL,
+csrc/ops.hip BandKey): rays whose pixel-row span exceeds their pixel-column span are banded in
+64-pixel-row strips (18.8 % -> 3.2 % of the fp64 chunks over 256 pages).
+usage: python scripts/page_stats_angles.py [--dual]"""
 import math
 import os
 import sys
@@ -16,6 +19,7 @@ CH, PAGE = 4096, 16
 
 
 def main():
+    dual = "--dual" in sys.argv
     N, na = 2048, 47
     bands = (8, 16, 24)                      # strips of 64 pixel columns (tile columns 16b..16b+15)
     p, theta, s = geometry(N, na)
@@ -32,6 +36,16 @@ def main():
             pc, pr = col // N, col % N
             stored = ((pc // 4) * (N // 4) + pr // 4) * 16 + (pc % 4) * 4 + pr % 4
             b = stored // st_cols
+            if dual and col.size:
+                rid = np.repeat(np.arange(d.size), cnt)
+                span = []
+                for v in (pr, pc):
+                    hi_, lo_ = np.full(d.size, -1), np.full(d.size, 1 << 30)
+                    np.maximum.at(hi_, rid, v)
+                    np.minimum.at(lo_, rid, v)
+                    span.append(hi_ - lo_)
+                steep = span[0] > span[1]
+                b = np.where(steep[rid], (stored % (4 * N)) // 256, b)
             for bb in bands:
                 segs[bb].append(stored[b == bb])       # ray order, then along-ray order
         for bb in bands:
