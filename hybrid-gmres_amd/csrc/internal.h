@@ -219,7 +219,10 @@ constexpr int PG_BYTES = 128;
 // more than 128 pages, 2.0 % more than 256: scripts/page_stats_angles.py; C5 A 1.43 -> 1.32 ms).
 // fp64: one (a second round cost every chunk more than it saved the 18.8 % above 256 pages:
 // C4 A 2.32 -> 2.42 ms, C3 A 0.25 -> 0.27 ms; profiles/r2_tworound_fp64_ab.jsonl).
-template <typename T> constexpr int pg_rounds() { return sizeof(T) == 4 ? 2 : 1; }
+#ifndef HGM_PG_ROUNDS32
+#define HGM_PG_ROUNDS32 2
+#endif
+template <typename T> constexpr int pg_rounds() { return sizeof(T) == 4 ? HGM_PG_ROUNDS32 : 1; }
 template <typename T> constexpr int pg_max() { return sizeof(T) == 8 ? HGM_PG_MAX64 : HGM_PG_MAX32; }
 template <typename T> constexpr int stream_lds_bytes(bool paged) {
     return paged && pg_max<T>() * PG_BYTES > SCH * (int)sizeof(T) ? pg_max<T>() * PG_BYTES : SCH * (int)sizeof(T);
