@@ -400,7 +400,12 @@ void set_bands(hgm_ctx* c, hgm_mat* M, int64_t W) {
         const int64_t t = o.tile > 1 ? o.tile : 1, tN = t * o.N;
         int64_t h = (int64_t)((double)W * o.N / (double)M->cols + 0.5);
         h = (h + t - 1) / t * t;
-        if (o.N % t == 0 && M->cols % tN == 0 && M->cols <= (int64_t)o.N * o.N && h >= t && h < o.N) {
+        // narrow shards: strips of h >= 4 W / N rows are as slow as the column strips (4 shards of
+        // C4) or slower (8 shards: A_g 0.305 -> 0.336 ms); strips of W / N rows there multiply
+        // the band count (4-6x slower).  Full grid and halves gain (C4 A 2.27 -> 2.11 ms, half
+        // 1.14-1.18 -> 1.11 ms; profiles/r2_shard_kernels_dual.log)
+        if (o.N % t == 0 && M->cols % tN == 0 && M->cols <= (int64_t)o.N * o.N && h >= t && h < o.N &&
+            h * o.N <= 2 * W) {
             key.dual = 1;
             key.tile = (int)t;
             key.N = o.N;

@@ -2,7 +2,8 @@
 stored-order shard for world = 2, 4, 8 exactly as bench.py does (build_shard) and time its
 A_g and B_g products (HIP events on the library stream).  Rank 0's shard is representative:
 parallel-beam nnz per pixel is uniform, so the shards are balanced to 0.02 %.
-usage: python scripts/shard_kernels.py [reps]"""
+usage: python scripts/shard_kernels.py [reps] [dual modes, e.g. 0,1,2: A re-banded under each
+HGM_OPT_BAND_DUAL value]"""
 import ctypes as C
 import json
 import os
@@ -38,6 +39,7 @@ def time_spmv(ctx, lib, M, reps):
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    modes = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [None]
     lib = L.load()
     ctx = hgmres.Context(0)
     wl = bench.WORKLOADS["c4"]
@@ -48,11 +50,16 @@ def main():
             B = A.T
         else:
             A, B, b, xs, (lo, hi), full = bench.build_shard(ctx, wl, 0, world)
-        ra = time_spmv(ctx, lib, A, reps)
         rb = time_spmv(ctx, lib, B, reps)
-        out[world] = {"A_ms": round(ra[0], 4), "A_GBps": round(ra[1] / ra[0] / 1e6, 1), "A_nnz": A.nnz,
-                      "B_ms": round(rb[0], 4), "B_GBps": round(rb[1] / rb[0] / 1e6, 1)}
-        print(world, out[world], flush=True)
+        for mode in modes:
+            if mode is not None:
+                ctx.set_option("band_dual", float(mode))
+                A.set_bands(64 * wl["N"])
+            ra = time_spmv(ctx, lib, A, reps)
+            key = world if mode is None else f"{world}/dual{mode}"
+            out[key] = {"A_ms": round(ra[0], 4), "A_GBps": round(ra[1] / ra[0] / 1e6, 1), "A_nnz": A.nnz,
+                        "B_ms": round(rb[0], 4), "B_GBps": round(rb[1] / rb[0] / 1e6, 1)}
+            print(key, out[key], flush=True)
         A.close()
         B.close()
     print(json.dumps(out))

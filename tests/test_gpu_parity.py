@@ -270,7 +270,7 @@ def test_dual_strip_bands(gpu_ctx, dtype):
     # a pixel shard (whole tile columns of the stored order, bench.py build_shard): A_g = B_g'
     # keeps the grid's strip geometry, with row strips of the column strips' pixel count
     col = 4 * N
-    B_s = A.T.row_slice(3 * col, 35 * col)
+    B_s = A.T.row_slice(3 * col, 35 * col)      # half the grid: the dual strips apply (h = 2 W / N rows)
     A_s = B_s.T
     Ss = A_s.to_scipy()
     xl = x[: Ss.shape[1]]
