@@ -10,7 +10,9 @@ tol = 0 (all 20 iterations run).  One "step" = one complete 20-iteration solve.
 Inputs (A, B, b, x_true) are resident in HBM before the timed region.
 `--workload c2|c3|c3gcv|c5|c5m` runs the other BASELINE configs as side lines.
 
-Multi-GPU (torchrun, one process per GPU): by default ONE global solve of the same
+Multi-GPU (one process per GPU): under torch.distributed.run WORLD_SIZE must equal --gpus;
+`python bench.py --gpus N` without a launcher spawns the N ranks itself (torch.distributed.run
+as a child process, before any GPU call).  By default ONE global solve of the same
 operator, pixel-sharded by nnz across the ranks: rank g holds
 A(:,P_g) and B(P_g,:), and the only data-path collective is an RCCL all-reduce of
 the m-vector partial A_g*(B_g*q) per Arnoldi step (strong scaling; value = GMRES
@@ -20,8 +22,9 @@ independent solve per GPU (weak scaling, no collective).
 Extra fields: "roofline" for the dominant SpMV kernel (algorithmic bytes per
 launch / average launch duration from HIP events recorded on the library's
 stream during the timed region), "kernels" (both SpMV classes and MGS),
-"cpu_baseline" (the oracle restatement timed on the host cores, rank 0, N=1: all cores
-through oracle/spmv_omp.c, plus a one-core scipy leg; nproc and CPU model stated).
+"cpu_baseline" (the oracle restatement timed on the host cores, rank 0, N=1: the process's
+OMP_NUM_THREADS share of the cores through oracle/spmv_omp.c -- 16 on the 1-GPU box -- plus a
+one-core scipy leg; thread count, its reason, nproc and CPU model stated).
 """
 import argparse
 import json
@@ -57,7 +60,11 @@ UNITS = {"lsqr_solver": "LSQR iters/s", "lsmr_solver": "LSMR iters/s"}
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node, one rank each: under torch.distributed.run WORLD_SIZE must equal it; "
+                         "without a launcher N > 1 spawns the N ranks itself")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print the planned world and every rank's pixel shard (JSON) without touching a GPU")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
@@ -123,6 +130,7 @@ def build_shard(ctx, wl, rank, world):
     import hgmres
     from hgmres.core import stored_pixel_index
     from hgmres.problems import shepp_logan
+    from hgmres.dist import tile_column_shards
     N, na = wl["N"], wl["angles"]
     Af = hgmres.SparseOperator.siddon(N, na, ctx=ctx)
     Nn, tile, sup = Af.pixel_order("cols")
@@ -133,9 +141,7 @@ def build_shard(ctx, wl, rank, world):
     e = e / np.linalg.norm(e) * 1e-2 * np.linalg.norm(b_exact)
     Bf = Af.T
     n = Af.shape[1]
-    col = max(tile, 1) * N                                 # one tile column of stored pixels
-    bounds = [0] + [int(round(g * (n // col) / world)) * col for g in range(1, world)] + [n]
-    lo, hi = bounds[rank], bounds[rank + 1]
+    lo, hi = tile_column_shards(N, world, tile)[rank]     # whole tile columns of stored pixels
     B_g = Bf.row_slice(lo, hi)
     A_g = B_g.T
     if Nn and sup == 0 and A_g.shape[1] * 8 > 4 * 1024 * 1024:
@@ -148,15 +154,68 @@ def build_shard(ctx, wl, rank, world):
     return A_g, B_g, b_exact + e, xs, (lo, hi), full
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`--gpus N` without a launcher: start N rank processes (torch.distributed.run, one per
+    GPU, rendezvous on 127.0.0.1) as CHILDREN of this process, which has not touched the GPU,
+    and return their exit code.  Rank 0 prints the JSON line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def plan(args, world):
+    """What a rank will run: the workload, the world and every rank's pixel shard (stored
+    positions, whole tile columns).  Host only."""
+    from hgmres.core import auto_pixel_order
+    from hgmres.dist import tile_column_shards
+    wl = WORKLOADS[args.workload]
+    N = wl["N"]
+    shard = (world > 1 and not args.replicas) or args.shard1
+    tile = auto_pixel_order(N)[0]
+    return {"workload": args.workload, "solver": wl["solver"], "N": N, "angles": wl["angles"], "world": world,
+            "mode": "pixel-sharded" if shard else ("replicas" if world > 1 else "single GPU"),
+            "shards": tile_column_shards(N, world, tile) if shard else [(0, N * N)] * world}
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # one process per GPU: spawn the ranks before anything initialises the GPU (never exec)
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    if args.dry_run:
+        # the launch plumbing without a GPU: every rank reports the shard it would hold
+        p = plan(args, world)
+        got = [None] * world
+        if world > 1:
+            dist.all_gather_object(got, {"rank": rank, "local_rank": local, "shard": p["shards"][rank]})
+            dist.destroy_process_group()
+        else:
+            got = [{"rank": 0, "local_rank": local, "shard": p["shards"][0]}]
+        if rank == 0:
+            print(json.dumps({"dry_run": True, **p, "ranks": got}))
+        return
     if args.same_device:
         local = 0                      # shard emulation: every rank on GPU 0
     torch.cuda.set_device(local)
@@ -377,7 +436,7 @@ def _host_cores():
 
 def cpu_baseline(A, B, b, x_true, wl, iters, iters_single):
     """The oracle restatement (the reference algorithm) on the same operator, timed on the
-    host: all cores (oracle/spmv_omp.c row-block SpMV, BLAS unrestricted; the products are
+    host: the process's OMP_NUM_THREADS cores (oracle/spmv_omp.c row-block SpMV, BLAS unrestricted; the products are
     bitwise those of the one-core scipy leg) and, if iters_single > 0, one core (scipy CSR
     SpMV, BLAS limited to one thread).  A timed solve includes the reference's setup
     (r0, norms), so iters/s understates the CPU's steady rate by that share (stated)."""
@@ -411,6 +470,9 @@ def cpu_baseline(A, B, b, x_true, wl, iters, iters_single):
     k_all, dt_all = run(PA, PB, iters)
     res = {"value": round(k_all / dt_all, 4), "unit": unit, "cores": threads, "kind": "port",
            "nproc": _host_cores(), "cpu_model": _cpu_model(),
+           "cores_reason": f"OpenMP threads = OMP_NUM_THREADS ({os.environ.get('OMP_NUM_THREADS', 'unset')}): the "
+                           "host-core share of this process (the 1-GPU box grants 16 cores; nproc counts the whole "
+                           "machine's CPUs, which other boxes' jobs use)",
            "sample": f"oracle/restatement.py {wl['solver']} on the same {wl['N']}^2 operator, one complete "
                      f"{k_all}-iteration solve incl. its setup ({dt_all:.1f} s), CSR SpMV on {threads} OpenMP "
                      f"threads (oracle/spmv_omp.c, bitwise = scipy), numpy BLAS unrestricted"}

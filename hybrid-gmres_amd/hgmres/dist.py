@@ -46,6 +46,24 @@ def plan_pixel_shards(A, world: int, B=None):
     return [(bounds[g], bounds[g + 1]) for g in range(world)]
 
 
+def tile_column_shards(N: int, world: int, tile: int):
+    """Pixel shards of a device-generated N x N operator in its tiled STORED order: `world`
+    contiguous ranges [(lo, hi), ...] of stored positions made of whole tile columns (tile * N
+    stored pixels each), as equal as the tile-column count allows.  Parallel-beam nnz per
+    pixel is uniform, so equal pixel counts balance nnz (0.02 % at 8 shards, checked at 512^2);
+    every shard keeps the tiled gather locality and the 64-column bands of the single-GPU
+    kernels (bench.py build_shard)."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    n = N * N
+    col = max(tile, 1) * N
+    ncol = n // col
+    if world > ncol:
+        raise ValueError(f"{world} shards of {ncol} tile columns")
+    bounds = [0] + [int(round(g * ncol / world)) * col for g in range(1, world)] + [n]
+    return [(bounds[g], bounds[g + 1]) for g in range(world)]
+
+
 def shard_operators(A, B, lo: int, hi: int):
     """(A_g, B_g) for the pixel range [lo, hi): A(:,lo:hi) as CSR with local
     columns, B(lo:hi,:) as CSR."""

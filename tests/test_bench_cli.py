@@ -1,0 +1,65 @@
+"""bench.py launch plumbing on the CPU (VERDICT r2 Missing #2): `--gpus N` without a launcher
+spawns N rank processes (torch.distributed.run, 127.0.0.1), a launcher's WORLD_SIZE must equal
+--gpus, and every rank holds the pixel shard DESIGN.md §5 plans (whole tile columns of the tiled
+stored order).  --dry-run stops before anything touches a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, env_extra=None, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, env=env, timeout=timeout,
+                       cwd=ROOT)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p
+
+
+def test_single_rank_plan():
+    rc, d, _ = _run(["--dry-run"])
+    assert rc == 0 and d["world"] == 1 and d["mode"] == "single GPU"
+    assert d["shards"] == [[0, 4096 * 4096]]
+
+
+@pytest.mark.parametrize("n,workload", [(2, "c4"), (3, "c3")])
+def test_gpus_n_spawns_n_ranks(n, workload):
+    rc, d, p = _run(["--gpus", str(n), "--dry-run", "--workload", workload])
+    assert rc == 0, p.stderr[-2000:]
+    N = 4096 if workload == "c4" else 2048
+    assert d["world"] == n and d["mode"] == "pixel-sharded"
+    assert [r["rank"] for r in d["ranks"]] == list(range(n))
+    assert [r["local_rank"] for r in d["ranks"]] == list(range(n))     # one GPU per rank
+    sh = [tuple(r["shard"]) for r in d["ranks"]]
+    assert sh[0][0] == 0 and sh[-1][1] == N * N
+    assert all(a[1] == b[0] for a, b in zip(sh, sh[1:]))
+    assert all((hi - lo) % (4 * N) == 0 for lo, hi in sh)               # whole 4 x N tile columns
+    sizes = [hi - lo for lo, hi in sh]
+    assert max(sizes) - min(sizes) <= 4 * N
+
+
+def test_replicas_plan():
+    rc, d, _ = _run(["--gpus", "2", "--dry-run", "--replicas"])
+    assert rc == 0 and d["mode"] == "replicas" and d["world"] == 2
+
+
+def test_world_size_must_match_gpus():
+    rc, d, p = _run(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "4", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc == 2 and d is None
+    assert "WORLD_SIZE=4" in p.stderr
+
+
+def test_tile_column_shards_host():
+    from hgmres.dist import tile_column_shards
+    for N, w in ((4096, 8), (2048, 8), (512, 4), (64, 3)):
+        sh = tile_column_shards(N, w, 4)
+        assert len(sh) == w and sh[0][0] == 0 and sh[-1][1] == N * N
+        assert all((hi - lo) % (4 * N) == 0 for lo, hi in sh)
+    with pytest.raises(ValueError):
+        tile_column_shards(8, 3, 4)
