@@ -41,6 +41,9 @@ enum { PROJ_LS = 0, PROJ_PTR = 1 };
 
 inline int64_t round64(int64_t x) { return (x + 63) / 64 * 64; }
 
+// ritz_steps = 0 runs the full Arnoldi (p = dim, the eigenpairs of M) up to this dimension
+constexpr int64_t kRitzFullDim = 512;
+
 struct DeltaM {
     const hgm_mat* L;
     const hgm_mat* R;   // nullptr: DeltaM = L
@@ -115,13 +118,17 @@ int gmres_bounds_filter(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const h
     const bool broke = Hh(k, k - 1) == 0.0;
     const int kf = broke ? k - 1 : k;
 
-    const int64_t ldq = krylov_ld(c, dim, false);
-    const double* Q = c->buf<double>("Q", (size_t)ldq * (maxit + 1));   // the solve's basis, Q(:,0:k)
+    // the solve's basis Q(:,0:k), read with gmres_family's own leading dimension: an n-space basis
+    // on a communicator (a one-rank RCCL context included) is laid out for the sharded path
+    const int64_t ldq = krylov_ld(c, dim, nspace && (c->world > 1 || c->nccl != nullptr));
+    const double* Q = c->buf<double>("Q", (size_t)ldq * (maxit + 1));
     // ---- dK = Qk' * DeltaM * Qk for every k at once (the leading blocks of the final one) ----
     const std::vector<double> dK = kf > 0 ? projected_delta(c, dm, Q, ldq, dim, kf) : std::vector<double>();
 
     // ---- leading eigenpairs of M: p-step Arnoldi with CGS2 (replaces eig(M), :4-9) ----
-    int p = ritz_steps > 0 ? ritz_steps : std::max(2 * kf + 10, 20);
+    // default: p = dim (eig(M) itself, to rounding) wherever that is cheap -- the reference's own
+    // problems (n = 32 shaw/heat/deriv2, 32^2 phantoms) -- else max(2k+10, 20) Ritz steps
+    int p = ritz_steps > 0 ? ritz_steps : (dim <= kRitzFullDim ? (int)dim : std::max(2 * kf + 10, 20));
     p = (int)std::min<int64_t>(std::max(p, kf), dim);
     std::vector<double> mu(std::max(kf, 1)), dmu(std::max(kf, 1)), rres(std::max(kf, 1));
     if (kf > 0) {

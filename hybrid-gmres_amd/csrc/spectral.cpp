@@ -88,6 +88,10 @@ inline cplx cdiv(double xr, double xi, double yr, double yi) { return cplx(xr, x
 // converge.  Column layout of V on return (LAPACK dgeev): a real eigenvalue j has its vector in
 // column j; a complex pair (j, j+1), wi[j] > 0, has the vector of wr[j] + i wi[j] as
 // V(:,j) + i V(:,j+1) and the conjugate one for j+1.
+// Attribution: this routine follows the structure and variable names (exshift, norm, low/high,
+// p, q, r, s, z, t, w, x, y) of the public-domain JAMA `EigenvalueDecomposition.hqr2` (NIST /
+// MathWorks, 1998), itself a translation of the EISPACK routine hqr2 (Wilkinson & Reinsch,
+// Handbook for Automatic Computation, Vol. II, 1971).
 bool schur_vectors(int nn, std::vector<double>& Hv, std::vector<double>& Vv, double* d, double* e) {
     double* H = Hv.data();
     double* V = Vv.data();

@@ -222,7 +222,9 @@ __device__ __forceinline__ V16 load_page16(const T* __restrict__ x, int64_t pid,
     return v;
 }
 
-template <typename T, int G, int EPI, bool NT, typename IX = int32_t, bool PG = false>
+// CLS: the operator class (KC_SPMV_A ray-major / KC_SPMV_B pixel-major) only names the
+// instantiation, so kernel traces (rocprofv3 --stats) report A and B separately.
+template <typename T, int G, int EPI, bool NT, typename IX = int32_t, bool PG = false, int CLS = 0>
 __global__ __launch_bounds__(BS) void k_spmv_stream(int64_t nnz, int64_t nseg, const int64_t* __restrict__ sp,
                                                     const int32_t* __restrict__ fo, const IX* __restrict__ ci,
                                                     const T* __restrict__ val, const T* __restrict__ x,
@@ -550,7 +552,7 @@ __global__ __launch_bounds__(BS) void k_epi(int64_t n, T* __restrict__ y, T a, c
 // launchers (every SpMV launch goes through hgm::launch so armed timing events ride
 // in the dispatch packets of the first / last kernel of the product)
 // ------------------------------------------------------------------------------
-template <typename T, int G, int EPI, bool NT, typename IX>
+template <typename T, int G, int EPI, bool NT, typename IX, int CLS>
 static void launch_stream_e(hgm_ctx* c, bool last, const SegIndex& si, const IX* ci, const T* val, const T* x,
                             T* out, T a, const T* z, T* head, T* tail, const PendNorm<T>& pn, const Paged<T>& pg) {
     if (si.nnz == 0) {
@@ -561,13 +563,13 @@ static void launch_stream_e(hgm_ctx* c, bool last, const SegIndex& si, const IX*
     }
     if constexpr (std::is_same<IX, int32_t>::value) {
         if (pg.pptr)
-            launch(c, false, k_spmv_stream<T, G, EPI, NT, IX, true>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg,
+            launch(c, false, k_spmv_stream<T, G, EPI, NT, IX, true, CLS>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg,
                    si.sp, si.fo, ci, val, x, out, a, z, head, tail, pn, pg);
         else
-            launch(c, false, k_spmv_stream<T, G, EPI, NT, IX, false>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg,
+            launch(c, false, k_spmv_stream<T, G, EPI, NT, IX, false, CLS>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg,
                    si.sp, si.fo, ci, val, x, out, a, z, head, tail, pn, pg);
     } else {
-        launch(c, false, k_spmv_stream<T, G, EPI, NT, IX, false>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg, si.sp,
+        launch(c, false, k_spmv_stream<T, G, EPI, NT, IX, false, CLS>, dim3(si.nchunks), dim3(BS), si.nnz, si.nseg, si.sp,
                si.fo, ci, val, x, out, a, z, head, tail, pn, pg);
     }
     int64_t g = (si.nchunks + BS - 1) / BS;
@@ -576,28 +578,33 @@ static void launch_stream_e(hgm_ctx* c, bool last, const SegIndex& si, const IX*
            (const T*)head, (const T*)tail, pn);
 }
 
-template <typename T, int G, bool NT, typename IX>
+template <typename T, int G, bool NT, typename IX, int CLS>
 static void launch_stream_g(hgm_ctx* c, bool last, const SegIndex& si, const IX* ci, const T* val, const T* x,
                             T* out, int epi, T a, const T* z, T* head, T* tail, const PendNorm<T>& pn,
                             const Paged<T>& pg) {
     switch (epi) {
-        case EPI_NONE: launch_stream_e<T, G, EPI_NONE, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
-        case EPI_ADD: launch_stream_e<T, G, EPI_ADD, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
-        case EPI_SUB: launch_stream_e<T, G, EPI_SUB, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
-        case EPI_ADDQ: launch_stream_e<T, G, EPI_ADDQ, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
-        default: launch_stream_e<T, G, EPI_RSUB, NT, IX>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
+        case EPI_NONE: launch_stream_e<T, G, EPI_NONE, NT, IX, CLS>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
+        case EPI_ADD: launch_stream_e<T, G, EPI_ADD, NT, IX, CLS>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
+        case EPI_SUB: launch_stream_e<T, G, EPI_SUB, NT, IX, CLS>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
+        case EPI_ADDQ: launch_stream_e<T, G, EPI_ADDQ, NT, IX, CLS>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
+        default: launch_stream_e<T, G, EPI_RSUB, NT, IX, CLS>(c, last, si, ci, val, x, out, a, z, head, tail, pn, pg); break;
     }
 }
 
 template <typename T, typename IX = int32_t>
 static void spmv_stream(hgm_ctx* c, bool last, const SegIndex& si, int G, bool nt, const IX* ci, const T* val,
                         const T* x, T* out, int epi, T a, const T* z, const PendNorm<T>& pn = PendNorm<T>{},
-                        const Paged<T>& pg = Paged<T>{}) {
+                        const Paged<T>& pg = Paged<T>{}, int kclass = KC_SPMV_A) {
     T* head = c->buf<T>("stream_head", si.nchunks + 1);
     T* tail = c->buf<T>("stream_tail", si.nchunks + 1);
-#define HGM_SG(GG)                                                                                      \
-    if (nt) launch_stream_g<T, GG, true, IX>(c, last, si, ci, val, x, out, epi, a, z, head, tail, pn, pg);  \
-    else launch_stream_g<T, GG, false, IX>(c, last, si, ci, val, x, out, epi, a, z, head, tail, pn, pg);
+#define HGM_SG(GG)                                                                                          \
+    if (kclass == KC_SPMV_B) {                                                                              \
+        if (nt) launch_stream_g<T, GG, true, IX, KC_SPMV_B>(c, last, si, ci, val, x, out, epi, a, z, head, tail, pn, pg); \
+        else launch_stream_g<T, GG, false, IX, KC_SPMV_B>(c, last, si, ci, val, x, out, epi, a, z, head, tail, pn, pg); \
+    } else {                                                                                                \
+        if (nt) launch_stream_g<T, GG, true, IX, KC_SPMV_A>(c, last, si, ci, val, x, out, epi, a, z, head, tail, pn, pg); \
+        else launch_stream_g<T, GG, false, IX, KC_SPMV_A>(c, last, si, ci, val, x, out, epi, a, z, head, tail, pn, pg); \
+    }
     switch (G) {
         case 64: HGM_SG(64) break;
         case 32: HGM_SG(32) break;
@@ -723,7 +730,8 @@ static void spmv_banded(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi,
 
 template <typename T>
 static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T* z,
-                          const PendNorm<T>& pn) {
+                          const PendNorm<T>& pn, int kclass) {
+    const int kc = kclass == KC_SPMV_B ? KC_SPMV_B : KC_SPMV_A;
     const bool nt = M->variant & SPMV_NT;
     // paged x gathers need the page index and a 16-B aligned x (vector page loads)
     Paged<T> pg;
@@ -738,7 +746,7 @@ static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int ep
         T* yp = c->buf<T>("band_part", (size_t)M->nbands * M->rows + 1);
         SegIndex si{M->nnz, (int64_t)M->nbands * M->rows, stream_chunks(M->nnz), M->brp, M->bcfo};
         spmv_stream<T>(c, false, si, M->bsgroup, nt, M->bci, reinterpret_cast<const T*>(M->bval), x, yp, EPI_NONE,
-                       T(0), nullptr, PendNorm<T>{}, pg);
+                       T(0), nullptr, PendNorm<T>{}, pg, kc);
         band_reduce<T>(c, M, yp, y, epi, a, z, pn);
     } else {
         SegIndex si{M->nnz, M->rows, stream_chunks(M->nnz), M->rp, M->cfo};
@@ -746,10 +754,10 @@ static void spmv_streamed(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int ep
         // 16-bit page-local indices instead, and only chunks past the page limit read M->ci
         if (M->ci16 && !(pg.pptr && c->num.paged16))
             spmv_stream<T, uint16_t>(c, true, si, M->sgroup, nt, M->ci16, reinterpret_cast<const T*>(M->val), x, y,
-                                     epi, a, z, pn, pg);
+                                     epi, a, z, pn, pg, kc);
         else
             spmv_stream<T>(c, true, si, M->sgroup, nt, M->ci, reinterpret_cast<const T*>(M->val), x, y, epi, a, z, pn,
-                           pg);
+                           pg, kc);
     }
 }
 
@@ -773,7 +781,7 @@ void spmv(hgm_ctx* c, const hgm_mat* M, const T* x, T* y, int epi, T a, const T*
     if (c->num.parity) {
         spmv_seq<T>(c, M, x, y, epi, a, z);
     } else if (stream) {
-        spmv_streamed<T>(c, M, x, y, epi, a, z, pn);
+        spmv_streamed<T>(c, M, x, y, epi, a, z, pn, kclass);
     } else if (M->nbands > 1) {
         spmv_banded<T>(c, M, x, y, epi, a, z, pn);
     } else {

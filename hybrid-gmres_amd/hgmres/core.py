@@ -475,7 +475,7 @@ def _bounds(A, B, b, x_true, tol, maxit, lam, side, hybrid, ctx, orth, return_H,
     dphi = np.zeros(maxit * maxit)
     mu = np.zeros(maxit)
     rres = np.zeros(maxit)
-    H = np.zeros((maxit + 1) * maxit) if return_H else None
+    H = np.zeros((maxit + 1) * maxit)          # also tells a breakdown at iteration k (below)
     o = _opts(orth, H, explicit_residual=explicit_residual)
     _check(L.load().hgm_gmres_bounds_filter(ctx.handle, C.byref(o), Ao._h, Bo._h, _dp(b), _dp(xt), float(tol),
                                             maxit, float(lam), side, hybrid, DL._h, DR._h if DR else None,
@@ -486,12 +486,13 @@ def _bounds(A, B, b, x_true, tol, maxit, lam, side, hybrid, ctx, orth, return_H,
     D_ = dphi.reshape(maxit, maxit)
     phi_iter = [P_[j, : j + 1].copy() for j in range(k)]
     dphi_iter = [D_[j, : j + 1].copy() for j in range(k)]
-    if k and np.isnan(phi_iter[-1]).all():         # breakdown at iteration k: phi_iter{k} = []
+    Hm = H.reshape(maxit, maxit + 1).T
+    if k and Hm[k, k - 1] == 0.0:   # breakdown at iteration k (*_bounds.m:31 before :80): phi_iter{k} = []
         phi_iter[-1] = np.zeros(0)
         dphi_iter[-1] = np.zeros(0)
     out = (x, err[:k].copy(), res[:k].copy(), k, phi_iter[-1], dphi_iter[-1], phi_iter, dphi_iter)
     if return_H:
-        out = out + (H.reshape(maxit, maxit + 1).T.copy(),)
+        out = out + (Hm.copy(),)
     if return_ritz:
         out = out + (mu[:k].copy(), rres[:k].copy())
     return out

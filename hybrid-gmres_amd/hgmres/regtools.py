@@ -17,12 +17,18 @@ below are the ones that package documents):
   ``s < t`` and ``t (s-1)`` otherwise on [0,1]^2, Galerkin with box functions (closed-form
   cell integrals), ``x(t) = t``, ``b(s) = (s^3 - s)/6`` projected on the same boxes.
 
-``heat`` (used only by the plot script ``plot_error_vs_mismatch_norm.m``) is not restated.
+* ``heat(n, kappa=1)``: inverse heat equation, a first-kind Volterra equation on [0,1] with the
+  convolution kernel ``k(t) = t^(-3/2) / (2 kappa sqrt(pi)) exp(-1/(4 kappa^2 t))``, collocated at
+  the midpoints ``t_i = (i - 1/2) h`` (``h = 1/n``) with the midpoint rule: ``A`` is the lower
+  triangular Toeplitz matrix with first column ``h k(t_i)``.  The solution is the package's
+  piecewise profile on the first half (``t_i = 20 i / n``: ``0.75 t^2/4`` below 2,
+  ``0.75 + (t-2)(3-t)`` below 3, ``0.75 exp(-2 (t-3))`` after) and zero on the second half,
+  ``b = A x`` (n even).  Used by ``plot_error_vs_mismatch_norm.m``.
 
 Parity: the arrays are MATLAB's up to rounding in the kernel evaluation order; no MATLAB
-output exists to pin them bitwise ("parity unpinned w.r.t. MATLAB's shaw/deriv2").  The tests
+output exists to pin them bitwise ("parity unpinned w.r.t. MATLAB's shaw/deriv2/heat").  The tests
 check them against their definitions (direct kernel evaluation, quadrature of the cell
-integrals).  This is host-side input generation, not part of the timed path.
+integrals, the heat equation's convolution structure).  This is host-side input generation, not part of the timed path.
 """
 from __future__ import annotations
 
@@ -71,6 +77,31 @@ def deriv2(n: int):
     return A, b, x
 
 
+def heat(n: int, kappa: float = 1.0):
+    """``[A, b, x] = heat(n, kappa)`` (Regularization Tools; kappa = 1 as generate_test_problem.m:6
+    calls it), dense ``n x n`` lower-triangular Toeplitz."""
+    if n % 2:
+        raise ValueError("The order n must be even")   # x(n/2+1:n) needs an integer n/2
+    h = 1.0 / n
+    t = (np.arange(n) + 0.5) * h
+    c = h / (2.0 * kappa * math.sqrt(math.pi))
+    d = 1.0 / (4.0 * kappa * kappa)
+    k = c * t ** (-1.5) * np.exp(-d / t)
+    idx = np.arange(n)
+    A = np.where(idx[:, None] >= idx[None, :], k[np.abs(idx[:, None] - idx[None, :])], 0.0)
+    x = np.zeros(n)
+    for i in range(1, n // 2 + 1):
+        ti = i * 20.0 / n
+        if ti < 2:
+            x[i - 1] = 0.75 * ti * ti / 4
+        elif ti < 3:
+            x[i - 1] = 0.75 + (ti - 2) * (3 - ti)
+        else:
+            x[i - 1] = 0.75 * math.exp(-(ti - 3) * 2)
+    b = A @ x
+    return A, b, x
+
+
 def generate_test_problem(name: str, n: int):
     """``[A, b_exact, x_true] = generate_test_problem(name, n)`` (generate_test_problem.m:1-11)."""
     key = name.lower()
@@ -79,5 +110,5 @@ def generate_test_problem(name: str, n: int):
     if key == "deriv2":
         return deriv2(n)
     if key == "heat":
-        raise NotImplementedError("heat (Regularization Tools) is not restated: only a plot script uses it")
+        return heat(n)
     raise ValueError("Unknown problem name. Use shaw, heat, or deriv2.")

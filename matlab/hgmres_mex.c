@@ -33,6 +33,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <math.h>
 #include <string.h>
 
 #include "hgmres.h"
@@ -339,23 +340,40 @@ static void bounds(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         const int ritz = nrhs > 12 ? (int)scalar(prhs[12], "ritz_steps") : 0;
         double* phi = (double*)mxCalloc((size_t)maxit * maxit, sizeof(double));
         double* dphi = (double*)mxCalloc((size_t)maxit * maxit, sizeof(double));
-        check(hgm_gmres_bounds_filter(ctx(), NULL, A, B, b, xt, tol, maxit, lambda, side, hybrid, DL, DR, ritz,
-                                      mxGetDoubles(x), mxGetDoubles(e), mxGetDoubles(r), &k, phi, dphi, NULL, NULL));
-        /* phi_iter{j} = column j (j entries); a breakdown at iteration k leaves phi_iter{k} = [] */
+        double* Hk = (double*)mxCalloc((size_t)(maxit + 1) * maxit, sizeof(double));
+        double* mu = (double*)mxCalloc((size_t)maxit, sizeof(double));
+        double* rres = (double*)mxCalloc((size_t)maxit, sizeof(double));
+        hgm_opts o = {0, HGM_MGS, Hk};
+        check(hgm_gmres_bounds_filter(ctx(), &o, A, B, b, xt, tol, maxit, lambda, side, hybrid, DL, DR, ritz,
+                                      mxGetDoubles(x), mxGetDoubles(e), mxGetDoubles(r), &k, phi, dphi, mu, rres));
+        /* a breakdown at iteration k (H(k+1,k) == 0, *_bounds.m:31 breaks before :80) leaves
+           phi_iter{k} unassigned in the reference: that cell alone is [] here; every other cell
+           holds its j values, NaN included (e.g. b = 0 gives NaN vectors, as MATLAB does) */
+        const int broke = k >= 1 && Hk[(size_t)(k - 1) * (maxit + 1) + k] == 0.0;
+        const int kf = broke ? k - 1 : k;
+        /* eig(M) of *_bounds.m:4-9 is replaced by Ritz pairs: exact for ritz_steps = dim (the default
+           for dim <= 512), otherwise approximations whose residuals are reported here */
+        double rmax = 0, mu1 = kf > 0 ? fabs(mu[0]) : 0;
+        for (int j = 0; j < kf; ++j) rmax = rres[j] > rmax ? rres[j] : rmax;
+        if (kf > 0 && !(rmax <= 1e-8 * mu1))
+            mexWarnMsgIdAndTxt("hgmres:ritz", "hgmres: the %d leading Ritz values stand in for eig(M) with a "
+                               "relative residual of %.2e; pass ritz_steps = size(M,1) for eig(M) itself", kf,
+                               mu1 > 0 ? rmax / mu1 : rmax);
         mxArray* pc = mxCreateCellMatrix((mwSize)k, 1);
         mxArray* dc = mxCreateCellMatrix((mwSize)k, 1);
         for (int j = 1; j <= k; ++j) {
-            const double* pj = phi + (size_t)(j - 1) * maxit;
-            const int len = (pj[0] != pj[0]) ? 0 : j;     /* NaN marks the unassigned cell */
-            mxSetCell(pc, (mwIndex)(j - 1), column(pj, len));
+            const int len = (broke && j == k) ? 0 : j;
+            mxSetCell(pc, (mwIndex)(j - 1), column(phi + (size_t)(j - 1) * maxit, len));
             mxSetCell(dc, (mwIndex)(j - 1), column(dphi + (size_t)(j - 1) * maxit, len));
         }
-        const double* pk = phi + (size_t)(k - 1) * maxit;
-        const int lk = (pk[0] != pk[0]) ? 0 : k;
-        plhs[4] = column(pk, lk);                                          /* phi_final  = phi_iter{k} */
+        const int lk = broke ? 0 : k;
+        plhs[4] = column(phi + (size_t)(k - 1) * maxit, lk);               /* phi_final  = phi_iter{k} */
         if (nlhs > 5) plhs[5] = column(dphi + (size_t)(k - 1) * maxit, lk); /* dphi_final */
         if (nlhs > 6) plhs[6] = pc;
         if (nlhs > 7) plhs[7] = dc;
+        mxFree(Hk);
+        mxFree(mu);
+        mxFree(rres);
         mxFree(phi);
         mxFree(dphi);
     }

@@ -41,6 +41,7 @@ void* mxCalloc(size_t n, size_t size);
 void mxFree(void* p);
 void mxDestroyArray(mxArray* a);
 void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...) __attribute__((noreturn));
+void mexWarnMsgIdAndTxt(const char* id, const char* fmt, ...);
 int mexAtExit(void (*fn)(void));
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]);

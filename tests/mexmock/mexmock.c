@@ -95,6 +95,25 @@ void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...) {
     va_end(ap);
     longjmp(g_jmp, 1);
 }
+/* warnings: the last one is kept (mock_last_warning) */
+static char g_wid[128], g_wmsg[1024];
+static int g_nwarn;
+void mexWarnMsgIdAndTxt(const char* id, const char* fmt, ...) {
+    snprintf(g_wid, sizeof g_wid, "%s", id);
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_wmsg, sizeof g_wmsg, fmt, ap);
+    va_end(ap);
+    ++g_nwarn;
+}
+int mock_last_warning(char* id, char* msg, int len) {
+    snprintf(id, len, "%s", g_wid);
+    snprintf(msg, len, "%s", g_wmsg);
+    const int n = g_nwarn;
+    g_nwarn = 0;
+    g_wid[0] = g_wmsg[0] = 0;
+    return n;
+}
 int mexAtExit(void (*fn)(void)) {
     g_exit = fn;
     return 0;

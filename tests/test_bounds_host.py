@@ -10,7 +10,7 @@ from scipy import integrate
 
 import hgmres
 from hgmres.problems import tomo_problem
-from hgmres.regtools import deriv2, generate_test_problem, shaw
+from hgmres.regtools import deriv2, generate_test_problem, heat, shaw
 from oracle import restatement as R
 
 
@@ -146,3 +146,26 @@ def test_deriv2_matches_cell_integrals():
     assert np.array_equal(A, A.T)
     with pytest.raises(ValueError):
         generate_test_problem("nope", 8)
+
+
+def test_heat_matches_its_definition():
+    """heat(n): midpoint collocation of the Volterra kernel k(s - t) = (s-t)^(-3/2)/(2 sqrt(pi))
+    exp(-1/(4 (s-t))) (kappa = 1), lower-triangular Toeplitz; the piecewise solution profile."""
+    for n in (8, 32, 64):
+        A, b, x = heat(n)
+        h = 1.0 / n
+        t = (np.arange(n) + 0.5) * h
+        for i, j in ((0, 0), (n - 1, 0), (n // 2, 3), (n - 1, n - 2)):
+            tau = t[i - j]                                # Toeplitz: k at the lag's midpoint
+            assert abs(A[i, j] - h * tau ** -1.5 / (2 * np.sqrt(np.pi)) * np.exp(-1 / (4 * tau))) <= 1e-15 * A[i, j] + 1e-300
+        assert np.all(np.triu(A, 1) == 0)
+        assert all(np.array_equal(np.diag(A, -d), np.full(n - d, A[d, 0])) for d in range(n))
+        ti = np.arange(1, n // 2 + 1) * 20.0 / n
+        xr = np.where(ti < 2, 0.75 * ti ** 2 / 4, np.where(ti < 3, 0.75 + (ti - 2) * (3 - ti), 0.75 * np.exp(-(ti - 3) * 2)))
+        assert np.allclose(x[: n // 2], xr, rtol=1e-15, atol=0) and np.all(x[n // 2:] == 0)
+        assert np.array_equal(b, A @ x)
+    # generate_test_problem.m:6 dispatches to heat(n)
+    A, b, x = generate_test_problem("heat", 32)
+    assert np.array_equal(A, heat(32)[0])
+    with pytest.raises(ValueError):
+        heat(7)

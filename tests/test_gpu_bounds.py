@@ -87,6 +87,56 @@ def test_bounds_filter_full_ritz_matches_dense_eig(gpu_ctx, tomo_mismatch, side,
     assert dev < 1e-12 and ddev < 1e-9, (dev, ddev)
 
 
+@pytest.mark.parametrize("side,hybrid", [("ab", 1), ("ba", 0)])
+def test_bounds_filter_default_is_dense_eig(gpu_ctx, tomo_mismatch, side, hybrid):
+    """ritz_steps left at its default (0): p = dim for dim <= 512, so the default path
+    -- the one the .m wrappers and the gateway take -- reproduces eig(M) of *_bounds.m:4-9."""
+    P, E = tomo_mismatch
+    maxit, lam = 8, 1e-2
+    dm = (P.A.tocsr() @ E).toarray() if side == "ab" else (E @ P.A.tocsr()).toarray()
+    dim = dm.shape[0]
+    assert dim <= 512
+    fn = getattr(hgmres, FN[(side, hybrid)])
+    args = (P.A, P.B, P.b, P.x_true, 0.0, maxit) + ((lam,) if hybrid else ())
+    out = fn(*args, dm, ctx=gpu_ctx, return_ritz=True)
+    full = fn(*args, dm, ctx=gpu_ctx, ritz_steps=dim, return_ritz=True)
+    k, mu = out[3], out[8]
+    mu_full, _ = R._spectrum(P.A, P.B, side)
+    assert np.max(np.abs(mu - mu_full[:k])) <= 1e-12 * abs(mu_full[0])
+    for j in range(k):                                  # the default IS the p = dim run
+        np.testing.assert_array_equal(out[6][j], full[6][j])
+        np.testing.assert_array_equal(out[7][j], full[7][j])
+    ref = _oracle(P, side, hybrid, maxit, lam, dm)
+    for j in range(k):
+        pr, dr = np.real(ref[6][j]), np.real(ref[7][j])
+        assert np.max(np.abs(out[6][j] - pr)) <= 1e-8 * np.max(np.abs(pr))
+        assert np.max(np.abs(out[7][j] - dr)) <= 1e-8 * np.max(np.abs(dr))
+
+
+def test_bounds_filter_one_rank_rccl(tomo_mismatch):
+    """A one-rank RCCL context sends the n-space solve down the sharded path, whose Krylov basis has
+    the sharded layout; the filter factors must read that basis with the same leading dimension
+    (dim = 576 <= 24576, where the single-context and sharded strides differ)."""
+    from hgmres.dist import init_context
+    P, E = tomo_mismatch
+    maxit, lam = 8, 1e-2
+    dm = (E @ P.A.tocsr()).toarray()
+    args = (P.A, P.B, P.b, P.x_true, 0.0, maxit, lam)
+    c1 = init_context(0, 0, 1, one_rank_comm=True)
+    c0 = hgmres.Context(0)
+    try:
+        o1 = hgmres.BAgmres_hybrid_bounds(*args, dm, ctx=c1)
+        o0 = hgmres.BAgmres_hybrid_bounds(*args, dm, ctx=c0)
+    finally:
+        c1.close()
+        c0.close()
+    assert o1[3] == o0[3]
+    assert np.linalg.norm(o1[0] - o0[0]) <= 1e-10 * np.linalg.norm(o0[0])
+    for j in range(o0[3]):
+        assert np.max(np.abs(o1[6][j] - o0[6][j])) <= 1e-10 * np.max(np.abs(o0[6][j])), j
+        assert np.max(np.abs(o1[7][j] - o0[7][j])) <= 1e-8 * np.max(np.abs(o0[7][j])), j
+
+
 def test_bounds_filter_truncated_ritz(gpu_ctx):
     """At scale the Ritz Arnoldi is short (p << dim): the leading Ritz values converge, and their
     reported residuals ||M u - mu u|| bound the eigenvalue error of these well-separated ones."""
