@@ -42,7 +42,7 @@ enum { PROJ_LS = 0, PROJ_PTR = 1 };
 inline int64_t round64(int64_t x) { return (x + 63) / 64 * 64; }
 
 // ritz_steps = 0 runs the full Arnoldi (p = dim, the eigenpairs of M) up to this dimension
-constexpr int64_t kRitzFullDim = 512;
+constexpr int64_t kRitzFullDim = 1024;
 
 struct DeltaM {
     const hgm_mat* L;

@@ -384,9 +384,19 @@ __global__ __launch_bounds__(BS) void k_fro2(int64_t nnz, const T* __restrict__ 
 }
 
 template <typename T>
+__global__ __launch_bounds__(BS) void k_to_f64(int64_t n, const T* __restrict__ in, double* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = (double)in[i];
+}
+
+template <typename T>
 void fro2(hgm_ctx* c, const hgm_mat* M, double* out) {
-    if (c->num.parity && std::is_same<T, double>::value) {   // norm(A,'fro')^2 over the stored values
+    if (c->num.parity) {   // norm(A,'fro')^2 over the stored values, in double, fixed order
         const double* v = reinterpret_cast<const double*>(M->val);
+        if (!std::is_same<T, double>::value) {                 // fp32 values, widened exactly
+            double* w = c->buf<double>("fro_f64", M->nnz + 1);
+            k_to_f64<T><<<grid_for(M->nnz), BS, 0, c->stream>>>(M->nnz, reinterpret_cast<const T*>(M->val), w);
+            v = w;
+        }
         fixed_reduce_op<double, 1>(c, M->nnz, v, v, 0, nullptr, nullptr, out);
         return;
     }

@@ -92,7 +92,9 @@ enum hgm_ctx_option {
      * order of oracle/restatement.py's fixed_order() (64-element sequential chunks, twice,
      * then sequential), MGS runs one dot + axpy pass per column exactly as
      * hybrid_ba_gmres_rtp.m:20-26, x = Q*y sums sequentially over the columns, and the
-     * monitors are formed explicitly (b - A*x).  Single rank, reference pixel order, fp64.
+     * monitors are formed explicitly (b - A*x).  Single rank, reference pixel order.  fp64, and
+     * fp32 operators for the Golub-Kahan solvers (lsqr_solver / lsmr_solver: float32 vectors and
+     * sums in the same order, scalars in double; oracle/restatement.py lsqr_solver_f32).
      * For parity checks only: a fraction of the production kernels' throughput. */
     HGM_OPT_PARITY = 1,
     HGM_OPT_MGS_FORM = 2,          /* MGS for long vectors: 1 one-reduction form [1], 0 one launch per pass */

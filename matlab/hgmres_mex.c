@@ -352,7 +352,7 @@ static void bounds(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         const int broke = k >= 1 && Hk[(size_t)(k - 1) * (maxit + 1) + k] == 0.0;
         const int kf = broke ? k - 1 : k;
         /* eig(M) of *_bounds.m:4-9 is replaced by Ritz pairs: exact for ritz_steps = dim (the default
-           for dim <= 512), otherwise approximations whose residuals are reported here */
+           for dim <= 1024), otherwise approximations whose residuals are reported here */
         double rmax = 0, mu1 = kf > 0 ? fabs(mu[0]) : 0;
         for (int j = 0; j < kf; ++j) rmax = rres[j] > rmax ? rres[j] : rmax;
         if (kf > 0 && !(rmax <= 1e-8 * mu1))

@@ -44,6 +44,9 @@ def load():
         lib.oracle_csr_matvec.argtypes = [C.c_int64, P(C.c_int64), P(C.c_int32), P(C.c_double), P(C.c_double),
                                           P(C.c_double)]
         lib.oracle_csr_matvec.restype = None
+        lib.oracle_csr_matvec_f32.argtypes = [C.c_int64, P(C.c_int64), P(C.c_int32), P(C.c_float), P(C.c_float),
+                                              P(C.c_float)]
+        lib.oracle_csr_matvec_f32.restype = None
         lib.oracle_num_threads.restype = C.c_int
         _lib = lib
     return _lib
@@ -57,15 +60,17 @@ class ParallelCSR:
     """CSR operator for the oracle whose products run on all host cores.  ``T`` may be
     given (an explicit transpose, e.g. the device's ``A'``); otherwise it is formed once
     with scipy (``M.T.tocsr()``, whose rows keep increasing column order: the order in
-    which scipy's ``csc_matvec`` accumulates ``M.T @ u``)."""
+    which scipy's ``csc_matvec`` accumulates ``M.T @ u``).  A float32 M keeps float32 values
+    and computes in single precision (scipy's ``csr_matvec<float>``), for the fp32 oracle."""
 
     def __init__(self, M, T=None):
         M = sp.csr_matrix(M)
         self.M = M
         self.shape = M.shape
+        self.dtype = np.float32 if M.dtype == np.float32 else np.float64
         self.rp = np.ascontiguousarray(M.indptr, dtype=np.int64)
         self.ci = np.ascontiguousarray(M.indices, dtype=np.int32)
-        self.val = np.ascontiguousarray(M.data, dtype=np.float64)
+        self.val = np.ascontiguousarray(M.data, dtype=self.dtype)
         self._T = T
         load()
 
@@ -77,6 +82,16 @@ class ParallelCSR:
         return self._T
 
     def _mv(self, v):
+        if self.dtype == np.float32:
+            if np.asarray(v).dtype != np.float32:
+                raise TypeError("fp32 operator: the vector must be float32")
+            v = np.ascontiguousarray(v, dtype=np.float32)
+            y = np.empty(self.shape[0], dtype=np.float32)
+            fp = C.POINTER(C.c_float)
+            load().oracle_csr_matvec_f32(self.shape[0], self.rp.ctypes.data_as(C.POINTER(C.c_int64)),
+                                         self.ci.ctypes.data_as(C.POINTER(C.c_int32)), self.val.ctypes.data_as(fp),
+                                         v.ctypes.data_as(fp), y.ctypes.data_as(fp))
+            return y
         v = np.ascontiguousarray(v, dtype=np.float64)
         y = np.empty(self.shape[0])
         dp = C.POINTER(C.c_double)
@@ -92,4 +107,4 @@ class ParallelCSR:
         return np.stack([self._mv(v[:, j]) for j in range(v.shape[1])], axis=1)
 
     def fro_norm(self):
-        return float(np.linalg.norm(self.val))
+        return float(np.linalg.norm(self.val.astype(np.float64)))

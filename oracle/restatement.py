@@ -852,3 +852,180 @@ def gcv_function(lam, A, B, b, m, k_gcv, gcv_type):
     H, beta = arnoldi(A, B, b, k_gcv, gcv_type)
     trace_m = m if gcv_type == "ab" else A.shape[1]   # :46-50
     return gcv_from_H(H, beta, lam, trace_m)
+
+
+# ---------------------------------------------------------------------------------------------
+# fp32 Golub-Kahan (BASELINE configs[4]: lsqr_solver / lsmr_solver with a single-precision
+# operator and single-precision Krylov vectors).  The reference is fp64 MATLAB; this is its
+# algorithm line by line (cited) in the arithmetic libhgmres' fp32 path uses, in the documented
+# fixed order:
+#   * operator and vectors in float32 (b, x_true rounded to float32 once);
+#   * products summed sequentially per row in float32 (scipy csr_matvec<float>, or
+#     oracle/parallel.py's float32 OpenMP product: the same bits);
+#   * sums of squares / differences in float32 in the fixed order of _fsum32;
+#   * the scalars (beta, alpha, the rotations) in double from those float32 sums, and every
+#     scalar that scales a vector rounded to float32 first;
+#   * ||A||_F (lsmr_solver.m:71) in double over the float32 values, fixed order.
+# libhgmres in parity mode (HGM_OPT_PARITY) on an HGM_F32 operator runs exactly this, so the
+# two agree bit for bit (tests/test_gpu_parity_mode.py).
+# ---------------------------------------------------------------------------------------------
+f32 = np.float32
+
+
+def _fsum32(p):
+    """_fsum's order (64-term chunks, then 64-value chunks of those, then left to right) with
+    every partial sum rounded to float32 (np.cumsum accumulates in the array's dtype)."""
+    p = np.ascontiguousarray(p, dtype=np.float32).ravel()
+    if p.size == 0:
+        return f32(0.0)
+    for _ in range(2):
+        r = (-p.size) % _FIX_CH
+        if r:
+            p = np.concatenate([p, np.zeros(r, dtype=np.float32)])
+        p = np.cumsum(p.reshape(-1, _FIX_CH), axis=1, dtype=np.float32)[:, -1]
+    return f32(np.cumsum(p, dtype=np.float32)[-1])
+
+
+def _nrm32(v):
+    """norm(v) of a float32 vector: sqrt in double of the float32 fixed-order sum of squares."""
+    v = np.asarray(v, dtype=np.float32)
+    return np.float64(np.sqrt(np.float64(_fsum32(v * v))))
+
+
+def _nrm32_diff(a, b):
+    d = np.asarray(a, dtype=np.float32) - np.asarray(b, dtype=np.float32)
+    return np.float64(np.sqrt(np.float64(_fsum32(d * d))))
+
+
+def _op32(A):
+    """(A*v, A'*u) of a float32 operator: scipy CSR float32 (or a ParallelCSR of one)."""
+    if hasattr(A, "dtype") and not sp.issparse(A):
+        return A, A.T
+    A = sp.csr_matrix(A, dtype=np.float32)
+    return A, A.T
+
+
+def _mv32(M, v):
+    y = M @ np.asarray(v, dtype=np.float32)
+    assert y.dtype == np.float32
+    return y
+
+
+def lsqr_solver_f32(A, b, x_true, tol, maxit):
+    """``lsqr_solver.m:1-54`` with a float32 operator and float32 vectors (see the section note)."""
+    A, At = _op32(A)
+    n = A.shape[1]
+    b32, xt32 = np.asarray(b, dtype=np.float32), np.asarray(x_true, dtype=np.float32)
+    x = np.zeros(n, dtype=np.float32)            # :5
+    nb = _nrm32(b32)
+    nxt = _nrm32_diff(xt32, x)
+    beta = nb                                    # :7
+    u = b32 / f32(beta)                          # :8
+    v_hat = _mv32(At, u)                         # :10
+    alpha = _nrm32(v_hat)                        # :11
+    v = v_hat / f32(alpha)                       # :12
+    w = v.copy()                                 # :14
+    phi_bar, rho_bar = beta, alpha               # :15-16
+    error_norm = np.zeros(maxit)
+    residual_norm = np.zeros(maxit)
+    k = 0
+    for k in range(maxit):                       # :20
+        u_hat = _mv32(A, v) - f32(alpha) * u     # :22
+        beta = _nrm32(u_hat)                     # :23
+        u = u_hat / f32(beta)                    # :24
+        v_hat = _mv32(At, u) - f32(beta) * v     # :26
+        alpha = _nrm32(v_hat)                    # :27
+        v = v_hat / f32(alpha)                   # :28
+        rho = np.sqrt(rho_bar * rho_bar + beta * beta)   # :31
+        c = rho_bar / rho                        # :32
+        s = beta / rho                           # :33
+        theta = s * alpha                        # :35
+        rho_bar = -c * alpha                     # :36
+        phi = c * phi_bar                        # :37
+        phi_bar = s * phi_bar                    # :38
+        x = x + f32(phi / rho) * w               # :40
+        w = v - f32(theta / rho) * w             # :41
+        error_norm[k] = _nrm32_diff(x, xt32) / nxt   # :43
+        residual_norm[k] = abs(phi_bar) / nb     # :44
+        if residual_norm[k] <= tol:              # :46
+            break
+    niters = k + 1                               # :49
+    error_norm = error_norm[:niters]
+    residual_norm = residual_norm[:niters].copy()
+    r = b32 - _mv32(A, x)
+    residual_norm[-1] = _nrm32(r) / nb           # :52
+    return x, error_norm, residual_norm, niters
+
+
+def lsmr_solver_f32(A, b, x_true=None, tol=None, maxit=None):
+    """``lsmr_solver.m:1-83`` with a float32 operator and float32 vectors (section note)."""
+    A, At = _op32(A)
+    if tol is None:
+        tol = 1e-6                               # :3
+    m, n = A.shape                               # :4
+    if maxit is None:
+        maxit = min(m, n)                        # :5
+    b32 = np.asarray(b, dtype=np.float32)
+    have_xt = x_true is not None and np.size(x_true) > 0
+    xt32 = np.asarray(x_true, dtype=np.float32) if have_xt else None
+    x = np.zeros(n, dtype=np.float32)            # :7
+    nb = _nrm32(b32)
+    nxt = _nrm32_diff(xt32, x) if have_xt else 0.0
+    vals = A.val if hasattr(A, "val") else sp.csr_matrix(A).data
+    normA = np.sqrt(_fsum(np.asarray(vals, dtype=np.float32).astype(np.float64) ** 2))   # :71 norm(A,'fro')
+    u = b32.copy()                               # :10
+    beta = nb                                    # :11
+    if beta > 0:
+        u = u / f32(beta)                        # :12
+    v = _mv32(At, u)                             # :14
+    alpha = _nrm32(v)                            # :15
+    if alpha > 0:
+        v = v / f32(alpha)                       # :16
+    zetabar = alpha * beta                       # :19
+    alphabar = alpha                             # :20
+    rho, rhobar, cbar, sbar = 1.0, 1.0, 1.0, 0.0 # :21-23
+    h = v.copy()                                 # :25
+    hbar = np.zeros(n, dtype=np.float32)         # :26
+    err_hist = np.full(maxit, np.nan)            # :28
+    res_hist = np.zeros(maxit)                   # :29
+    ar_hist = np.zeros(maxit)                    # :30
+    k = 0
+    for k in range(maxit):                       # :32
+        u = _mv32(A, v) - f32(alpha) * u         # :34
+        beta = _nrm32(u)                         # :35
+        if beta > 0:
+            u = u / f32(beta)                    # :36
+        v = _mv32(At, u) - f32(beta) * v         # :38
+        alpha = _nrm32(v)                        # :39
+        if alpha > 0:
+            v = v / f32(alpha)                   # :40
+        alphahat = alphabar                      # :42
+        rhoold = rho                             # :43
+        rho = np.hypot(alphahat, beta)           # :44
+        c = alphahat / rho                       # :45
+        s = beta / rho                           # :46
+        thetanew = s * alpha                     # :48
+        alphabar = c * alpha                     # :49
+        rhobarold = rhobar                       # :51
+        thetabar = sbar * rho                    # :52
+        rhobar = np.hypot(cbar * rho, thetanew)  # :53
+        cbar = (cbar * rho) / rhobar             # :54
+        sbar = thetanew / rhobar                 # :55
+        zeta = cbar * zetabar                    # :58
+        zetabar = -sbar * zetabar                # :59
+        if k == 0:
+            hbar = h.copy()                      # :62
+        else:
+            hbar = h - f32((thetabar * rho) / (rhoold * rhobarold)) * hbar   # :64
+        x = x + f32(zeta / (rho * rhobar)) * hbar   # :66
+        h = v - f32(thetanew / rho) * h          # :67
+        r = b32 - _mv32(A, x)                    # :69
+        nr = _nrm32(r)
+        res_hist[k] = nr / (nb + EPS)            # :70
+        ar_hist[k] = _nrm32(_mv32(At, r)) / (normA * max(nr, EPS))   # :71
+        if have_xt:
+            err_hist[k] = _nrm32_diff(x, xt32) / nxt                   # :72-73
+        if res_hist[k] < tol:                    # :76
+            break
+    iters = k + 1                                # :79
+    return x, err_hist[:iters], res_hist[:iters], ar_hist[:iters], iters

@@ -23,4 +23,16 @@ void oracle_csr_matvec(int64_t rows, const int64_t* rp, const int32_t* ci, const
     }
 }
 
+/* fp32 (BASELINE configs[4]): the same sequential row sums in single precision, as scipy's
+   csr_matvec<float> computes `A32 @ v32` (and libhgmres' parity-mode k_spmv_seq<float>). */
+void oracle_csr_matvec_f32(int64_t rows, const int64_t* rp, const int32_t* ci, const float* val, const float* x,
+                           float* y) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < rows; ++i) {
+        float s = 0.0f;
+        for (int64_t j = rp[i]; j < rp[i + 1]; ++j) s += val[j] * x[ci[j]];
+        y[i] = s;
+    }
+}
+
 int oracle_num_threads(void) { return omp_get_max_threads(); }

@@ -8,7 +8,7 @@ O=gpurun_out/r3
 mkdir -p $O
 TESTS=${TESTS:-tests}
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -q -rA --timeout 300 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest $TESTS -m gpu ${PYX:--x} -q -rA --timeout 300 --timeout-method thread \
       > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
   tail -3 $O/gpu_tests.log
   timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1

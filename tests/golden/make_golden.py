@@ -23,9 +23,14 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 
 
 def csr_hash(M):
+    """sha256 over indptr (int64), indices (int32), data (float64), without copying the arrays
+    (the C4 operator is 12 GB)."""
     h = hashlib.sha256()
-    for a in (M.indptr.astype(np.int64), M.indices.astype(np.int32), M.data.astype(np.float64)):
-        h.update(np.ascontiguousarray(a).tobytes())
+    for a, dt in ((M.indptr, np.int64), (M.indices, np.int32), (M.data, np.float64)):
+        a = np.ascontiguousarray(a, dtype=dt).reshape(-1)
+        step = 1 << 24
+        for i in range(0, a.size, step):
+            h.update(memoryview(a[i:i + step]))
     return h.hexdigest()
 
 
@@ -63,26 +68,68 @@ def dump(name, P, maxit, lam, tol=0.0, store_raw=True):
     print("wrote", name, {k: (v.shape if hasattr(v, "shape") else v) for k, v in d.items() if "sha" in k or k == "shape"})
 
 
-def dump_c3(name="c3_2048.npz", k=5):
-    """BASELINE configs[2] at full size (2048^2, 19 angles, nnz 1.01e8): BA-GMRES + GCV Arnoldi
+def dump_c3(name="c3_2048.npz", k=20):
+    """BASELINE configs[2] at full size (2048^2, 19 angles, nnz 1.01e8) at the bench's iteration
+    counts (bench.py WORKLOADS["c3gcv"]): BA-GMRES (hybrid_ba_gmres_rtp, 20 iterations, lambda 1e-2)
     with MGS (the reference's orthogonalisation, hybrid_ba_gmres_rtp.m:20-23) and with CGS2 (the
-    config's alternative), k steps.  The operator is pinned by its CSR hash (the device generator
-    reproduces it bitwise); x is stored as its norm plus every 997th entry."""
+    config's alternative), and the 20-step GCV Arnoldi (gcv_function.m:18-33) with the lambda that
+    fminbnd picks on it over the bench's bounds [1e-8, 1] (TolX 1e-10, analyze_regularization.m:39-46).
+    The operator is pinned by its CSR hash (the device generator reproduces it bitwise); x is stored
+    as its norm plus every 997th entry.  SpMVs run on the host's OpenMP threads (oracle/parallel.py:
+    bitwise scipy's csr_matvec)."""
+    from oracle import parallel as OP
+    from hgmres.core import gcv_fminbnd
     P = tomo_problem(2048, 19, noise=1e-2, seed=0, backprojector="matched")
     A, B, b, xt = P.A, P.B.tocsr(), P.b, P.x_true
+    OP.build()
+    PA, PB = OP.ParallelCSR(A), OP.ParallelCSR(B)
+    gcv = dict(lo=1e-8, hi=1.0, tolx=1e-10)
     d = {"maxit": k, "lam": 1e-2, "N": 2048, "n_angles": 19, "A_sha256": csr_hash(A), "b": b,
-         "sample_stride": 997}
+         "sample_stride": 997, "gcv_k": k, "gcv_lo": gcv["lo"], "gcv_hi": gcv["hi"], "gcv_tolx": gcv["tolx"]}
     for orth in ("mgs", "cgs2"):
-        x, e, r, kk, H = R.hybrid_ba_gmres_rtp(A, B, b, xt, 0.0, k, 1e-2, return_H=True, orth=orth)
+        x, e, r, kk, H = R.hybrid_ba_gmres_rtp(PA, PB, b, xt, 0.0, k, 1e-2, return_H=True, orth=orth)
         d.update({f"hba_{orth}_H": H, f"hba_{orth}_err": e, f"hba_{orth}_res": r, f"hba_{orth}_k": kk,
                   f"hba_{orth}_xnorm": np.linalg.norm(x), f"hba_{orth}_xs": x[::997].copy()})
-        Hg, beta = R.arnoldi(A, B, b, k, "ba", orth=orth)
-        d.update({f"gcv_{orth}_H": Hg, f"gcv_{orth}_beta": beta})
+        Hg, beta = R.arnoldi(PA, PB, b, k, "ba", orth=orth)
+        lam, g = gcv_fminbnd(Hg, beta, A.shape[1], gcv["lo"], gcv["hi"], gcv["tolx"])
+        d.update({f"gcv_{orth}_H": Hg, f"gcv_{orth}_beta": beta, f"gcv_{orth}_lam": lam, f"gcv_{orth}_val": g})
+        # the solve at the GCV lambda: the c3gcv bench step (hybrid_ba_gmres_rtp at lambda_GCV)
+        x, e, r, kk, H = R.hybrid_ba_gmres_rtp(PA, PB, b, xt, 0.0, k, lam, return_H=True, orth=orth)
+        d.update({f"hbg_{orth}_H": H, f"hbg_{orth}_err": e, f"hbg_{orth}_res": r, f"hbg_{orth}_k": kk,
+                  f"hbg_{orth}_xnorm": np.linalg.norm(x), f"hbg_{orth}_xs": x[::997].copy()})
     np.savez_compressed(os.path.join(OUT, name), **d)
     print("wrote", name, "MGS vs CGS2 |dH|/|H| =",
-          np.max(np.abs(d["hba_mgs_H"] - d["hba_cgs2_H"])) / np.max(np.abs(d["hba_mgs_H"])))
+          np.max(np.abs(d["hba_mgs_H"] - d["hba_cgs2_H"])) / np.max(np.abs(d["hba_mgs_H"])),
+          "lambda_GCV", d["gcv_mgs_lam"], d["gcv_cgs2_lam"])
 
 
+def dump_c4(name="c4_4096.npz", k=20):
+    """BASELINE configs[3] at full size (4096^2, 47 angles, nnz 1.004e9): the bench's AB-GMRES
+    (ABgmres_nonhybrid_bounds.m, m-space Arnoldi on A*B, B = A') through all 20 iterations.
+    Inputs: b (stored: the device forms A*x_true in another summation order), the operator pinned
+    by the sha256 of its CSR (reference pixel order).  Outputs: H (21 x 20), the histories, x as its
+    norm plus every 997th entry.  SpMVs on the host's OpenMP threads (bitwise scipy).  Needs ~45 GB
+    of host memory and ~10 minutes on 8 cores."""
+    import gc
+    from oracle import parallel as OP
+    from hgmres.problems import siddon_projector, shepp_logan
+    A = siddon_projector(4096, 47)
+    h = csr_hash(A)
+    xt = shepp_logan(4096).ravel(order="F")
+    OP.build()
+    PA = OP.ParallelCSR(A)
+    del A
+    gc.collect()
+    b_exact = PA @ xt
+    e = np.random.default_rng(0).standard_normal(PA.shape[0])
+    b = b_exact + e / np.linalg.norm(e) * 1e-2 * np.linalg.norm(b_exact)
+    PB = PA.T                                     # scipy M.T.tocsr(): rows keep increasing column order
+    x, err, res, kk, H = R.ABgmres_nonhybrid_bounds(PA, PB, b, xt, 0.0, k, return_H=True)
+    d = {"maxit": k, "N": 4096, "n_angles": 47, "A_sha256": h, "b": b, "sample_stride": 997,
+         "abn_H": H, "abn_err": err, "abn_res": res, "abn_k": kk, "abn_xnorm": np.linalg.norm(x),
+         "abn_xs": x[::997].copy()}
+    np.savez_compressed(os.path.join(OUT, name), **d)
+    print("wrote", name, "k", kk, "res", res[-1], "err", err[-1])
 def dump_shaw_pipeline(name="shaw32_pipeline.npz"):
     """analyze_regularization.m on shaw(32) (restated, hgmres.regtools) with numpy noise and
     mismatch (MATLAB's randn stream cannot be reproduced): inputs, the oracle's outputs in the
@@ -115,6 +162,9 @@ def dump_shaw_pipeline(name="shaw32_pipeline.npz"):
 if __name__ == "__main__":
     if sys.argv[1:] == ["c3"]:
         dump_c3()
+        sys.exit(0)
+    if sys.argv[1:] == ["c4"]:
+        dump_c4()
         sys.exit(0)
     if sys.argv[1:] == ["shaw"]:
         dump_shaw_pipeline()

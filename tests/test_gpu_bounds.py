@@ -89,13 +89,13 @@ def test_bounds_filter_full_ritz_matches_dense_eig(gpu_ctx, tomo_mismatch, side,
 
 @pytest.mark.parametrize("side,hybrid", [("ab", 1), ("ba", 0)])
 def test_bounds_filter_default_is_dense_eig(gpu_ctx, tomo_mismatch, side, hybrid):
-    """ritz_steps left at its default (0): p = dim for dim <= 512, so the default path
+    """ritz_steps left at its default (0): p = dim for dim <= 1024, so the default path
     -- the one the .m wrappers and the gateway take -- reproduces eig(M) of *_bounds.m:4-9."""
     P, E = tomo_mismatch
     maxit, lam = 8, 1e-2
     dm = (P.A.tocsr() @ E).toarray() if side == "ab" else (E @ P.A.tocsr()).toarray()
     dim = dm.shape[0]
-    assert dim <= 512
+    assert dim <= 1024
     fn = getattr(hgmres, FN[(side, hybrid)])
     args = (P.A, P.B, P.b, P.x_true, 0.0, maxit) + ((lam,) if hybrid else ())
     out = fn(*args, dm, ctx=gpu_ctx, return_ritz=True)

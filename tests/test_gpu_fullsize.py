@@ -1,11 +1,12 @@
 """BASELINE configs[2]-[4] at full size on one MI355X ("configs untested").
 
-* C3 (2048^2, 19 angles, nnz 1.01e8): BA-GMRES + GCV Arnoldi, MGS and CGS2, against the
-  committed oracle fixture tests/golden/c3_2048.npz (operator pinned by CSR hash; the device
-  generator must reproduce it bitwise).  CGS2 is held both against the oracle's CGS2 and
-  against the oracle's MGS -- the reference only has MGS (hybrid_ba_gmres_rtp.m:20-23) --
-  with the north_star bar 1e-10; the oracle's own MGS-vs-CGS2 difference at this size is
-  8.5e-14 (make_golden.py prints it).
+* C3 (2048^2, 19 angles, nnz 1.01e8) at the bench's iteration counts: the 20-step GCV Arnoldi,
+  fminbnd on it with the bench's bounds, and 20-iteration BA-GMRES at lambda 1e-2 and at the GCV
+  lambda, MGS and CGS2, against the committed oracle fixture tests/golden/c3_2048.npz (operator
+  pinned by CSR hash; the device generator must reproduce it bitwise).  CGS2 is held both
+  against the oracle's CGS2 and against the oracle's MGS -- the reference only has MGS
+  (hybrid_ba_gmres_rtp.m:20-23) -- with the north_star bar 1e-10; the oracle's own MGS-vs-CGS2
+  difference at k = 20 is 9.0e-12 (make_golden.py prints it).
 * C4 (4096^2, 47 angles, nnz 1.0e9): ABgmres_nonhybrid_bounds (the configs[3] AB-GMRES)
   through 20 iterations, size-independent properties (Hessenberg structure, monitors
   consistent with the returned x), plus the first 2 iterations against the oracle run on the
@@ -13,6 +14,9 @@
 * C5 (configs[4], fp32 operator at 4096^2): LSQR / LSMR through 20 iterations, properties,
   and agreement with the fp64 solve at k = 4 (fp32 Golub-Kahan departs from fp64 after a few
   steps, as a numpy float32 emulation does too; tests/test_gpu_parity.py::test_lsqr_fp32).
+  Against the fp32 oracle (oracle/restatement.py lsqr_solver_f32 / lsmr_solver_f32, the
+  reference's loops in fp32, fixed order) on the downloaded operator: parity mode bit-identical
+  through 8 iterations, and the production kernels within the stated envelope.
 """
 import gc
 
@@ -46,46 +50,66 @@ def H_rel(H, Hr):
 
 
 def _csr_hash(M):
+    """sha256 of (indptr int64, indices int32, data float64), chunked: no copies of a 12 GB CSR."""
     import hashlib
     h = hashlib.sha256()
-    for a in (M.indptr.astype(np.int64), M.indices.astype(np.int32), M.data.astype(np.float64)):
-        h.update(np.ascontiguousarray(a).tobytes())
+    for a, dt in ((M.indptr, np.int64), (M.indices, np.int32), (M.data, np.float64)):
+        a = np.ascontiguousarray(a, dtype=dt).reshape(-1)
+        for i in range(0, a.size, 1 << 24):
+            h.update(memoryview(a[i:i + (1 << 24)]))
     return h.hexdigest()
 
 
 # ---------------------------------------------------------------------------------------
 # C3
 # ---------------------------------------------------------------------------------------
+def _solve_ok(tag, x, e, r, kk, H, g, st):
+    """One BA-GMRES solve against the fixture entries `tag`_* at the north_star bar."""
+    assert kk == int(g[f"{tag}_k"])
+    assert H_rel(H, g[f"{tag}_H"]) <= TOL, (tag, H_rel(H, g[f"{tag}_H"]))
+    hist_ok(e, g[f"{tag}_err"])
+    hist_ok(r, g[f"{tag}_res"])
+    assert abs(np.linalg.norm(x) - float(g[f"{tag}_xnorm"])) <= TOL * float(g[f"{tag}_xnorm"])
+    assert rel(x[::st], g[f"{tag}_xs"]) <= TOL
+    print(f"[c3 {tag}] k={kk} |dH|/|H|={H_rel(H, g[f'{tag}_H']):.2e} |dx_s|={rel(x[::st], g[f'{tag}_xs']):.2e}")
+
+
 def test_c3_ba_gmres_gcv_mgs_cgs2(gpu_ctx):
+    """configs[2] at the bench's counts (bench.py WORKLOADS["c3gcv"]): the 20-step GCV Arnoldi,
+    fminbnd over [1e-8, 1] (TolX 1e-10) on it, and the 20-iteration BA-GMRES solve at lambda = 1e-2
+    and at the GCV lambda, with MGS and CGS2, against the oracle fixture."""
     g = load_golden("c3_2048.npz")
     k, lam, st = int(g["maxit"]), float(g["lam"]), int(g["sample_stride"])
+    assert k == 20 and int(g["gcv_k"]) == 20
+    lo, hi, tolx = float(g["gcv_lo"]), float(g["gcv_hi"]), float(g["gcv_tolx"])
     A = hgmres.SparseOperator.siddon(2048, 19, ctx=gpu_ctx)           # tiled pixel order
     assert _csr_hash(A.to_scipy()) == str(g["A_sha256"])             # = the oracle's operator, bitwise
     B = A.T
     b = g["b"]
+    n = A.shape[1]
     xt = shepp_logan(2048).ravel(order="F")
     for orth in ("mgs", "cgs2"):
         x, e, r, kk, H = hgmres.hybrid_ba_gmres_rtp(A, B, b, xt, 0.0, k, lam, ctx=gpu_ctx, return_H=True, orth=orth)
-        assert kk == int(g[f"hba_{orth}_k"])
-        assert H_rel(H, g[f"hba_{orth}_H"]) <= TOL, (orth, H_rel(H, g[f"hba_{orth}_H"]))
-        hist_ok(e, g[f"hba_{orth}_err"])
-        hist_ok(r, g[f"hba_{orth}_res"])
-        assert abs(np.linalg.norm(x) - float(g[f"hba_{orth}_xnorm"])) <= TOL * float(g[f"hba_{orth}_xnorm"])
-        assert rel(x[::st], g[f"hba_{orth}_xs"]) <= TOL
-        # CGS2 against the reference's MGS (the bound stated in the module docstring)
+        _solve_ok(f"hba_{orth}", x, e, r, kk, H, g, st)
+        # CGS2 against the reference's MGS too (the bound stated in the module docstring)
         assert H_rel(H, g["hba_mgs_H"]) <= TOL, (orth, H_rel(H, g["hba_mgs_H"]))
         hist_ok(r, g["hba_mgs_res"])
         Hg, beta, kd = hgmres.arnoldi(A, B, b, k, "ba", ctx=gpu_ctx, orth=orth)
         assert kd == k and H_rel(Hg, g[f"gcv_{orth}_H"]) <= TOL and abs(beta - float(g[f"gcv_{orth}_beta"])) <= TOL * beta
-        # GCV lambda on the device Arnoldi vs on the oracle's (analyze_regularization.m:39-46)
-        lg, gv = hgmres.gcv_fminbnd(Hg, beta, A.shape[1], 1e-9, 1e-1, 1e-8)
-        lr, gr = hgmres.gcv_fminbnd(g[f"gcv_{orth}_H"], float(g[f"gcv_{orth}_beta"]), A.shape[1], 1e-9, 1e-1, 1e-8)
-        # same GCV minimum value, and the device lambda minimises the oracle's GCV function
-        # equally well (at k = 5 the GCV curve is flat near its minimum, so the minimiser's
-        # location is ill-determined: with CGS2 the two lambdas differ by 25 % at equal values)
+        # GCV lambda on the device Arnoldi vs the oracle's (analyze_regularization.m:39-46), the
+        # bench's bounds: the same minimum value, and the device lambda minimises the oracle's
+        # GCV function equally well (the curve is flat near its minimum: MGS and CGS2 pick
+        # 3.1e-4 and 2.4e-4 on the oracle's own Arnoldi at equal values)
+        lg, gv = hgmres.gcv_fminbnd(Hg, beta, n, lo, hi, tolx)
+        gr, lr = float(g[f"gcv_{orth}_val"]), float(g[f"gcv_{orth}_lam"])
         assert abs(gv - gr) <= 1e-9 * abs(gr), (gv, gr)
-        f_ref = R.gcv_from_H(g[f"gcv_{orth}_H"], float(g[f"gcv_{orth}_beta"]), lg, A.shape[1])
+        f_ref = R.gcv_from_H(g[f"gcv_{orth}_H"], float(g[f"gcv_{orth}_beta"]), lg, n)
         assert abs(f_ref - gr) <= 1e-9 * abs(gr), (f_ref, gr, lg, lr)
+        print(f"[c3 gcv {orth}] lambda dev {lg:.6e} oracle {lr:.6e}, gcv {gv:.6e} / {gr:.6e}")
+        # the c3gcv bench step's solve, at the oracle's GCV lambda (a lambda within fminbnd's TolX
+        # moves x by ~TolX * |dx/dlambda|: the solve is compared at the same lambda)
+        x, e, r, kk, H = hgmres.hybrid_ba_gmres_rtp(A, B, b, xt, 0.0, k, lr, ctx=gpu_ctx, return_H=True, orth=orth)
+        _solve_ok(f"hbg_{orth}", x, e, r, kk, H, g, st)
     A.close()
     B.close()
     gc.collect()
@@ -167,4 +191,56 @@ def test_c5_fp32_golub_kahan_full_size(gpu_ctx):
     hist_ok(e4, e64, 1e-3)
     A.close()
     B.close()
+    gc.collect()
+
+
+# production fp32 kernels vs the fp32 oracle at 4096^2: the Golub-Kahan recurrences amplify the
+# summation-order difference (fp32 rounding, 6e-8) chaotically; measured at k = 8 (printed)
+C5_ENVELOPE = {"lsqr": 1e-2, "lsmr": 1e-2}
+
+
+def test_c5_fp32_vs_fp32_oracle_full_size(gpu_ctx):
+    import scipy.sparse as sp
+    from oracle import parallel as OP
+    A64, _, b, xt = _c4_problem(gpu_ctx)
+    A64.close()
+    gc.collect()
+    K = 8
+    # parity mode runs in the reference pixel order; the production solve keeps the tiled order
+    Ar = hgmres.SparseOperator.siddon(4096, 47, ctx=gpu_ctx, dtype=L.HGM_F32, order="reference")
+    As = Ar.to_scipy()
+    A32 = sp.csr_matrix((As.data.astype(np.float32), As.indices, As.indptr), shape=As.shape)
+    del As
+    gc.collect()
+    OP.build()
+    PA = OP.ParallelCSR(A32)
+    del A32
+    Art = Ar.T
+    At_ = hgmres.SparseOperator.siddon(4096, 47, ctx=gpu_ctx, dtype=L.HGM_F32)
+    Att = At_.T
+    for name in ("lsqr", "lsmr"):
+        if name == "lsqr":
+            ref = R.lsqr_solver_f32(PA, b, xt, 0.0, K)
+            with gpu_ctx.options(parity=1):
+                par = hgmres.lsqr_solver(Ar, b, xt, 0.0, K, ctx=gpu_ctx, At=Art)
+            prod = hgmres.lsqr_solver(At_, b, xt, 0.0, K, ctx=gpu_ctx, At=Att)
+            nh = 2
+        else:
+            ref = R.lsmr_solver_f32(PA, b, xt, 0.0, K)
+            with gpu_ctx.options(parity=1):
+                par = hgmres.lsmr_solver(Ar, b, xt, 0.0, K, ctx=gpu_ctx, At=Art)
+            prod = hgmres.lsmr_solver(At_, b, xt, 0.0, K, ctx=gpu_ctx, At=Att)
+            nh = 3
+        x32 = ref[0].astype(np.float64)
+        assert par[-1] == ref[-1] == K
+        bit = np.array_equal(par[0], x32) and all(np.array_equal(par[1 + i], ref[1 + i]) for i in range(nh))
+        dx = rel(prod[0], x32)
+        dh = [float(np.max(np.abs(prod[1 + i] - ref[1 + i]) / np.abs(ref[1 + i]))) for i in range(nh)]
+        print(f"[c5 {name} k={K}] parity bit-identical={bit}; production vs fp32 oracle: x {dx:.2e}, "
+              f"histories {', '.join(f'{d:.2e}' for d in dh)}")
+        assert bit, (name, rel(par[0], x32))
+        assert dx <= C5_ENVELOPE[name] and max(dh) <= C5_ENVELOPE[name], (name, dx, dh)
+    del PA
+    for M in (Ar, Art, At_, Att):
+        M.close()
     gc.collect()

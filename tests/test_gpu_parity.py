@@ -799,6 +799,46 @@ def test_lsmr(gpu_ctx, P64):
     assert it2 == itr and np.all(np.isnan(eh2))
 
 
+# production Golub-Kahan kernels at the north_star bar over the early iterations (VERDICT r2 "Next"
+# #3): every history entry of the first GKB_EARLY iterations, and x after GKB_EARLY iterations,
+# within 1e-10 of the oracle -- before the recurrences (no reorthogonalisation, as the reference)
+# have amplified the summation-order difference past it.  The per-iteration deviations of the full
+# 20-iteration run are printed (pytest -rA) so the iteration where 1e-10 is lost is on record.
+GKB_EARLY = 6
+
+
+@pytest.mark.parametrize("solver", ["lsqr", "lsmr", "hybrid_lsqr", "hybrid_lsmr"])
+@pytest.mark.parametrize("name", ["tomo64", "tomo24_matched.npz", "tomo24_pixel.npz"])
+def test_gkb_production_early_iterations(gpu_ctx, P64, solver, name):
+    if name == "tomo64":
+        A, b, xt = P64.A, P64.b, P64.x_true
+    else:
+        A, _, b, xt, g = golden_problem(name)
+    lam = 1e-2
+    fns = {"lsqr": (lambda k: R.lsqr_solver(A, b, xt, 0.0, k), lambda k: hgmres.lsqr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx)),
+           "lsmr": (lambda k: R.lsmr_solver(A, b, xt, 0.0, k), lambda k: hgmres.lsmr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx)),
+           "hybrid_lsqr": (lambda k: R.hybrid_lsqr_solver(A, b, xt, 0.0, k, lam),
+                           lambda k: hgmres.hybrid_lsqr_solver(A, b, xt, 0.0, k, lam, ctx=gpu_ctx)),
+           "hybrid_lsmr": (lambda k: R.hybrid_lsmr_solver(A, b, xt, 0.0, k, lam),
+                           lambda k: hgmres.hybrid_lsmr_solver(A, b, xt, 0.0, k, lam, ctx=gpu_ctx))}[solver]
+    nh = 3 if solver == "lsmr" else 2
+    ref_fn, gpu_fn = fns
+    full, fref = gpu_fn(20), ref_fn(20)
+    per_it = np.max([np.abs(np.asarray(full[1 + i]) - np.asarray(fref[1 + i])) / np.abs(np.asarray(fref[1 + i]))
+                     for i in range(nh)], axis=0)
+    print(f"[gkb early {solver} {name}] per-iteration max history deviation: "
+          + " ".join(f"{d:.0e}" for d in per_it))
+    K = GKB_EARLY
+    out, ref = gpu_fn(K), ref_fn(K)
+    assert out[-1] == ref[-1] == K
+    # lsqr_solver.m:52 overwrites the last residual with the exact one: that entry of the K-run
+    # is a different quantity from the 20-run's, compared on its own
+    for i in range(nh):
+        hist_ok(out[1 + i], ref[1 + i], TOL)
+    assert rel(out[0], ref[0]) <= TOL, (solver, name, rel(out[0], ref[0]))
+    assert np.all(per_it[:K - 1] <= TOL), per_it[:K]
+
+
 @pytest.mark.parametrize("dtype", [0, 1])
 def test_lsmr_monitor_forms_agree(gpu_ctx, P64, dtype):
     """lsmr_solver.m:69-71 monitors: kept-product images (default) vs the explicit SpMVs of

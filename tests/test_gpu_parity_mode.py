@@ -15,7 +15,9 @@ the parity claim is made in ONE documented order that both sides follow (DESIGN.
 
 Bar: BIT-IDENTICAL x, Hessenberg matrix and every history entry, k = 20, tomo24 (matched and
 unmatched B) and tomo64 (measured: profiles/r2_parity_mode.json) -- stricter than
-north_star's 1e-10.  The measured deviations are printed and, with HGM_PARITY_REPORT=<file>,
+north_star's 1e-10 -- and at BASELINE configs[1]'s full size (C2: 512^2, nnz 1.0e7) for every
+solver.  fp32 (configs[4]): LSQR / LSMR on float32 operators against the fp32 fixed-order
+restatement (oracle/restatement.py lsqr_solver_f32 / lsmr_solver_f32), bit-identical too.  The measured deviations are printed and, with HGM_PARITY_REPORT=<file>,
 written as JSON.
 """
 import json
@@ -26,6 +28,7 @@ import pytest
 
 from conftest import golden_problem
 import hgmres
+from hgmres import _lib as L
 from hgmres.problems import tomo_problem
 from oracle import restatement as R
 
@@ -198,3 +201,72 @@ def test_parity_cgs2(pctx, name):
     assert np.array_equal(out[-1], ref[-1]) and np.array_equal(out[0], ref[0])
     assert np.array_equal(out[1], ref[1]) and np.array_equal(out[2], ref[2])
     assert np.array_equal(H, Hr) and beta == br
+
+
+# ------------------------------------------------------------------ fp32 (BASELINE configs[4])
+GKB32 = {
+    "lsqr": (lambda A, b, xt, k: R.lsqr_solver_f32(A, b, xt, 0.0, k),
+             lambda A, At, b, xt, k, c: hgmres.lsqr_solver(A, b, xt, 0.0, k, ctx=c, At=At), 2),
+    "lsmr": (lambda A, b, xt, k: R.lsmr_solver_f32(A, b, xt, 0.0, k),
+             lambda A, At, b, xt, k, c: hgmres.lsmr_solver(A, b, xt, 0.0, k, ctx=c, At=At), 3),
+}
+
+
+@pytest.mark.parametrize("name", sorted(PROBLEMS))
+@pytest.mark.parametrize("solver", sorted(GKB32))
+def test_parity_golub_kahan_fp32(pctx, name, solver):
+    """fp32 LSQR / LSMR (configs[4]'s path) on a float32 operator, 20 iterations: x and every
+    history entry bit-identical to the fp32 fixed-order restatement."""
+    A, B, b, xt = PROBLEMS[name]
+    A32 = A.astype(np.float32)
+    ref_fn, gpu_fn, nh = GKB32[solver]
+    ref = ref_fn(A32, b, xt, 20)
+    Ao = hgmres.SparseOperator.from_scipy(A32, pctx, dtype=L.HGM_F32)
+    out = gpu_fn(Ao, Ao.T, b, xt, 20, pctx)
+    assert out[-1] == ref[-1]
+    dx = _rel_dev(out[0], ref[0].astype(np.float64))
+    dh = [_rel_dev(out[1 + i], ref[1 + i]) for i in range(nh)]
+    bitwise = bool(np.array_equal(out[0], ref[0].astype(np.float64)) and
+                   all(np.array_equal(out[1 + i], ref[1 + i], equal_nan=True) for i in range(nh)))
+    _record(f"{solver}_fp32/{name}", x=dx, hist_max=max(dh), bitwise=bitwise, iters=int(out[-1]))
+    assert bitwise, (dx, dh)
+
+
+# ------------------------------------------------------------------ C2 full size (configs[1])
+@pytest.fixture(scope="module")
+def c2():
+    P = tomo_problem(512, 30, noise=1e-2, seed=0)
+    assert P.A.nnz > 9.9e6
+    return P.A, P.B.tocsr(), P.b, P.x_true
+
+
+@pytest.mark.parametrize("tag", sorted(GM))
+def test_parity_c2_full_size_gmres(pctx, c2, tag):
+    """The six Arnoldi solvers in parity mode at C2 (512^2, nnz 1.0e7), 20 iterations: H, x and
+    both histories bit-identical to the fixed-order oracle (parity mode is not toy-only)."""
+    A, B, b, xt = c2
+    ref_fn, gpu_fn = GM[tag]
+    with R.fixed_order():
+        ref = ref_fn(A, B, b, xt, 20)
+    out = gpu_fn(A, B, b, xt, 20, pctx)
+    assert out[3] == ref[3] == 20
+    H, Hr = out[-1], ref[-1]
+    _record(f"{tag}/c2_512", H_bitwise=bool(np.array_equal(H, Hr)), x=_rel_dev(out[0], ref[0]),
+            err_hist=_rel_dev(out[1], ref[1]), res_hist=_rel_dev(out[2], ref[2]))
+    assert np.array_equal(H, Hr) and np.array_equal(out[0], ref[0])
+    assert np.array_equal(out[1], ref[1]) and np.array_equal(out[2], ref[2])
+
+
+@pytest.mark.parametrize("solver", sorted(GKB))
+def test_parity_c2_full_size_golub_kahan(pctx, c2, solver):
+    """LSQR / LSMR / hybrids in parity mode at C2, 20 iterations: bit-identical."""
+    A, B, b, xt = c2
+    ref_fn, gpu_fn, nh = GKB[solver]
+    with R.fixed_order():
+        ref = ref_fn(A, b, xt, 20)
+    out = gpu_fn(A, b, xt, 20, pctx)
+    assert out[-1] == ref[-1]
+    bitwise = bool(np.array_equal(out[0], ref[0]) and
+                   all(np.array_equal(out[1 + i], ref[1 + i], equal_nan=True) for i in range(nh)))
+    _record(f"{solver}/c2_512", x=_rel_dev(out[0], ref[0]), bitwise=bitwise, iters=int(out[-1]))
+    assert bitwise

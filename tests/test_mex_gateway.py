@@ -280,7 +280,7 @@ def test_gateway_bounds_eight_outputs(mex, gpu_ctx, side, hybrid):
     for j in range(k):
         np.testing.assert_array_equal(outs[6][j], ref[6][j])
         np.testing.assert_array_equal(outs[7][j], ref[7][j])
-    # the gateway's default ritz_steps (0: p = dim for dim <= 512) is eig(M) itself: against the
+    # the gateway's default ritz_steps (0: p = dim for dim <= 1024) is eig(M) itself: against the
     # oracle's dense eig at the filter-factor bar, with no Ritz-residual warning
     n_w, _, _ = mex.last_warning()
     assert n_w == 0
