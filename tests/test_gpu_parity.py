@@ -804,7 +804,7 @@ def test_lsmr(gpu_ctx, P64):
 # within 1e-10 of the oracle -- before the recurrences (no reorthogonalisation, as the reference)
 # have amplified the summation-order difference past it.  The per-iteration deviations of the full
 # 20-iteration run are printed (pytest -rA) so the iteration where 1e-10 is lost is on record.
-GKB_EARLY = 6
+GKB_EARLY = 8     # measured: 1e-10 holds through iterations 9-11 on these problems (printed)
 
 
 @pytest.mark.parametrize("solver", ["lsqr", "lsmr", "hybrid_lsqr", "hybrid_lsmr"])
