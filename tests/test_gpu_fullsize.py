@@ -203,11 +203,12 @@ def test_c5_fp32_golub_kahan_full_size(gpu_ctx):
 
 # production fp32 kernels vs the fp32 oracle at 4096^2: the Golub-Kahan recurrences amplify the
 # summation-order difference (fp32 rounding, 6e-8) by ~10x per iteration (the fp64 runs of
-# test_gkb_production_early_iterations show the same growth from 1e-16); measured: x 2.0e-2 and
-# residual estimate 0.21 at k = 8 for LSQR.  Held: iteration j (1-based) within 1e-6 * 10^(j-1)
-# through j = 4, x within 5e-2 at k = 8; every deviation printed.
+# test_gkb_production_early_iterations show the same growth from 1e-16).  Measured for LSQR: the
+# histories at 1e-6 (fp32 sums of ~3700-entry rows) through iteration 4, 3e-5 at 5, 1e-2 at 6,
+# 0.2 at 7; x 2.0e-2 at k = 8.  Held: iterations 1-4 within 1e-5, iteration 5 within 1e-3, x within
+# 5e-2 at k = 8; every deviation printed.
 def _c5_envelope(j):
-    return 1e-6 * 10.0 ** (j - 1)
+    return 1e-5 if j <= 4 else 1e-3
 
 
 def test_c5_fp32_vs_fp32_oracle_full_size(gpu_ctx):
@@ -250,7 +251,7 @@ def test_c5_fp32_vs_fp32_oracle_full_size(gpu_ctx):
         print(f"[c5 {name} k={K}] parity bit-identical={bit}; production vs fp32 oracle: x {dx:.2e}, "
               f"per-iteration max history deviation {' '.join(f'{d:.0e}' for d in per_it)}")
         assert bit, (name, rel(par[0], x32))
-        for j in range(1, 5):
+        for j in range(1, 6):
             assert per_it[j - 1] <= _c5_envelope(j), (name, j, per_it[j - 1])
         assert dx <= 5e-2, (name, dx)
     del PA
