@@ -494,6 +494,11 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
         case HGM_OPT_LSQR_DEV: n.lsqr_dev = v != 0.0; break;
         case HGM_OPT_PAGED16: n.paged16 = v != 0.0; break;
         case HGM_OPT_BAND_DUAL: n.band_dual = v != 0.0; break;
+        case HGM_OPT_FUSED_AB: if (!b01) return bad("fused_ab is 0 or 1"); n.fused_ab = v != 0; break;
+        case HGM_OPT_FUSED_REGION:
+            if (!(v >= 8 && v <= 1024 && v == std::floor(v))) return bad("fused_region is an integer in [8, 1024]");
+            n.fused_region = (int)v;
+            break;
         default: return bad("unknown option");
     }
     return HGM_OK;
@@ -520,6 +525,8 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_LSQR_DEV: *v = n.lsqr_dev; break;
         case HGM_OPT_PAGED16: *v = n.paged16; break;
         case HGM_OPT_BAND_DUAL: *v = n.band_dual; break;
+        case HGM_OPT_FUSED_AB: *v = n.fused_ab; break;
+        case HGM_OPT_FUSED_REGION: *v = n.fused_region; break;
         default: return HGM_E_ARG;
     }
     return HGM_OK;

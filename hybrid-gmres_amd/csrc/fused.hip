@@ -1,0 +1,392 @@
+// One pass over B for the m-space Arnoldi operator w = A*(B*q) (ABgmres_*_bounds.m:25,
+// gcv_function.m:20) when B is A' value for value (a device transpose pair) -- DESIGN.md §3.5.
+//
+// The two-pass form streams the same values twice (B*q pixel-major, then A*z ray-major: 24.5 GB
+// of algorithmic traffic per step at C4).  Here B's pixel-major entries are read ONCE:
+//   z_j = sum_i B(j,i) q_i                  (row sums: the kept column B*q, written out)
+//   w_i = sum_j A(i,j) z_j = sum_j B(j,i) z_j
+// The second sum scatters from pixel rows into rays.  To keep it deterministic (no atomics) and
+// its partials few, the pixels are grouped into REGIONS (R x R pixel squares of the image): one
+// workgroup owns one region and accumulates the region's rays in LDS (a 64 x 64 square is
+// crossed by ~3,900 of the 272,271 C4 rays), so one partial per (region, ray) leaves the kernel;
+// a ray-major pass then sums each ray's partials in region order.
+//
+// Inside a region the entries are processed in SUB-CHUNKS of <= FCH entries (whole pixel rows of
+// one region).  Per sub-chunk the plan holds a local CSC: the distinct rays of the sub-chunk
+// (`lr_*`: global ray id, first position, region-ray index) and perm[e] = the sub-chunk position
+// of the k-th entry in ray order.  The kernel
+//   1. loads the values (registers) and scatters q_ray to every entry of the ray (LDS, via perm),
+//   2. forms the products and the row sums z_j (FG lanes per row, fixed tree), writes z,
+//   3. forms u_e = B(j,i) z_j (LDS) and sums each local ray's u_e in position order,
+//   4. adds that to the region accumulator (one owner thread per ray per sub-chunk, sub-chunks
+//      in a fixed order): every sum has a fixed order, so products are bitwise reproducible.
+// Per entry the pass reads the value (8 B) and perm (2 B); the local-ray records add ~1.4 B.
+#include <algorithm>
+#include <chrono>
+#include <numeric>
+#include <thread>
+
+#include "device_common.h"
+
+namespace hgm {
+
+namespace {
+constexpr int FCH = 4096;      // entries per sub-chunk
+constexpr int FRMAX = 4096;    // rays per region (LDS accumulators)
+constexpr int FROWS = 128;     // pixel rows per sub-chunk
+constexpr int FG = 4;          // lanes per row sum
+constexpr int FVPT = FCH / BS; // values per thread
+}  // namespace
+
+struct FusedSub {
+    int64_t e0;        // first entry (B's CSR order)
+    int64_t lr0;       // first local-ray record
+    int32_t r0;        // first row
+    uint16_t len;      // entries
+    uint16_t nrow;     // rows
+    uint16_t nlr;      // local rays
+    uint16_t pad0, pad1, pad2;
+};
+static_assert(sizeof(FusedSub) == 32, "FusedSub layout");
+
+struct FusedPlan {
+    int region = 0;
+    int64_t nreg = 0, nsub = 0, nlr = 0, nslot = 0, m = 0;
+    int32_t* reg_sub = nullptr;   // nreg+1
+    int64_t* reg_base = nullptr;  // nreg+1
+    FusedSub* subs = nullptr;     // nsub
+    uint16_t* perm = nullptr;     // nnz
+    int32_t* lr_ray = nullptr;    // nlr
+    uint32_t* lr_pk = nullptr;    // nlr: first position | region ray index << 16
+    int64_t* rs_ptr = nullptr;    // m+1
+    int32_t* rs_slot = nullptr;   // nslot
+    double* part = nullptr;       // nslot
+    double build_s = 0;
+};
+
+void fused_plan_free(FusedPlan* P) {
+    if (!P) return;
+    for (void* p : {(void*)P->reg_sub, (void*)P->reg_base, (void*)P->subs, (void*)P->perm, (void*)P->lr_ray,
+                    (void*)P->lr_pk, (void*)P->rs_ptr, (void*)P->rs_slot, (void*)P->part})
+        if (p) (void)hipFree(p);
+    delete P;
+}
+
+// ------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(BS) void k_fused_ab(const FusedSub* __restrict__ subs, const int32_t* __restrict__ reg_sub,
+                                                 const int64_t* __restrict__ reg_base,
+                                                 const uint16_t* __restrict__ perm, const int32_t* __restrict__ lr_ray,
+                                                 const uint32_t* __restrict__ lr_pk, const int64_t* __restrict__ rp,
+                                                 const double* __restrict__ val, const double* __restrict__ q,
+                                                 double* __restrict__ z, double* __restrict__ part) {
+    __shared__ double prod[FCH];
+    __shared__ double acc[FRMAX];
+    __shared__ double zrow[FROWS];
+    __shared__ uint8_t rowid[FCH];
+    const int g = blockIdx.x;
+    const int64_t pb = reg_base[g];
+    const int nr = (int)(reg_base[g + 1] - pb);
+    for (int r = threadIdx.x; r < nr; r += BS) acc[r] = 0.0;
+    const int s0 = reg_sub[g], s1 = reg_sub[g + 1];
+    const int gid = threadIdx.x / FG, gl = threadIdx.x % FG;
+    for (int s = s0; s < s1; ++s) {
+        const FusedSub sc = subs[s];
+        const int len = sc.len, nlr = sc.nlr, nrow = sc.nrow;
+        double v[FVPT];
+#pragma unroll
+        for (int i = 0; i < FVPT; ++i) {
+            const int j = threadIdx.x + i * BS;
+            v[i] = j < len ? __builtin_nontemporal_load(val + sc.e0 + j) : 0.0;
+        }
+        const uint16_t* pm = perm + sc.e0;
+        __syncthreads();                                   // the previous sub-chunk is done with prod
+        // q of every local ray to each of its entries
+        for (int r = threadIdx.x; r < nlr; r += BS) {
+            const uint32_t pk = lr_pk[sc.lr0 + r];
+            const int k1 = r + 1 < nlr ? (int)(lr_pk[sc.lr0 + r + 1] & 0xffffu) : len;
+            const double qv = q[lr_ray[sc.lr0 + r]];
+            for (int k = (int)(pk & 0xffffu); k < k1; ++k) prod[pm[k]] = qv;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < FVPT; ++i) {
+            const int j = threadIdx.x + i * BS;
+            if (j < len) prod[j] = v[i] * prod[j];
+        }
+        __syncthreads();
+        // z_j = B(j,:) q: FG lanes per row, strided partials, fixed tree
+        for (int ri = gid; ri < nrow; ri += BS / FG) {
+            const int a = (int)(rp[sc.r0 + ri] - sc.e0), b = (int)(rp[sc.r0 + ri + 1] - sc.e0);
+            double t = 0.0;
+            for (int j = a + gl; j < b; j += FG) {
+                t += prod[j];
+                rowid[j] = (uint8_t)ri;
+            }
+            t = group_sum<double, FG>(t);
+            if (gl == 0) {
+                zrow[ri] = t;
+                z[sc.r0 + ri] = t;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < FVPT; ++i) {
+            const int j = threadIdx.x + i * BS;
+            if (j < len) prod[j] = v[i] * zrow[rowid[j]];
+        }
+        __syncthreads();
+        // each local ray's share, in position order, into the region accumulator
+        for (int r = threadIdx.x; r < nlr; r += BS) {
+            const uint32_t pk = lr_pk[sc.lr0 + r];
+            const int k1 = r + 1 < nlr ? (int)(lr_pk[sc.lr0 + r + 1] & 0xffffu) : len;
+            double t = 0.0;
+            for (int k = (int)(pk & 0xffffu); k < k1; ++k) t += prod[pm[k]];
+            acc[pk >> 16] += t;
+        }
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < nr; r += BS) part[pb + r] = acc[r];
+}
+
+// w_i = sum of ray i's region partials, in region order
+__global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* __restrict__ rs_ptr,
+                                                     const int32_t* __restrict__ rs_slot,
+                                                     const double* __restrict__ part, double* __restrict__ w) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < m; i += (int64_t)gridDim.x * BS) {
+        double s = 0.0;
+        const int64_t k0 = rs_ptr[i], k1 = rs_ptr[i + 1];
+        for (int64_t k = k0; k < k1; ++k) s += part[rs_slot[k]];
+        w[i] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// plan (host, from B's CSR structure; once per operator)
+// ------------------------------------------------------------------------------------------
+namespace {
+template <typename F>
+void parallel_for(int64_t n, F f) {
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = std::max(1u, std::min(nt, 16u));
+    if (n < 64 || nt == 1) {
+        for (int64_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int64_t step = (n + nt - 1) / nt;
+    for (unsigned t = 0; t < nt; ++t) {
+        const int64_t a = t * step, b = std::min<int64_t>(n, a + step);
+        if (a >= b) break;
+        th.emplace_back([=, &f]() {
+            for (int64_t i = a; i < b; ++i) f(i);
+        });
+    }
+    for (auto& t : th) t.join();
+}
+
+template <typename T>
+T* upload(const std::vector<T>& v) {
+    T* d = nullptr;
+    const size_t bytes = std::max<size_t>(v.size(), 1) * sizeof(T);
+    if (hipMalloc(&d, bytes) != hipSuccess) throw Error{HGM_E_NOMEM, "fused plan: hipMalloc failed"};
+    if (!v.empty()) HGM_HIP(hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return d;
+}
+}  // namespace
+
+// Region (R x R pixel square) of every row of B (rows = pixels in B's stored order).
+static std::vector<int32_t> row_regions(const hgm_mat* B, int R, int64_t* nreg) {
+    const PixOrder o = B->row_order;
+    HGM_REQUIRE(!o.trivial() && o.N > 0 && (int64_t)o.N * o.N == B->rows,
+                "fused A*(B*q): B's rows must be the pixels of a tiled N x N grid");
+    const int N = o.N;
+    const int nb = (N + R - 1) / R;
+    *nreg = (int64_t)nb * nb;
+    const std::vector<int64_t> ref = pix_reference_of_stored(o);
+    std::vector<int32_t> reg(B->rows);
+    for (int64_t s = 0; s < B->rows; ++s) {
+        const int64_t r = ref[s] % N, c = ref[s] / N;
+        reg[s] = (int32_t)((c / R) * nb + r / R);
+    }
+    return reg;
+}
+
+FusedPlan* fused_plan_build(hgm_ctx* c, const hgm_mat* B, int R) {
+    HGM_REQUIRE(B->dtype == HGM_F64, "fused A*(B*q): fp64 operators");
+    HGM_REQUIRE(B->cols < (int64_t(1) << 31) && B->rows < (int64_t(1) << 31), "fused A*(B*q): index range");
+    const auto t0 = std::chrono::steady_clock::now();
+    const int64_t n = B->rows, m = B->cols, nnz = B->nnz;
+    int64_t nreg = 0;
+    const std::vector<int32_t> reg = row_regions(B, R, &nreg);
+    std::vector<int64_t> rp(n + 1);
+    std::vector<int32_t> ci(std::max<int64_t>(nnz, 1));
+    HGM_HIP(hipMemcpy(rp.data(), B->rp, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost));
+    if (nnz) HGM_HIP(hipMemcpy(ci.data(), B->ci, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
+    // sub-chunks: runs of rows of one region, cut at FCH entries / FROWS rows
+    struct Sub { int64_t e0; int32_t r0, reg; int len, nrow; };
+    std::vector<Sub> sv;
+    for (int64_t s = 0; s < n;) {
+        Sub u{rp[s], (int32_t)s, reg[s], 0, 0};
+        while (s < n && reg[s] == u.reg && u.nrow < FROWS && u.len + (rp[s + 1] - rp[s]) <= FCH) {
+            u.len += (int)(rp[s + 1] - rp[s]);
+            ++u.nrow;
+            ++s;
+        }
+        HGM_REQUIRE(u.nrow > 0, "fused A*(B*q): a row longer than the sub-chunk");
+        sv.push_back(u);
+    }
+    // plan order: by region, storage order inside a region
+    std::stable_sort(sv.begin(), sv.end(), [](const Sub& a, const Sub& b) { return a.reg < b.reg; });
+    const int64_t nsub = (int64_t)sv.size();
+    std::vector<int32_t> reg_sub(nreg + 1, 0);
+    for (const Sub& u : sv) reg_sub[u.reg + 1]++;
+    for (int64_t g = 0; g < nreg; ++g) reg_sub[g + 1] += reg_sub[g];
+    // local CSC of every sub-chunk: perm (entries in ray order), distinct rays and their starts
+    std::vector<uint16_t> perm(std::max<int64_t>(nnz, 1));
+    std::vector<std::vector<int32_t>> lray(nsub);
+    std::vector<std::vector<uint16_t>> lpos(nsub);
+    parallel_for(nsub, [&](int64_t i) {
+        const Sub& u = sv[i];
+        std::vector<uint64_t> key(u.len);
+        for (int k = 0; k < u.len; ++k) key[k] = ((uint64_t)(uint32_t)ci[u.e0 + k] << 16) | (uint64_t)k;
+        std::sort(key.begin(), key.end());
+        auto& lr = lray[i];
+        auto& lp = lpos[i];
+        for (int k = 0; k < u.len; ++k) {
+            const int32_t ray = (int32_t)(key[k] >> 16);
+            perm[u.e0 + k] = (uint16_t)(key[k] & 0xffffu);
+            if (k == 0 || ray != lr.back()) {
+                lr.push_back(ray);
+                lp.push_back((uint16_t)k);
+            }
+        }
+    });
+    // region ray sets (sorted), their sizes and each local ray's index in its region's set
+    std::vector<std::vector<int32_t>> rrays(nreg);
+    std::vector<std::vector<uint16_t>> lrr(nsub);
+    bool too_many = false;
+    parallel_for(nreg, [&](int64_t g) {
+        auto& rs = rrays[g];
+        for (int32_t i = reg_sub[g]; i < reg_sub[g + 1]; ++i) rs.insert(rs.end(), lray[i].begin(), lray[i].end());
+        std::sort(rs.begin(), rs.end());
+        rs.erase(std::unique(rs.begin(), rs.end()), rs.end());
+        if ((int)rs.size() > FRMAX) {
+            too_many = true;
+            return;
+        }
+        for (int32_t i = reg_sub[g]; i < reg_sub[g + 1]; ++i) {
+            auto& out = lrr[i];
+            out.resize(lray[i].size());
+            for (size_t k = 0; k < lray[i].size(); ++k)
+                out[k] = (uint16_t)(std::lower_bound(rs.begin(), rs.end(), lray[i][k]) - rs.begin());
+        }
+    });
+    HGM_REQUIRE(!too_many, "fused A*(B*q): a region is crossed by more rays than the LDS holds");
+    // flat device arrays
+    std::vector<FusedSub> subs(nsub);
+    int64_t nlr = 0;
+    for (int64_t i = 0; i < nsub; ++i) {
+        HGM_REQUIRE(lray[i].size() <= 0xffff, "fused A*(B*q): local rays");
+        subs[i] = FusedSub{sv[i].e0, nlr, sv[i].r0, (uint16_t)sv[i].len, (uint16_t)sv[i].nrow,
+                           (uint16_t)lray[i].size(), 0, 0, 0};
+        nlr += (int64_t)lray[i].size();
+    }
+    std::vector<int32_t> lr_ray(nlr);
+    std::vector<uint32_t> lr_pk(nlr);
+    parallel_for(nsub, [&](int64_t i) {
+        for (size_t k = 0; k < lray[i].size(); ++k) {
+            lr_ray[subs[i].lr0 + k] = lray[i][k];
+            lr_pk[subs[i].lr0 + k] = (uint32_t)lpos[i][k] | ((uint32_t)lrr[i][k] << 16);
+        }
+    });
+    std::vector<int64_t> reg_base(nreg + 1, 0);
+    for (int64_t g = 0; g < nreg; ++g) reg_base[g + 1] = reg_base[g] + (int64_t)rrays[g].size();
+    const int64_t nslot = reg_base[nreg];
+    HGM_REQUIRE(nslot < (int64_t(1) << 31), "fused A*(B*q): partial slots");
+    // ray-major reduction index: ray i's slots in region order
+    std::vector<int64_t> rs_ptr(m + 1, 0);
+    for (int64_t g = 0; g < nreg; ++g)
+        for (int32_t ray : rrays[g]) rs_ptr[ray + 1]++;
+    for (int64_t i = 0; i < m; ++i) rs_ptr[i + 1] += rs_ptr[i];
+    std::vector<int32_t> rs_slot(std::max<int64_t>(nslot, 1));
+    {
+        std::vector<int64_t> fill(rs_ptr.begin(), rs_ptr.end() - 1);
+        for (int64_t g = 0; g < nreg; ++g)
+            for (size_t r = 0; r < rrays[g].size(); ++r) rs_slot[fill[rrays[g][r]]++] = (int32_t)(reg_base[g] + r);
+    }
+    FusedPlan* P = new FusedPlan;
+    try {
+        P->region = R;
+        P->nreg = nreg;
+        P->nsub = nsub;
+        P->nlr = nlr;
+        P->nslot = nslot;
+        P->m = m;
+        P->reg_sub = upload(reg_sub);
+        P->reg_base = upload(reg_base);
+        P->subs = upload(subs);
+        P->perm = upload(perm);
+        P->lr_ray = upload(lr_ray);
+        P->lr_pk = upload(lr_pk);
+        P->rs_ptr = upload(rs_ptr);
+        P->rs_slot = upload(rs_slot);
+        if (hipMalloc(&P->part, sizeof(double) * std::max<int64_t>(nslot, 1)) != hipSuccess)
+            throw Error{HGM_E_NOMEM, "fused plan: hipMalloc failed"};
+    } catch (...) {
+        fused_plan_free(P);
+        throw;
+    }
+    (void)c;
+    P->build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return P;
+}
+
+// Whether w = A*(B*q) can run fused for this pair (B = A' value for value, fp64, tiled pixels).
+bool fused_ab_eligible(const hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
+    if (!c->num.fused_ab || c->num.parity || c->world > 1 || c->nccl || c->host_ar) return false;
+    if (!A || !B || A->dtype != HGM_F64 || B->dtype != HGM_F64) return false;
+    if (!(B->transpose_of == A->uid || A->transpose_of == B->uid)) return false;
+    const PixOrder o = B->row_order;
+    return !o.trivial() && (int64_t)o.N * o.N == B->rows && B->nnz > 0;
+}
+
+// The plan of B, built on first use (a failure to plan leaves the two-pass path in place).
+const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
+    if (!fused_ab_eligible(c, A, B)) return nullptr;
+    hgm_mat* Bm = const_cast<hgm_mat*>(B);
+    if (Bm->fused && Bm->fused->region != c->num.fused_region) {
+        fused_plan_free(Bm->fused);
+        Bm->fused = nullptr;
+        Bm->fused_failed = false;
+    }
+    if (!Bm->fused && !Bm->fused_failed) {
+        try {
+            Bm->fused = fused_plan_build(c, B, c->num.fused_region);
+        } catch (const Error& e) {
+            if (e.code != HGM_E_ARG) throw;
+            Bm->fused_failed = true;
+        }
+    }
+    return Bm->fused;
+}
+
+// Bq = B*q (n), ABq = A*(B*q) (m), one pass over B.
+void fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq) {
+    hipEvent_t t0 = nullptr;
+    timing_begin(c, KC_FUSED, &t0);
+    launch(c, false, k_fused_ab, dim3((unsigned)P->nreg), dim3(BS), (const FusedSub*)P->subs,
+           (const int32_t*)P->reg_sub, (const int64_t*)P->reg_base, (const uint16_t*)P->perm,
+           (const int32_t*)P->lr_ray, (const uint32_t*)P->lr_pk, (const int64_t*)B->rp, (const double*)B->val, q, Bq,
+           P->part);
+    launch(c, true, k_fused_reduce, dim3(grid_for(P->m)), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
+           (const int32_t*)P->rs_slot, (const double*)P->part, ABq);
+    HGM_HIP(hipGetLastError());
+    // algorithmic bytes of the fused pass: B's CSR once (values, 32-bit indices, row pointers),
+    // q read, z and w written (SURVEY.md §8(d)'s SpMV count for one pass over the operator)
+    const double bytes = 12.0 * (double)B->nnz + 8.0 * (B->rows + 1) + 8.0 * B->cols + 8.0 * B->rows + 8.0 * B->cols;
+    timing_end(c, KC_FUSED, t0, bytes);
+}
+
+}  // namespace hgm

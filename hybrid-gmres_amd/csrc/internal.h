@@ -45,14 +45,14 @@ struct DevBuf {
 };
 
 // Kernel classes timed by hgm_kernel_timing (bench roofline).
-enum KClass { KC_SPMV_A = 0, KC_SPMV_B = 1, KC_MGS = 2, KC_N = 3 };
+enum KClass { KC_SPMV_A = 0, KC_SPMV_B = 1, KC_MGS = 2, KC_FUSED = 3, KC_N = 4 };
 
 struct Timing {
     bool on = false;
     bool paused = false;   // hgm_kernel_timing_pause: armed but not recording
     unsigned mask = 0xffu;   // timed classes
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[KC_N];
-    double bytes[KC_N] = {0, 0, 0};
+    double bytes[KC_N] = {0, 0, 0, 0};
     std::vector<hipEvent_t> pool;
     hipEvent_t get();
     void clear();
@@ -77,7 +77,10 @@ struct Numerics {
     bool lsqr_dev = true;           // LSQR: device-resident beta/alpha/rotation (no host round trip)
     bool paged16 = true;            // streaming SpMV: paged gathers also for 16-bit-index operators
     bool band_dual = true;          // banded tiled ray-major operators: steep rows in row strips
+    bool fused_ab = true;           // m-space operator A*(B*q) in one pass over B (fused.hip)
+    int fused_region = 64;          // ... pixel square per workgroup (its rays accumulate in LDS)
 };
+struct FusedPlan;
 
 }  // namespace hgm
 
@@ -189,6 +192,9 @@ struct hgm_mat {
     int32_t* pg_ptr = nullptr;
     int32_t* pg_ids = nullptr;
     uint16_t* pg_lidx = nullptr;
+    // one-pass A*(B*q) plan over this pixel-major operator (fused.hip), built on first use
+    hgm::FusedPlan* fused = nullptr;
+    bool fused_failed = false;
 };
 
 namespace hgm {
@@ -401,6 +407,15 @@ void pix_permute(hgm_ctx* c, const PixOrder& o, const T* in, T* out, int dir);
 void pix_unmap_indices(hgm_ctx* c, const PixOrder& o, int32_t* idx, int64_t n);
 // reference index of every stored position (host vector, for host-side row reordering)
 std::vector<int64_t> pix_reference_of_stored(const PixOrder& o);
+
+// ---------------- one-pass m-space operator (fused.hip) ----------------
+// w = A*(B*q) and the kept B*q in one pass over B's pixel-major entries when B is A' value for
+// value.  fused_ab_plan: B's plan (built on first use), or nullptr when the
+// pair / context does not qualify (the two-pass path then runs).
+bool fused_ab_eligible(const hgm_ctx* c, const hgm_mat* A, const hgm_mat* B);
+const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B);
+void fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq);
+void fused_plan_free(FusedPlan* P);
 
 // ---------------- comm / scalars (capi.cpp) ----------------
 void allreduce(hgm_ctx* c, double* dev, int64_t count);

@@ -247,6 +247,7 @@ static void free_bands(hgm_mat* M) {
 
 void mat_free(hgm_mat* M) {
     if (!M) return;
+    fused_plan_free(M->fused);
     free_page_index(M);
     free_bands(M);
     if (M->ci16) (void)hipFree(M->ci16);

@@ -393,6 +393,8 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // recorded at the end of step k+1.  HGM_OPT_PEND_NORM = 0 keeps the scale pass.
     const bool pn_ok = nspace && !dist && orth == HGM_MGS && c->num.pend_norm && !parity &&
                        spmv_pn_ok(A, EPI_DIVH) && spmv_pn_ok(B, EPI_ADDQ);
+    // m-space side with B = A' value for value: B*q and A*(B*q) in one pass over B (fused.hip)
+    const FusedPlan* fplan = nspace ? nullptr : fused_ab_plan(c, A, B);
     PendNorm<T> pend;                                  // np > 0: Q(:,next step) awaits its division
     T* pn_h = c->buf<T>("pn_h", 2);
     // Enqueue Arnoldi step kq: operator application + orthogonalisation (+ Gram column).
@@ -419,17 +421,18 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             else apply_B<T>(c, B, Aq, v, EPI_NONE, T(0), nullptr);                  // B*(A*v)
         } else {
             T* Bq = BQ ? BQ + (int64_t)kq * ldbq : tn;
-            apply_B<T>(c, B, qk, Bq, EPI_NONE, T(0), nullptr);                      // B*Q(:,k)
-            if (ABQ && orth != HGM_CGS2) {
-                // A*(B*Q(:,k)) lands in its kept column; MGS reads it from there and
-                // writes the orthogonalised vector to Q(:,k+1) (no copy)
-                apply_A<T>(c, A, Bq, ABQ + (int64_t)kq * ldaq, EPI_NONE, T(0), nullptr);
+            // A*(B*Q(:,k)) lands in its kept column (MGS reads it from there and writes the
+            // orthogonalised vector to Q(:,k+1), no copy), or in Q(:,k+1) for CGS2
+            T* w = (ABQ && orth != HGM_CGS2) ? ABQ + (int64_t)kq * ldaq : v;
+            if (fplan) {
+                fused_ab(c, B, fplan, qk, Bq, w);                                   // both in one pass over B
             } else {
-                apply_A<T>(c, A, Bq, v, EPI_NONE, T(0), nullptr);                   // A*(B*Q(:,k))
-                if (ABQ)
-                    HGM_HIP(hipMemcpyAsync(ABQ + (int64_t)kq * ldaq, v, sizeof(T) * m, hipMemcpyDeviceToDevice,
-                                           c->stream));
+                apply_B<T>(c, B, qk, Bq, EPI_NONE, T(0), nullptr);                  // B*Q(:,k)
+                apply_A<T>(c, A, Bq, w, EPI_NONE, T(0), nullptr);                   // A*(B*Q(:,k))
             }
+            if (ABQ && orth == HGM_CGS2)
+                HGM_HIP(hipMemcpyAsync(ABQ + (int64_t)kq * ldaq, v, sizeof(T) * m, hipMemcpyDeviceToDevice,
+                                       c->stream));
         }
         // ---- orthogonalisation (hybrid_*_rtp.m:20-26) ----
         T* Hcol = dr + (size_t)kq * LH;                  // -> host H(:,k)

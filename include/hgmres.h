@@ -117,10 +117,15 @@ enum hgm_ctx_option {
                                       test stay on the device (same bits, no host round trip per iteration) [1] */
     HGM_OPT_PAGED16 = 16,          /* streaming SpMV: LDS-paged x gathers also for operators with <= 65,536
                                       columns (instead of their 16-bit column indices) [1] */
-    HGM_OPT_BAND_DUAL = 17         /* banded ray-major operators over a whole tiled N x N grid: rows steeper
+    HGM_OPT_BAND_DUAL = 17,        /* banded ray-major operators over a whole tiled N x N grid: rows steeper
                                       than 45 deg are cut into 64-pixel-row strips instead of 64-column strips,
                                       so every ray crosses its strips [1]; read when an operator is banded
                                       (creation, hgm_mat_set_bands) */
+    HGM_OPT_FUSED_AB = 18,         /* the m-space operator A*(B*q) of the AB solvers in ONE pass over B's
+                                      pixel-major entries when B is A' value for value (a device transpose
+                                      pair over a tiled pixel grid), single rank [1]: the kept B*q and
+                                      A*(B*q) come out of one kernel (plan built on first use) */
+    HGM_OPT_FUSED_REGION = 19      /* ... pixel square (side) per workgroup of that pass [64] */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for

@@ -1,0 +1,91 @@
+"""The one-pass m-space operator A*(B*q) (csrc/fused.hip; HGM_OPT_FUSED_AB).
+
+For the AB solvers (ABgmres_*_bounds.m:25, m-space Arnoldi on A*B) with B = A' value for value,
+B*q (the kept column) and A*(B*q) come out of one pass over B's pixel-major entries.  The sums run
+in another fixed order than the two-pass kernels', so:
+  * against the two-pass path and the oracle: H, x and the histories within 1e-10 (north_star),
+  * repeated solves: bitwise equal (no atomics),
+  * B*q itself (the kept column, read by x = (B*Q) y): within rounding of the two-pass product,
+  * pixel grids whose side is not a multiple of the region, several region sizes, and a region
+    crossed by more rays than the LDS holds (the plan is refused: the two-pass path runs).
+The full-size check (C4, 1e9 nnz, 20 iterations vs the oracle fixture) is
+tests/test_gpu_fullsize.py::test_c4_ab_gmres_full_size, which runs with the fused pass on (default).
+"""
+import numpy as np
+import pytest
+
+import hgmres
+from hgmres.problems import shepp_logan, tomo_problem
+from oracle import restatement as R
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-10
+
+
+def rel(a, b):
+    return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / max(np.linalg.norm(b), 1e-300))
+
+
+def hist_dev(a, b):
+    return float(np.max(np.abs(np.asarray(a) - np.asarray(b)) / np.abs(np.asarray(b))))
+
+
+def _device_problem(ctx, N, na, seed=0):
+    A = hgmres.SparseOperator.siddon(N, na, ctx=ctx)          # tiled pixel order (fused-eligible)
+    xt = shepp_logan(N).ravel(order="F")
+    b0 = A @ xt
+    e = np.random.default_rng(seed).standard_normal(A.shape[0])
+    return A, A.T, b0 + e / np.linalg.norm(e) * 1e-2 * np.linalg.norm(b0), xt
+
+
+@pytest.mark.parametrize("N,na,region", [(512, 30, 64), (100, 17, 64), (256, 47, 32), (256, 47, 16), (128, 90, 24)])
+def test_fused_ab_matches_two_pass_and_oracle(gpu_ctx, N, na, region):
+    A, B, b, xt = _device_problem(gpu_ctx, N, na)
+    k = 20
+    with gpu_ctx.options(fused_ab=0):
+        ref2 = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
+    with gpu_ctx.options(fused_ab=1, fused_region=region):
+        out = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
+        again = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
+        hyb = hgmres.ABgmres_hybrid_bounds(A, B, b, xt, 0.0, k, 1e-2, ctx=gpu_ctx, return_H=True)
+    with gpu_ctx.options(fused_ab=0):
+        hyb2 = hgmres.ABgmres_hybrid_bounds(A, B, b, xt, 0.0, k, 1e-2, ctx=gpu_ctx, return_H=True)
+    for a_, b_ in zip(out, again):
+        assert np.array_equal(np.asarray(a_), np.asarray(b_))               # bitwise reproducible
+    dH = float(np.max(np.abs(out[-1] - ref2[-1])) / np.max(np.abs(ref2[-1])))
+    print(f"[fused N={N} angles={na} region={region}] |dH| vs two-pass {dH:.1e}, x {rel(out[0], ref2[0]):.1e}")
+    assert dH <= TOL and rel(out[0], ref2[0]) <= TOL
+    assert hist_dev(out[1], ref2[1]) <= TOL and hist_dev(out[2], ref2[2]) <= TOL
+    assert rel(hyb[0], hyb2[0]) <= TOL and hist_dev(hyb[2], hyb2[2]) <= TOL
+    # the oracle on the downloaded operator (reference pixel order)
+    As = A.to_scipy()
+    Bs = As.T.tocsr()
+    xo, eo, ro, ko, Ho = R.ABgmres_nonhybrid_bounds(As, Bs, b, xt, 0.0, k, return_H=True)
+    assert ko == out[3] == k
+    assert float(np.max(np.abs(out[-1] - Ho)) / np.max(np.abs(Ho))) <= TOL
+    assert rel(out[0], xo) <= TOL and hist_dev(out[1], eo) <= TOL and hist_dev(out[2], ro) <= TOL
+
+
+def test_fused_region_overflow_falls_back(gpu_ctx):
+    """A 128 x 128 region at 47 angles is crossed by ~7,700 rays (> the 4,096 LDS accumulators):
+    the plan is refused and the two-pass path gives the result, bit for bit."""
+    A, B, b, xt = _device_problem(gpu_ctx, 256, 47)
+    with gpu_ctx.options(fused_ab=0):
+        ref = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True)
+    with gpu_ctx.options(fused_ab=1, fused_region=128):
+        out = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True)
+    for a_, b_ in zip(out, ref):
+        assert np.array_equal(np.asarray(a_), np.asarray(b_))
+
+
+def test_fused_not_taken_for_unmatched_or_reference_order(gpu_ctx):
+    """Unmatched B (not A' value for value) and reference-order operators keep the two-pass path:
+    the option changes nothing there."""
+    P = tomo_problem(32, 16, noise=1e-2, seed=0, backprojector="pixel")
+    outs = []
+    for f in (0, 1):
+        with gpu_ctx.options(fused_ab=f):
+            outs.append(hgmres.ABgmres_nonhybrid_bounds(P.A, P.B, P.b, P.x_true, 0.0, 8, ctx=gpu_ctx, return_H=True))
+    for a_, b_ in zip(*outs):
+        assert np.array_equal(np.asarray(a_), np.asarray(b_))
