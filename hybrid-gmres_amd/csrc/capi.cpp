@@ -499,6 +499,14 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             if (!(v >= 8 && v <= 1024 && v == std::floor(v))) return bad("fused_region is an integer in [8, 1024]");
             n.fused_region = (int)v;
             break;
+        case HGM_OPT_FUSED_BS:
+            if (!(v == 512 || v == 1024)) return bad("fused_bs is 512 or 1024");
+            n.fused_bs = (int)v;
+            break;
+        case HGM_OPT_FUSED_DBG:
+            if (!(v >= 0 && v <= 15 && v == std::floor(v))) return bad("fused_dbg is 0..15");
+            n.fused_dbg = (int)v;
+            break;
         default: return bad("unknown option");
     }
     return HGM_OK;
@@ -527,6 +535,8 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_BAND_DUAL: *v = n.band_dual; break;
         case HGM_OPT_FUSED_AB: *v = n.fused_ab; break;
         case HGM_OPT_FUSED_REGION: *v = n.fused_region; break;
+        case HGM_OPT_FUSED_BS: *v = n.fused_bs; break;
+        case HGM_OPT_FUSED_DBG: *v = n.fused_dbg; break;
         default: return HGM_E_ARG;
     }
     return HGM_OK;
@@ -778,6 +788,31 @@ HGM_API int hgm_spmv(hgm_ctx* c, const hgm_mat* A, const void* x, void* y) {
     HGM_TRY(c, {
         if (A->dtype == HGM_F64) spmv_ref<double>(c, A, (const double*)x, (double*)y);
         else spmv_ref<float>(c, A, (const float*)x, (float*)y);
+    });
+    return HGM_OK;
+}
+
+HGM_API int hgm_spmv_ab(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const void* q, void* Bq, void* ABq) {
+    if (!c || !A || !B || !q || !Bq || !ABq) return HGM_E_ARG;
+    HGM_TRY(c, {
+        HGM_REQUIRE(A->rows == B->cols && A->cols == B->rows, "spmv_ab: B must be size(A')");
+        HGM_REQUIRE(A->dtype == B->dtype, "spmv_ab: A and B share the dtype");
+        HGM_REQUIRE(A->col_order == B->row_order && A->row_order.trivial() && B->col_order.trivial(),
+                    "spmv_ab: A's columns and B's rows share the pixel order");
+        if (A->dtype == HGM_F64) {
+            double* bq = B->row_order.trivial() ? (double*)Bq : c->buf<double>("spmv_ab_bq", B->rows);
+            const FusedPlan* P = fused_ab_plan(c, A, B);
+            if (P) {
+                fused_ab(c, B, P, (const double*)q, bq, (double*)ABq);
+            } else {
+                spmv<double>(c, B, (const double*)q, bq, EPI_NONE, 0.0, nullptr, KC_SPMV_B);
+                spmv<double>(c, A, bq, (double*)ABq, EPI_NONE, 0.0, nullptr, KC_SPMV_A);
+            }
+            if (!B->row_order.trivial()) pix_permute<double>(c, B->row_order, bq, (double*)Bq, 1);
+        } else {
+            spmv_ref<float>(c, B, (const float*)q, (float*)Bq);
+            spmv_ref<float>(c, A, (const float*)Bq, (float*)ABq);
+        }
     });
     return HGM_OK;
 }

@@ -32,10 +32,9 @@ namespace hgm {
 
 namespace {
 constexpr int FCH = 4096;      // entries per sub-chunk
-constexpr int FRMAX = 4096;    // rays per region (LDS accumulators)
+constexpr int FRMAX = 3968;    // rays per region (LDS accumulators; 64 x 64 pixels at 47 angles: ~3,900)
+constexpr int FLRMAX = 768;    // distinct rays per sub-chunk (C4: <= ~700)
 constexpr int FROWS = 128;     // pixel rows per sub-chunk
-constexpr int FG = 4;          // lanes per row sum
-constexpr int FVPT = FCH / BS; // values per thread
 }  // namespace
 
 struct FusedSub {
@@ -57,7 +56,7 @@ struct FusedPlan {
     FusedSub* subs = nullptr;     // nsub
     uint16_t* perm = nullptr;     // nnz
     int32_t* lr_ray = nullptr;    // nlr
-    uint32_t* lr_pk = nullptr;    // nlr: first position | region ray index << 16
+    uint32_t* lr_pk = nullptr;    // nlr: first position | entries << 12 | region ray index << 20
     int64_t* rs_ptr = nullptr;    // m+1
     int32_t* rs_slot = nullptr;   // nslot
     double* part = nullptr;       // nslot
@@ -75,79 +74,141 @@ void fused_plan_free(FusedPlan* P) {
 // ------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BS) void k_fused_ab(const FusedSub* __restrict__ subs, const int32_t* __restrict__ reg_sub,
-                                                 const int64_t* __restrict__ reg_base,
-                                                 const uint16_t* __restrict__ perm, const int32_t* __restrict__ lr_ray,
-                                                 const uint32_t* __restrict__ lr_pk, const int64_t* __restrict__ rp,
-                                                 const double* __restrict__ val, const double* __restrict__ q,
-                                                 double* __restrict__ z, double* __restrict__ part) {
+// FBS threads per workgroup; LDS 77 KB (two workgroups per CU), so FBS sets the waves in flight.
+// Every global read of a sub-chunk is issued as a batch (values and perm, entry j on thread
+// j mod FBS: every load instruction coalesced; the local-ray records and row pointers; then the q
+// gathers of its rays) and the loops over entries run from LDS.  The local rays come longest first
+// (plan order), so the lanes of a wave walk rays of about the same length.  FGR lanes per row sum.
+// Measured variants (C4, one box): consecutive entries per thread for 16-byte LDS accesses made
+// every value load strided (4.71 vs 3.73 ms); software pipelining of the next sub-chunk's loads
+// cost the registers two workgroups per CU need (4.39 ms, spilling at 1024 threads).
+// dbg (HGM_OPT_FUSED_DBG, timing experiments only; the results are then wrong): bit 1 skips the
+// q scatter, 2 the row sums, 4 the per-ray sums, 8 the two elementwise passes.
+template <int FBS, int FGR>
+__global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 8))) void k_fused_ab(
+    const FusedSub* __restrict__ subs, const int32_t* __restrict__ reg_sub, const int64_t* __restrict__ reg_base,
+    const uint16_t* __restrict__ perm, const int32_t* __restrict__ lr_ray, const uint32_t* __restrict__ lr_pk,
+    const int64_t* __restrict__ rp, const double* __restrict__ val, const double* __restrict__ q,
+    double* __restrict__ z, double* __restrict__ part, int dbg) {
+    constexpr int VPT = FCH / FBS;                      // entries per thread
+    constexpr int RPT = (FLRMAX + FBS - 1) / FBS;       // local rays per thread
+    static_assert(FBS > FROWS, "one row pointer per thread");
     __shared__ double prod[FCH];
     __shared__ double acc[FRMAX];
+    __shared__ uint16_t sperm[FCH];
+    __shared__ int32_t srp[FROWS + 1];
     __shared__ double zrow[FROWS];
     __shared__ uint8_t rowid[FCH];
     const int g = blockIdx.x;
     const int64_t pb = reg_base[g];
     const int nr = (int)(reg_base[g + 1] - pb);
-    for (int r = threadIdx.x; r < nr; r += BS) acc[r] = 0.0;
+    for (int r = threadIdx.x; r < nr; r += FBS) acc[r] = 0.0;
     const int s0 = reg_sub[g], s1 = reg_sub[g + 1];
-    const int gid = threadIdx.x / FG, gl = threadIdx.x % FG;
+    const int gid = threadIdx.x / FGR, gl = threadIdx.x % FGR;
     for (int s = s0; s < s1; ++s) {
-        const FusedSub sc = subs[s];
+        // the record through two 16-byte uniform loads (scalar unit), unpacked
+        const int4 w0 = reinterpret_cast<const int4*>(subs + s)[0];
+        const int4 w1 = reinterpret_cast<const int4*>(subs + s)[1];
+        FusedSub sc;
+        sc.e0 = (int64_t)(uint32_t)w0.x | ((int64_t)w0.y << 32);
+        sc.lr0 = (int64_t)(uint32_t)w0.z | ((int64_t)w0.w << 32);
+        sc.r0 = w1.x;
+        sc.len = (uint16_t)(w1.y & 0xffff);
+        sc.nrow = (uint16_t)((uint32_t)w1.y >> 16);
+        sc.nlr = (uint16_t)(w1.z & 0xffff);
         const int len = sc.len, nlr = sc.nlr, nrow = sc.nrow;
-        double v[FVPT];
+        // Branch-free loads through buffer resources sized to the sub-chunk (a load past the end
+        // returns 0): conditional loads made hipcc wait for every earlier load at each branch, so
+        // the batch went out one round trip at a time.  The ray ids go first, so the q gathers
+        // that depend on them wait for those alone (vmcnt retires in issue order).
+        const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + sc.e0, len * 8);
+        const __amdgpu_buffer_rsrc_t rpm = buf_rsrc(perm + sc.e0, len * 2);
+        const __amdgpu_buffer_rsrc_t rk = buf_rsrc(lr_pk + sc.lr0, nlr * 4);
+        const __amdgpu_buffer_rsrc_t ry = buf_rsrc(lr_ray + sc.lr0, nlr * 4);
+        const __amdgpu_buffer_rsrc_t rr = buf_rsrc(rp + sc.r0, (nrow + 1) * 8);
+        int32_t ray[RPT];
 #pragma unroll
-        for (int i = 0; i < FVPT; ++i) {
-            const int j = threadIdx.x + i * BS;
-            v[i] = j < len ? __builtin_nontemporal_load(val + sc.e0 + j) : 0.0;
-        }
-        const uint16_t* pm = perm + sc.e0;
-        __syncthreads();                                   // the previous sub-chunk is done with prod
-        // q of every local ray to each of its entries
-        for (int r = threadIdx.x; r < nlr; r += BS) {
-            const uint32_t pk = lr_pk[sc.lr0 + r];
-            const int k1 = r + 1 < nlr ? (int)(lr_pk[sc.lr0 + r + 1] & 0xffffu) : len;
-            const double qv = q[lr_ray[sc.lr0 + r]];
-            for (int k = (int)(pk & 0xffffu); k < k1; ++k) prod[pm[k]] = qv;
-        }
-        __syncthreads();
+        for (int i = 0; i < RPT; ++i)
+            ray[i] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ry, (threadIdx.x + i * FBS) * 4, 0, 0);
+        double qv[RPT];
 #pragma unroll
-        for (int i = 0; i < FVPT; ++i) {
-            const int j = threadIdx.x + i * BS;
-            if (j < len) prod[j] = v[i] * prod[j];
+        for (int i = 0; i < RPT; ++i) qv[i] = q[ray[i]];      // (ray 0 past nlr: a harmless read)
+        uint32_t pk[RPT];
+#pragma unroll
+        for (int i = 0; i < RPT; ++i)
+            pk[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rk, (threadIdx.x + i * FBS) * 4, 0, 0);
+        const int rpv = (int)(__builtin_bit_cast(int64_t, __builtin_amdgcn_raw_buffer_load_b64(rr, threadIdx.x * 8, 0, 0)) -
+                              sc.e0);
+        double v[VPT];
+        uint16_t pv[VPT];
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            const int j = threadIdx.x + i * FBS;
+            v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, j * 8, 0, 2));
+            pv[i] = (uint16_t)__builtin_amdgcn_raw_buffer_load_b16(rpm, j * 2, 0, 2);
         }
+        __syncthreads();                                   // the previous sub-chunk is done with the LDS
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) sperm[threadIdx.x + i * FBS] = pv[i];
+        if (threadIdx.x <= nrow) srp[threadIdx.x] = rpv;
         __syncthreads();
-        // z_j = B(j,:) q: FG lanes per row, strided partials, fixed tree
-        for (int ri = gid; ri < nrow; ri += BS / FG) {
-            const int a = (int)(rp[sc.r0 + ri] - sc.e0), b = (int)(rp[sc.r0 + ri + 1] - sc.e0);
-            double t = 0.0;
-            for (int j = a + gl; j < b; j += FG) {
-                t += prod[j];
-                rowid[j] = (uint8_t)ri;
+        // q of every local ray to each of its entries (pk: first position | length << 12 | rr << 20)
+        if (!(dbg & 1)) {
+#pragma unroll
+            for (int i = 0; i < RPT; ++i) {
+                const int k0 = (int)(pk[i] & 0xfffu), k1 = k0 + (int)((pk[i] >> 12) & 0xffu);
+                for (int k = k0; k < k1; ++k) prod[sperm[k]] = qv[i];
             }
-            t = group_sum<double, FG>(t);
-            if (gl == 0) {
-                zrow[ri] = t;
-                z[sc.r0 + ri] = t;
+        }
+        __syncthreads();
+        if (!(dbg & 8)) {
+#pragma unroll
+            for (int i = 0; i < VPT; ++i) {
+                const int j = threadIdx.x + i * FBS;
+                if (j < len) prod[j] = v[i] * prod[j];
             }
         }
         __syncthreads();
+        // z_j = B(j,:) q: FGR lanes per row, strided partials, fixed tree
+        if (!(dbg & 2)) {
+            for (int ri = gid; ri < nrow; ri += FBS / FGR) {
+                const int a = srp[ri], b = srp[ri + 1];
+                double t = 0.0;
+                for (int j = a + gl; j < b; j += FGR) {
+                    t += prod[j];
+                    rowid[j] = (uint8_t)ri;
+                }
+                t = group_sum<double, FGR>(t);
+                if (gl == 0) {
+                    zrow[ri] = t;
+                    z[sc.r0 + ri] = t;
+                }
+            }
+        }
+        __syncthreads();
+        if (!(dbg & 8)) {
 #pragma unroll
-        for (int i = 0; i < FVPT; ++i) {
-            const int j = threadIdx.x + i * BS;
-            if (j < len) prod[j] = v[i] * zrow[rowid[j]];
+            for (int i = 0; i < VPT; ++i) {
+                const int j = threadIdx.x + i * FBS;
+                if (j < len) prod[j] = v[i] * zrow[rowid[j]];
+            }
         }
         __syncthreads();
         // each local ray's share, in position order, into the region accumulator
-        for (int r = threadIdx.x; r < nlr; r += BS) {
-            const uint32_t pk = lr_pk[sc.lr0 + r];
-            const int k1 = r + 1 < nlr ? (int)(lr_pk[sc.lr0 + r + 1] & 0xffffu) : len;
-            double t = 0.0;
-            for (int k = (int)(pk & 0xffffu); k < k1; ++k) t += prod[pm[k]];
-            acc[pk >> 16] += t;
+        if (!(dbg & 4)) {
+#pragma unroll
+            for (int i = 0; i < RPT; ++i) {
+                const int k0 = (int)(pk[i] & 0xfffu), k1 = k0 + (int)((pk[i] >> 12) & 0xffu);
+                if (k1 > k0) {
+                    double t = 0.0;
+                    for (int k = k0; k < k1; ++k) t += prod[sperm[k]];
+                    acc[pk[i] >> 20] += t;
+                }
+            }
         }
     }
     __syncthreads();
-    for (int r = threadIdx.x; r < nr; r += BS) part[pb + r] = acc[r];
+    for (int r = threadIdx.x; r < nr; r += FBS) part[pb + r] = acc[r];
 }
 
 // w_i = sum of ray i's region partials, in region order
@@ -237,6 +298,33 @@ FusedPlan* fused_plan_build(hgm_ctx* c, const hgm_mat* B, int R) {
         HGM_REQUIRE(u.nrow > 0, "fused A*(B*q): a row longer than the sub-chunk");
         sv.push_back(u);
     }
+    // sub-chunks crossed by more than FLRMAX distinct rays (many angles) are halved by rows until
+    // none is (a sub-chunk keeps whole rows, so a single row always fits: <= FCH entries)
+    auto distinct_rays = [&](const Sub& u) {
+        std::vector<int32_t> r(ci.begin() + u.e0, ci.begin() + u.e0 + u.len);
+        std::sort(r.begin(), r.end());
+        return (int)(std::unique(r.begin(), r.end()) - r.begin());
+    };
+    for (bool again = true; again;) {
+        std::vector<char> big(sv.size(), 0);
+        parallel_for((int64_t)sv.size(), [&](int64_t i) { big[i] = distinct_rays(sv[i]) > FLRMAX; });
+        again = false;
+        std::vector<Sub> nv;
+        for (size_t i = 0; i < sv.size(); ++i) {
+            if (!big[i] || sv[i].nrow < 2) {
+                HGM_REQUIRE(!big[i], "fused A*(B*q): a pixel row is crossed by too many rays");
+                nv.push_back(sv[i]);
+                continue;
+            }
+            again = true;
+            const Sub& u = sv[i];
+            const int h = u.nrow / 2;
+            const int l0 = (int)(rp[u.r0 + h] - u.e0);
+            nv.push_back(Sub{u.e0, u.r0, u.reg, l0, h});
+            nv.push_back(Sub{u.e0 + l0, u.r0 + h, u.reg, u.len - l0, u.nrow - h});
+        }
+        sv.swap(nv);
+    }
     // plan order: by region, storage order inside a region
     std::stable_sort(sv.begin(), sv.end(), [](const Sub& a, const Sub& b) { return a.reg < b.reg; });
     const int64_t nsub = (int64_t)sv.size();
@@ -263,6 +351,8 @@ FusedPlan* fused_plan_build(hgm_ctx* c, const hgm_mat* B, int R) {
             }
         }
     });
+    for (int64_t i = 0; i < nsub; ++i)
+        HGM_REQUIRE((int)lray[i].size() <= FLRMAX, "fused A*(B*q): a sub-chunk is crossed by too many rays");
     // region ray sets (sorted), their sizes and each local ray's index in its region's set
     std::vector<std::vector<int32_t>> rrays(nreg);
     std::vector<std::vector<uint16_t>> lrr(nsub);
@@ -293,14 +383,27 @@ FusedPlan* fused_plan_build(hgm_ctx* c, const hgm_mat* B, int R) {
                            (uint16_t)lray[i].size(), 0, 0, 0};
         nlr += (int64_t)lray[i].size();
     }
+    // records: first position (12 bits) | entries (8) | region ray index (12); longest first, so
+    // the lanes of a wave walk rays of about the same length (ties: position order)
     std::vector<int32_t> lr_ray(nlr);
     std::vector<uint32_t> lr_pk(nlr);
+    bool rec_ok = true;
     parallel_for(nsub, [&](int64_t i) {
-        for (size_t k = 0; k < lray[i].size(); ++k) {
-            lr_ray[subs[i].lr0 + k] = lray[i][k];
-            lr_pk[subs[i].lr0 + k] = (uint32_t)lpos[i][k] | ((uint32_t)lrr[i][k] << 16);
+        const size_t nl = lray[i].size();
+        std::vector<int> ord(nl), lenv(nl);
+        for (size_t k = 0; k < nl; ++k) {
+            ord[k] = (int)k;
+            lenv[k] = (k + 1 < nl ? (int)lpos[i][k + 1] : sv[i].len) - (int)lpos[i][k];
+            if (lenv[k] > 0xff || lrr[i][k] > 0xfff) rec_ok = false;
+        }
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return lenv[a] > lenv[b]; });
+        for (size_t k = 0; k < nl; ++k) {
+            const int o = ord[k];
+            lr_ray[subs[i].lr0 + k] = lray[i][o];
+            lr_pk[subs[i].lr0 + k] = (uint32_t)lpos[i][o] | ((uint32_t)lenv[o] << 12) | ((uint32_t)lrr[i][o] << 20);
         }
     });
+    HGM_REQUIRE(rec_ok, "fused A*(B*q): a ray's share of a sub-chunk or a region's ray count exceeds the record");
     std::vector<int64_t> reg_base(nreg + 1, 0);
     for (int64_t g = 0; g < nreg; ++g) reg_base[g + 1] = reg_base[g] + (int64_t)rrays[g].size();
     const int64_t nslot = reg_base[nreg];
@@ -376,10 +479,15 @@ const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
 void fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq) {
     hipEvent_t t0 = nullptr;
     timing_begin(c, KC_FUSED, &t0);
-    launch(c, false, k_fused_ab, dim3((unsigned)P->nreg), dim3(BS), (const FusedSub*)P->subs,
-           (const int32_t*)P->reg_sub, (const int64_t*)P->reg_base, (const uint16_t*)P->perm,
-           (const int32_t*)P->lr_ray, (const uint32_t*)P->lr_pk, (const int64_t*)B->rp, (const double*)B->val, q, Bq,
-           P->part);
+#define HGM_FUSED_LAUNCH(FB, FGV)                                                                               \
+    launch(c, false, k_fused_ab<FB, FGV>, dim3((unsigned)P->nreg), dim3(FB), (const FusedSub*)P->subs,           \
+           (const int32_t*)P->reg_sub, (const int64_t*)P->reg_base, (const uint16_t*)P->perm,                    \
+           (const int32_t*)P->lr_ray, (const uint32_t*)P->lr_pk, (const int64_t*)B->rp, (const double*)B->val, q, \
+           Bq, P->part, c->num.fused_dbg)
+    // (one lane count per row sum for both sizes: the same summation order, the same bits)
+    if (c->num.fused_bs == 512) HGM_FUSED_LAUNCH(512, 16);
+    else HGM_FUSED_LAUNCH(1024, 16);
+#undef HGM_FUSED_LAUNCH
     launch(c, true, k_fused_reduce, dim3(grid_for(P->m)), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
            (const int32_t*)P->rs_slot, (const double*)P->part, ABq);
     HGM_HIP(hipGetLastError());

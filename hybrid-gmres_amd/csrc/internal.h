@@ -79,6 +79,8 @@ struct Numerics {
     bool band_dual = true;          // banded tiled ray-major operators: steep rows in row strips
     bool fused_ab = true;           // m-space operator A*(B*q) in one pass over B (fused.hip)
     int fused_region = 64;          // ... pixel square per workgroup (its rays accumulate in LDS)
+    int fused_bs = 1024;            // ... threads per workgroup (512, 1024)
+    int fused_dbg = 0;              // ... timing experiments: skip phases (wrong results)
 };
 struct FusedPlan;
 

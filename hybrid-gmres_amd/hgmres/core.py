@@ -368,6 +368,33 @@ class SparseOperator:
             pass
 
 
+def spmv_ab(A: "SparseOperator", B: "SparseOperator", q):
+    """(B*q, A*(B*q)) through ``hgm_spmv_ab`` (host arrays in, host arrays out): the m-space
+    operator of the AB solvers, one pass over B when B is A' value for value (fused.hip)."""
+    ctx = A.ctx
+    lib = L.load()
+    m, n = A.shape
+    es = 8 if A.dtype == L.HGM_F64 else 4
+    dt = np.float64 if es == 8 else np.float32
+    q = np.ascontiguousarray(np.asarray(q, dtype=dt).reshape(-1))
+    if q.shape[0] != m:
+        raise ValueError(f"q has length {q.shape[0]}, expected {m}")
+    ptr = [C.c_void_p() for _ in range(3)]
+    try:
+        for p_, k in zip(ptr, (m, n, m)):
+            _check(lib.hgm_dev_alloc(ctx.handle, es * max(1, k), C.byref(p_)), ctx)
+        _check(lib.hgm_memcpy_h2d(ctx.handle, ptr[0], q.ctypes.data_as(C.c_void_p), es * m), ctx)
+        _check(lib.hgm_spmv_ab(ctx.handle, A._h, B._h, ptr[0], ptr[1], ptr[2]), ctx)
+        bq, abq = np.empty(n, dtype=dt), np.empty(m, dtype=dt)
+        _check(lib.hgm_memcpy_d2h(ctx.handle, bq.ctypes.data_as(C.c_void_p), ptr[1], es * n), ctx)
+        _check(lib.hgm_memcpy_d2h(ctx.handle, abq.ctypes.data_as(C.c_void_p), ptr[2], es * m), ctx)
+    finally:
+        for p_ in ptr:
+            if p_.value:
+                lib.hgm_dev_free(ctx.handle, p_)
+    return bq.astype(np.float64), abq.astype(np.float64)
+
+
 def as_operator(M, ctx=None, dtype=L.HGM_F64) -> SparseOperator:
     if isinstance(M, SparseOperator):
         return M

@@ -125,7 +125,9 @@ enum hgm_ctx_option {
                                       pixel-major entries when B is A' value for value (a device transpose
                                       pair over a tiled pixel grid), single rank [1]: the kept B*q and
                                       A*(B*q) come out of one kernel (plan built on first use) */
-    HGM_OPT_FUSED_REGION = 19      /* ... pixel square (side) per workgroup of that pass [64] */
+    HGM_OPT_FUSED_REGION = 19,     /* ... pixel square (side) per workgroup of that pass [64] */
+    HGM_OPT_FUSED_BS = 20,         /* ... threads per workgroup: 512 or 1024 [1024] (same summation order) */
+    HGM_OPT_FUSED_DBG = 21         /* ... timing experiments only: bits skip its phases, results WRONG [0] */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for
@@ -220,6 +222,14 @@ HGM_API void hgm_mat_destroy(hgm_mat* mat);
 
 /* y = A*x on device pointers (elements of the matrix dtype), on the context stream. */
 HGM_API int hgm_spmv(hgm_ctx* ctx, const hgm_mat* A, const void* x_dev, void* y_dev);
+
+/* The m-space operator of the AB solvers (ABgmres_*_bounds.m:25, gcv_function.m:20):
+ * Bq = B*q (n) and ABq = A*(B*q) (m), device pointers, on the context stream.  When B is A' value
+ * for value (hgm_mat_transpose) over a tiled pixel grid, fp64, one rank, both come out of ONE pass
+ * over B's entries (HGM_OPT_FUSED_AB; the plan is built on first use); otherwise two SpMVs.  Bq is
+ * in the reference pixel order, as hgm_spmv's. */
+HGM_API int hgm_spmv_ab(hgm_ctx* ctx, const hgm_mat* A, const hgm_mat* B, const void* q_dev, void* Bq_dev,
+                        void* ABq_dev);
 
 /* ---- device memory helpers (for callers without their own allocator) ---- */
 HGM_API int hgm_dev_alloc(hgm_ctx* ctx, int64_t bytes, void** ptr);

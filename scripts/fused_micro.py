@@ -1,0 +1,49 @@
+"""Micro-benchmark of the m-space operator A*(B*q) (hgm_spmv_ab) at a BASELINE geometry: the
+one-pass kernel (fused.hip) against the two SpMVs, and phase-skip timing variants (fused_dbg:
+results wrong, timing only).  Prints one JSON line per variant.  Run on the GPU box:
+    python scripts/fused_micro.py [N angles reps]"""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "hybrid-gmres_amd"), ROOT]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+import hgmres  # noqa: E402
+from hgmres import _lib as L  # noqa: E402
+
+N, na, reps = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (4096, 47, 20)))
+variants = sys.argv[4].split(",") if len(sys.argv) > 4 else ["two", "f1024", "f512", "d1", "d2", "d4", "d8", "d15"]
+ctx = hgmres.Context(0)
+lib = L.load()
+A = hgmres.SparseOperator.siddon(N, na, ctx=ctx)
+B = A.T
+m, n = A.shape
+dev = torch.device("cuda", 0)
+q = torch.from_numpy(np.random.default_rng(0).standard_normal(m)).to(dev)
+bq = torch.empty(n, dtype=torch.float64, device=dev)
+abq = torch.empty(m, dtype=torch.float64, device=dev)
+P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+two = 2 * 12.0 * A.nnz + 8.0 * (m + 1) + 8.0 * (n + 1) + 16.0 * (m + n)
+ref = None
+for vname in variants:
+    opts = {"two": dict(fused_ab=0), "f1024": dict(fused_ab=1, fused_bs=1024), "f512": dict(fused_ab=1, fused_bs=512)}
+    o = opts.get(vname, dict(fused_ab=1, fused_dbg=int(vname[1:]) if vname.startswith("d") else 0))
+    with ctx.options(**o):
+        lib.hgm_spmv_ab(ctx.handle, A._h, B._h, P(q), P(bq), P(abq))      # plan / warm-up
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            rc = lib.hgm_spmv_ab(ctx.handle, A._h, B._h, P(q), P(bq), P(abq))
+        ctx.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+    assert rc == 0
+    out = abq.cpu().numpy()
+    if vname == "two":
+        ref = (bq.cpu().numpy(), out)
+    dev_ = None if ref is None else float(np.linalg.norm(out - ref[1]) / np.linalg.norm(ref[1]))
+    print(json.dumps({"variant": vname, "N": N, "angles": na, "ms": round(dt * 1e3, 4),
+                      "effective_GBps_two_pass": round(two / dt / 1e9, 1), "rel_dev_vs_two_pass": dev_}), flush=True)

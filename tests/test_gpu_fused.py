@@ -49,6 +49,10 @@ def test_fused_ab_matches_two_pass_and_oracle(gpu_ctx, N, na, region):
         out = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
         again = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
         hyb = hgmres.ABgmres_hybrid_bounds(A, B, b, xt, 0.0, k, 1e-2, ctx=gpu_ctx, return_H=True)
+        # the workgroup-size variant keeps the summation order: the same bits
+        with gpu_ctx.options(fused_bs=512):
+            o2 = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
+        assert all(np.array_equal(np.asarray(a_), np.asarray(b_)) for a_, b_ in zip(out, o2))
     with gpu_ctx.options(fused_ab=0):
         hyb2 = hgmres.ABgmres_hybrid_bounds(A, B, b, xt, 0.0, k, 1e-2, ctx=gpu_ctx, return_H=True)
     for a_, b_ in zip(out, again):
