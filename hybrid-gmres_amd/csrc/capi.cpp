@@ -503,6 +503,7 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             if (!(v == 512 || v == 1024)) return bad("fused_bs is 512 or 1024");
             n.fused_bs = (int)v;
             break;
+        case HGM_OPT_FUSED_PF: if (!b01) return bad("fused_pf is 0 or 1"); n.fused_pf = v != 0; break;
         case HGM_OPT_FUSED_DBG:
             if (!(v >= 0 && v <= 15 && v == std::floor(v))) return bad("fused_dbg is 0..15");
             n.fused_dbg = (int)v;
@@ -537,6 +538,7 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_FUSED_REGION: *v = n.fused_region; break;
         case HGM_OPT_FUSED_BS: *v = n.fused_bs; break;
         case HGM_OPT_FUSED_DBG: *v = n.fused_dbg; break;
+        case HGM_OPT_FUSED_PF: *v = n.fused_pf; break;
         default: return HGM_E_ARG;
     }
     return HGM_OK;

@@ -74,6 +74,17 @@ void fused_plan_free(FusedPlan* P) {
 // ------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------
+// Workgroup barrier for LDS hand-offs only: this wave's LDS accesses retire (lgkmcnt), then
+// s_barrier; the empty asm statements keep the compiler from moving memory accesses across it.
+// __syncthreads() is a release/acquire fence as well, and with the kernel's global stores (z) in
+// flight its fence drains vmcnt -- every global load still in flight, the next sub-chunk's batch
+// included -- at every barrier.
+__device__ __forceinline__ void lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // FBS threads per workgroup; LDS 77 KB (two workgroups per CU), so FBS sets the waves in flight.
 // Every global read of a sub-chunk is issued as a batch (values and perm, entry j on thread
 // j mod FBS: every load instruction coalesced; the local-ray records and row pointers; then the q
@@ -84,7 +95,7 @@ void fused_plan_free(FusedPlan* P) {
 // cost the registers two workgroups per CU need (4.39 ms, spilling at 1024 threads).
 // dbg (HGM_OPT_FUSED_DBG, timing experiments only; the results are then wrong): bit 1 skips the
 // q scatter, 2 the row sums, 4 the per-ray sums, 8 the two elementwise passes.
-template <int FBS, int FGR>
+template <int FBS, int FGR, bool PF>
 __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 8))) void k_fused_ab(
     const FusedSub* __restrict__ subs, const int32_t* __restrict__ reg_sub, const int64_t* __restrict__ reg_base,
     const uint16_t* __restrict__ perm, const int32_t* __restrict__ lr_ray, const uint32_t* __restrict__ lr_pk,
@@ -105,53 +116,70 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
     for (int r = threadIdx.x; r < nr; r += FBS) acc[r] = 0.0;
     const int s0 = reg_sub[g], s1 = reg_sub[g + 1];
     const int gid = threadIdx.x / FGR, gl = threadIdx.x % FGR;
-    for (int s = s0; s < s1; ++s) {
-        // the record through two 16-byte uniform loads (scalar unit), unpacked
-        const int4 w0 = reinterpret_cast<const int4*>(subs + s)[0];
-        const int4 w1 = reinterpret_cast<const int4*>(subs + s)[1];
+    // one sub-chunk's operands, loaded branch-free through buffer resources sized to it (a load
+    // past the end returns 0): conditional loads made hipcc wait for every earlier load at each
+    // branch, so a batch went out one round trip at a time.  The ray ids go first, so the q
+    // gathers that depend on them wait for those alone (vmcnt retires in issue order).
+    struct Batch {
         FusedSub sc;
-        sc.e0 = (int64_t)(uint32_t)w0.x | ((int64_t)w0.y << 32);
-        sc.lr0 = (int64_t)(uint32_t)w0.z | ((int64_t)w0.w << 32);
-        sc.r0 = w1.x;
-        sc.len = (uint16_t)(w1.y & 0xffff);
-        sc.nrow = (uint16_t)((uint32_t)w1.y >> 16);
-        sc.nlr = (uint16_t)(w1.z & 0xffff);
-        const int len = sc.len, nlr = sc.nlr, nrow = sc.nrow;
-        // Branch-free loads through buffer resources sized to the sub-chunk (a load past the end
-        // returns 0): conditional loads made hipcc wait for every earlier load at each branch, so
-        // the batch went out one round trip at a time.  The ray ids go first, so the q gathers
-        // that depend on them wait for those alone (vmcnt retires in issue order).
-        const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + sc.e0, len * 8);
-        const __amdgpu_buffer_rsrc_t rpm = buf_rsrc(perm + sc.e0, len * 2);
-        const __amdgpu_buffer_rsrc_t rk = buf_rsrc(lr_pk + sc.lr0, nlr * 4);
-        const __amdgpu_buffer_rsrc_t ry = buf_rsrc(lr_ray + sc.lr0, nlr * 4);
-        const __amdgpu_buffer_rsrc_t rr = buf_rsrc(rp + sc.r0, (nrow + 1) * 8);
         int32_t ray[RPT];
-#pragma unroll
-        for (int i = 0; i < RPT; ++i)
-            ray[i] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ry, (threadIdx.x + i * FBS) * 4, 0, 0);
-        double qv[RPT];
-#pragma unroll
-        for (int i = 0; i < RPT; ++i) qv[i] = q[ray[i]];      // (ray 0 past nlr: a harmless read)
         uint32_t pk[RPT];
-#pragma unroll
-        for (int i = 0; i < RPT; ++i)
-            pk[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rk, (threadIdx.x + i * FBS) * 4, 0, 0);
-        const int rpv = (int)(__builtin_bit_cast(int64_t, __builtin_amdgcn_raw_buffer_load_b64(rr, threadIdx.x * 8, 0, 0)) -
-                              sc.e0);
+        int rpv;
         double v[VPT];
         uint16_t pv[VPT];
+        double qv[RPT];
+    };
+    auto issue = [&](int s, Batch& bt) {
+        const int4 w0 = reinterpret_cast<const int4*>(subs + s)[0];   // uniform: scalar loads
+        const int4 w1 = reinterpret_cast<const int4*>(subs + s)[1];
+        bt.sc.e0 = (int64_t)(uint32_t)w0.x | ((int64_t)w0.y << 32);
+        bt.sc.lr0 = (int64_t)(uint32_t)w0.z | ((int64_t)w0.w << 32);
+        bt.sc.r0 = w1.x;
+        bt.sc.len = (uint16_t)(w1.y & 0xffff);
+        bt.sc.nrow = (uint16_t)((uint32_t)w1.y >> 16);
+        bt.sc.nlr = (uint16_t)(w1.z & 0xffff);
+        const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + bt.sc.e0, bt.sc.len * 8);
+        const __amdgpu_buffer_rsrc_t rpm = buf_rsrc(perm + bt.sc.e0, bt.sc.len * 2);
+        const __amdgpu_buffer_rsrc_t rk = buf_rsrc(lr_pk + bt.sc.lr0, bt.sc.nlr * 4);
+        const __amdgpu_buffer_rsrc_t ry = buf_rsrc(lr_ray + bt.sc.lr0, bt.sc.nlr * 4);
+        const __amdgpu_buffer_rsrc_t rr = buf_rsrc(rp + bt.sc.r0, (bt.sc.nrow + 1) * 8);
+#pragma unroll
+        for (int i = 0; i < RPT; ++i)
+            bt.ray[i] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ry, (threadIdx.x + i * FBS) * 4, 0, 0);
+        asm volatile("" ::: "memory");                     // (issued before the rest of the batch)
+#pragma unroll
+        for (int i = 0; i < RPT; ++i)
+            bt.pk[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rk, (threadIdx.x + i * FBS) * 4, 0, 0);
+        bt.rpv = (int)(__builtin_bit_cast(int64_t, __builtin_amdgcn_raw_buffer_load_b64(rr, threadIdx.x * 8, 0, 0)) -
+                       bt.sc.e0);
 #pragma unroll
         for (int i = 0; i < VPT; ++i) {
             const int j = threadIdx.x + i * FBS;
-            v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, j * 8, 0, 2));
-            pv[i] = (uint16_t)__builtin_amdgcn_raw_buffer_load_b16(rpm, j * 2, 0, 2);
+            bt.v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, j * 8, 0, 2));
+            bt.pv[i] = (uint16_t)__builtin_amdgcn_raw_buffer_load_b16(rpm, j * 2, 0, 2);
         }
-        __syncthreads();                                   // the previous sub-chunk is done with the LDS
+    };
+    auto gather_q = [&](Batch& bt) {
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) bt.qv[i] = q[bt.ray[i]];     // (ray 0 past nlr: a harmless read)
+    };
+    // process(cur, nx, more): sub-chunk `cur`; with `more`, the q gathers of `nx` (whose batch is
+    // in flight) go out halfway through.  Two batches alternate roles (the loop is unrolled by
+    // two), so no register copy of an in-flight load forces a wait.
+    auto process = [&](Batch& cur, Batch& nx, bool more) {
+        const FusedSub sc = cur.sc;
+        const int len = sc.len, nrow = sc.nrow;
+        const double* v = cur.v;
+        const uint16_t* pv = cur.pv;
+        const uint32_t* pk = cur.pk;
+        const double* qv = cur.qv;
+        const int rpv = cur.rpv;
+        lds_sync();                                   // the previous sub-chunk is done with the LDS
 #pragma unroll
         for (int i = 0; i < VPT; ++i) sperm[threadIdx.x + i * FBS] = pv[i];
         if (threadIdx.x <= nrow) srp[threadIdx.x] = rpv;
-        __syncthreads();
+        lds_sync();
+        if (more) gather_q(nx);                           // s+1's ray ids are in by now
         // q of every local ray to each of its entries (pk: first position | length << 12 | rr << 20)
         if (!(dbg & 1)) {
 #pragma unroll
@@ -160,7 +188,7 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
                 for (int k = k0; k < k1; ++k) prod[sperm[k]] = qv[i];
             }
         }
-        __syncthreads();
+        lds_sync();
         if (!(dbg & 8)) {
 #pragma unroll
             for (int i = 0; i < VPT; ++i) {
@@ -168,7 +196,7 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
                 if (j < len) prod[j] = v[i] * prod[j];
             }
         }
-        __syncthreads();
+        lds_sync();
         // z_j = B(j,:) q: FGR lanes per row, strided partials, fixed tree
         if (!(dbg & 2)) {
             for (int ri = gid; ri < nrow; ri += FBS / FGR) {
@@ -185,7 +213,7 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
                 }
             }
         }
-        __syncthreads();
+        lds_sync();
         if (!(dbg & 8)) {
 #pragma unroll
             for (int i = 0; i < VPT; ++i) {
@@ -193,7 +221,7 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
                 if (j < len) prod[j] = v[i] * zrow[rowid[j]];
             }
         }
-        __syncthreads();
+        lds_sync();
         // each local ray's share, in position order, into the region accumulator
         if (!(dbg & 4)) {
 #pragma unroll
@@ -206,8 +234,32 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
                 }
             }
         }
+    };
+    Batch b0, b1;
+    if (s0 < s1) {
+        issue(s0, b0);
+        gather_q(b0);
     }
-    __syncthreads();
+    if constexpr (PF) {
+        for (int s = s0; s < s1; s += 2) {
+            const bool m1 = s + 1 < s1;
+            if (m1) issue(s + 1, b1);
+            process(b0, b1, m1);
+            if (!m1) break;
+            const bool m2 = s + 2 < s1;
+            if (m2) issue(s + 2, b0);
+            process(b1, b0, m2);
+        }
+    } else {
+        for (int s = s0; s < s1; ++s) {
+            if (s > s0) {
+                issue(s, b0);
+                gather_q(b0);
+            }
+            process(b0, b1, false);
+        }
+    }
+    lds_sync();
     for (int r = threadIdx.x; r < nr; r += FBS) part[pb + r] = acc[r];
 }
 
@@ -479,14 +531,14 @@ const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
 void fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq) {
     hipEvent_t t0 = nullptr;
     timing_begin(c, KC_FUSED, &t0);
-#define HGM_FUSED_LAUNCH(FB, FGV)                                                                               \
-    launch(c, false, k_fused_ab<FB, FGV>, dim3((unsigned)P->nreg), dim3(FB), (const FusedSub*)P->subs,           \
+#define HGM_FUSED_LAUNCH(FB, FGV, PFV)                                                                          \
+    launch(c, false, k_fused_ab<FB, FGV, PFV>, dim3((unsigned)P->nreg), dim3(FB), (const FusedSub*)P->subs,      \
            (const int32_t*)P->reg_sub, (const int64_t*)P->reg_base, (const uint16_t*)P->perm,                    \
            (const int32_t*)P->lr_ray, (const uint32_t*)P->lr_pk, (const int64_t*)B->rp, (const double*)B->val, q, \
            Bq, P->part, c->num.fused_dbg)
     // (one lane count per row sum for both sizes: the same summation order, the same bits)
-    if (c->num.fused_bs == 512) HGM_FUSED_LAUNCH(512, 16);
-    else HGM_FUSED_LAUNCH(1024, 16);
+    if (c->num.fused_bs == 512) { if (c->num.fused_pf) HGM_FUSED_LAUNCH(512, 16, true); else HGM_FUSED_LAUNCH(512, 16, false); }
+    else { if (c->num.fused_pf) HGM_FUSED_LAUNCH(1024, 16, true); else HGM_FUSED_LAUNCH(1024, 16, false); }
 #undef HGM_FUSED_LAUNCH
     launch(c, true, k_fused_reduce, dim3(grid_for(P->m)), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
            (const int32_t*)P->rs_slot, (const double*)P->part, ABq);

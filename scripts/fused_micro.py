@@ -30,7 +30,8 @@ P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
 two = 2 * 12.0 * A.nnz + 8.0 * (m + 1) + 8.0 * (n + 1) + 16.0 * (m + n)
 ref = None
 for vname in variants:
-    opts = {"two": dict(fused_ab=0), "f1024": dict(fused_ab=1, fused_bs=1024), "f512": dict(fused_ab=1, fused_bs=512)}
+    opts = {"two": dict(fused_ab=0), "f1024": dict(fused_ab=1, fused_bs=1024), "f512": dict(fused_ab=1, fused_bs=512),
+            "p1024": dict(fused_ab=1, fused_bs=1024, fused_pf=1), "p512": dict(fused_ab=1, fused_bs=512, fused_pf=1)}
     o = opts.get(vname, dict(fused_ab=1, fused_dbg=int(vname[1:]) if vname.startswith("d") else 0))
     with ctx.options(**o):
         lib.hgm_spmv_ab(ctx.handle, A._h, B._h, P(q), P(bq), P(abq))      # plan / warm-up
