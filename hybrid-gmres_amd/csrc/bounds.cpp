@@ -140,6 +140,7 @@ int gmres_bounds_filter(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const h
         double* tm = c->buf<double>("fb_t", std::max(A->rows, A->cols) + 1);
         double* nrm = c->buf<double>("fb_nrm", 2);
         HGM_HIP(hipMemsetAsync(Hd, 0, sizeof(double) * ((size_t)(p + 1) * p + 8), c->stream));
+        const FusedPlan* fplan = nspace ? nullptr : fused_ab_plan(c, A, B);
         const uint64_t seed = 0x5EEDB0A4D5ull;
         fill_hash<double>(c, dim, Qp, seed);
         normalize_to<double>(c, dim, Qp, nrm);
@@ -157,6 +158,8 @@ int gmres_bounds_filter(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const h
                 if (nspace) {                                    // M = B*A
                     spmv<double>(c, A, qj, tm, EPI_NONE, 0.0, nullptr, KC_SPMV_A);
                     spmv<double>(c, B, tm, v, EPI_NONE, 0.0, nullptr, KC_SPMV_B);
+                } else if (fplan) {                              // M = A*B, one pass over B
+                    fused_ab(c, B, fplan, qj, tm, v);
                 } else {                                         // M = A*B
                     spmv<double>(c, B, qj, tm, EPI_NONE, 0.0, nullptr, KC_SPMV_B);
                     spmv<double>(c, A, tm, v, EPI_NONE, 0.0, nullptr, KC_SPMV_A);

@@ -1229,6 +1229,8 @@ int arnoldi(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b_in, 
     div_scalar<T>(c, dim, Q, Q, beta);                                         // :15
     std::vector<double> H((size_t)(kg + 1) * kg, 0.0);
     int done = 0;
+    const FusedPlan* fplan = nullptr;                                          // A*(B*q) in one pass
+    if constexpr (std::is_same_v<T, double>) if (!nspace) fplan = fused_ab_plan(c, A, B);
     // The steps are enqueued back to back, with no host round trip per step: the breakdown
     // test H(k+1,k) < btol runs on the host afterwards, and the steps past a breakdown (which
     // wrote only Q(:,>k+1) and H(:,>k) on the device) are discarded.
@@ -1238,6 +1240,8 @@ int arnoldi(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b_in, 
         if (nspace) {
             apply_A<T>(c, A, qk, t, EPI_NONE, 0.0, nullptr);
             apply_B<T>(c, B, t, v, EPI_NONE, 0.0, nullptr);                    // :22 B*(A*Q(:,k))
+        } else if (fplan) {
+            if constexpr (std::is_same_v<T, double>) fused_ab(c, B, fplan, qk, tn, v);   // :20
         } else {
             apply_B<T>(c, B, qk, tn, EPI_NONE, 0.0, nullptr);
             apply_A<T>(c, A, tn, v, EPI_NONE, 0.0, nullptr);                   // :20 A*(B*Q(:,k))
