@@ -37,14 +37,18 @@ constexpr int FLRMAX = 768;    // distinct rays per sub-chunk (C4: <= ~700)
 constexpr int FROWS = 128;     // pixel rows per sub-chunk
 }  // namespace
 
+// A sub-chunk's entries sit at LDS positions ("coordinates") e - (e0 & ~1): the values are loaded
+// in 16-byte pairs aligned in memory, so with an odd e0 coordinate 0 is the previous sub-chunk's
+// last entry, loaded and never used.
 struct FusedSub {
     int64_t e0;        // first entry (B's CSR order)
     int64_t lr0;       // first local-ray record
     int32_t r0;        // first row
+    uint32_t p0q;      // perm of this sub-chunk at perm[4 * p0q] (padded to 4 entries: 8-byte loads)
     uint16_t len;      // entries
     uint16_t nrow;     // rows
     uint16_t nlr;      // local rays
-    uint16_t pad0, pad1, pad2;
+    uint16_t pad;
 };
 static_assert(sizeof(FusedSub) == 32, "FusedSub layout");
 
@@ -54,7 +58,7 @@ struct FusedPlan {
     int32_t* reg_sub = nullptr;   // nreg+1
     int64_t* reg_base = nullptr;  // nreg+1
     FusedSub* subs = nullptr;     // nsub
-    uint16_t* perm = nullptr;     // nnz
+    uint16_t* perm = nullptr;     // per sub-chunk: coordinate of its k-th entry in ray order
     int32_t* lr_ray = nullptr;    // nlr
     uint32_t* lr_pk = nullptr;    // nlr: first position | entries << 12 | region ray index << 20
     int64_t* rs_ptr = nullptr;    // m+1
@@ -101,15 +105,16 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
     const uint16_t* __restrict__ perm, const int32_t* __restrict__ lr_ray, const uint32_t* __restrict__ lr_pk,
     const int64_t* __restrict__ rp, const double* __restrict__ val, const double* __restrict__ q,
     double* __restrict__ z, double* __restrict__ part, int dbg) {
-    constexpr int VPT = FCH / FBS;                      // entries per thread
+    constexpr int VP = FCH / 2 / FBS;                   // value pairs per thread
+    constexpr int PQ = FCH / 4 / FBS;                   // perm quads per thread
     constexpr int RPT = (FLRMAX + FBS - 1) / FBS;       // local rays per thread
     static_assert(FBS > FROWS, "one row pointer per thread");
-    __shared__ double prod[FCH];
+    __shared__ __attribute__((aligned(16))) double prod[FCH];
     __shared__ double acc[FRMAX];
-    __shared__ uint16_t sperm[FCH];
+    __shared__ __attribute__((aligned(16))) uint16_t sperm[FCH];
     __shared__ int32_t srp[FROWS + 1];
     __shared__ double zrow[FROWS];
-    __shared__ uint8_t rowid[FCH];
+    __shared__ __attribute__((aligned(16))) uint8_t rowid[FCH];
     const int g = blockIdx.x;
     const int64_t pb = reg_base[g];
     const int nr = (int)(reg_base[g + 1] - pb);
@@ -125,8 +130,8 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
         int32_t ray[RPT];
         uint32_t pk[RPT];
         int rpv;
-        double v[VPT];
-        uint16_t pv[VPT];
+        double2 v[VP];
+        uint2 pq[PQ];
         double qv[RPT];
     };
     auto issue = [&](int s, Batch& bt) {
@@ -135,11 +140,15 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
         bt.sc.e0 = (int64_t)(uint32_t)w0.x | ((int64_t)w0.y << 32);
         bt.sc.lr0 = (int64_t)(uint32_t)w0.z | ((int64_t)w0.w << 32);
         bt.sc.r0 = w1.x;
-        bt.sc.len = (uint16_t)(w1.y & 0xffff);
-        bt.sc.nrow = (uint16_t)((uint32_t)w1.y >> 16);
-        bt.sc.nlr = (uint16_t)(w1.z & 0xffff);
-        const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + bt.sc.e0, bt.sc.len * 8);
-        const __amdgpu_buffer_rsrc_t rpm = buf_rsrc(perm + bt.sc.e0, bt.sc.len * 2);
+        bt.sc.p0q = (uint32_t)w1.y;
+        bt.sc.len = (uint16_t)(w1.z & 0xffff);
+        bt.sc.nrow = (uint16_t)((uint32_t)w1.z >> 16);
+        bt.sc.nlr = (uint16_t)(w1.w & 0xffff);
+        const int64_t ea = bt.sc.e0 & ~int64_t(1);
+        const int span = bt.sc.len + (int)(bt.sc.e0 & 1);   // coordinates in use
+        // (values: whole pairs, the last one may end one entry past nnz: the allocation is padded)
+        const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + ea, ((span + 1) & ~1) * 8);
+        const __amdgpu_buffer_rsrc_t rpm = buf_rsrc(perm + 4 * (int64_t)bt.sc.p0q, ((bt.sc.len + 3) & ~3) * 2);
         const __amdgpu_buffer_rsrc_t rk = buf_rsrc(lr_pk + bt.sc.lr0, bt.sc.nlr * 4);
         const __amdgpu_buffer_rsrc_t ry = buf_rsrc(lr_ray + bt.sc.lr0, bt.sc.nlr * 4);
         const __amdgpu_buffer_rsrc_t rr = buf_rsrc(rp + bt.sc.r0, (bt.sc.nrow + 1) * 8);
@@ -150,14 +159,13 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
 #pragma unroll
         for (int i = 0; i < RPT; ++i)
             bt.pk[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rk, (threadIdx.x + i * FBS) * 4, 0, 0);
-        bt.rpv = (int)(__builtin_bit_cast(int64_t, __builtin_amdgcn_raw_buffer_load_b64(rr, threadIdx.x * 8, 0, 0)) -
-                       bt.sc.e0);
+        bt.rpv = (int)(__builtin_bit_cast(int64_t, __builtin_amdgcn_raw_buffer_load_b64(rr, threadIdx.x * 8, 0, 0)) - ea);
 #pragma unroll
-        for (int i = 0; i < VPT; ++i) {
-            const int j = threadIdx.x + i * FBS;
-            bt.v[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, j * 8, 0, 2));
-            bt.pv[i] = (uint16_t)__builtin_amdgcn_raw_buffer_load_b16(rpm, j * 2, 0, 2);
-        }
+        for (int i = 0; i < VP; ++i)
+            bt.v[i] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, (threadIdx.x + i * FBS) * 16, 0, 2));
+#pragma unroll
+        for (int i = 0; i < PQ; ++i)
+            bt.pq[i] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rpm, (threadIdx.x + i * FBS) * 8, 0, 2));
     };
     auto gather_q = [&](Batch& bt) {
 #pragma unroll
@@ -168,15 +176,15 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
     // two), so no register copy of an in-flight load forces a wait.
     auto process = [&](Batch& cur, Batch& nx, bool more) {
         const FusedSub sc = cur.sc;
-        const int len = sc.len, nrow = sc.nrow;
-        const double* v = cur.v;
-        const uint16_t* pv = cur.pv;
+        const int span = sc.len + (int)(sc.e0 & 1), nrow = sc.nrow;
+        const double2* v = cur.v;
+        const uint2* pq = cur.pq;
         const uint32_t* pk = cur.pk;
         const double* qv = cur.qv;
         const int rpv = cur.rpv;
         lds_sync();                                   // the previous sub-chunk is done with the LDS
 #pragma unroll
-        for (int i = 0; i < VPT; ++i) sperm[threadIdx.x + i * FBS] = pv[i];
+        for (int i = 0; i < PQ; ++i) reinterpret_cast<uint2*>(sperm)[threadIdx.x + i * FBS] = pq[i];
         if (threadIdx.x <= nrow) srp[threadIdx.x] = rpv;
         lds_sync();
         if (more) gather_q(nx);                           // s+1's ray ids are in by now
@@ -185,15 +193,28 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
 #pragma unroll
             for (int i = 0; i < RPT; ++i) {
                 const int k0 = (int)(pk[i] & 0xfffu), k1 = k0 + (int)((pk[i] >> 12) & 0xffu);
-                for (int k = k0; k < k1; ++k) prod[sperm[k]] = qv[i];
+                int k = k0;
+                for (; k + 4 <= k1; k += 4) {              // (4 index reads in flight, then 4 stores)
+                    const int a0 = sperm[k], a1 = sperm[k + 1], a2 = sperm[k + 2], a3 = sperm[k + 3];
+                    prod[a0] = qv[i];
+                    prod[a1] = qv[i];
+                    prod[a2] = qv[i];
+                    prod[a3] = qv[i];
+                }
+                for (; k < k1; ++k) prod[sperm[k]] = qv[i];
             }
         }
         lds_sync();
         if (!(dbg & 8)) {
 #pragma unroll
-            for (int i = 0; i < VPT; ++i) {
-                const int j = threadIdx.x + i * FBS;
-                if (j < len) prod[j] = v[i] * prod[j];
+            for (int i = 0; i < VP; ++i) {
+                const int jp = threadIdx.x + i * FBS;
+                if (2 * jp < span) {
+                    double2 t = reinterpret_cast<double2*>(prod)[jp];
+                    t.x = v[i].x * t.x;
+                    t.y = v[i].y * t.y;
+                    reinterpret_cast<double2*>(prod)[jp] = t;
+                }
             }
         }
         lds_sync();
@@ -216,9 +237,15 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
         lds_sync();
         if (!(dbg & 8)) {
 #pragma unroll
-            for (int i = 0; i < VPT; ++i) {
-                const int j = threadIdx.x + i * FBS;
-                if (j < len) prod[j] = v[i] * zrow[rowid[j]];
+            for (int i = 0; i < VP; ++i) {
+                const int jp = threadIdx.x + i * FBS;
+                if (2 * jp < span) {   // (the row ids of unused coordinates are stale: masked)
+                    const uint32_t rid = reinterpret_cast<const uint16_t*>(rowid)[jp];
+                    double2 t;
+                    t.x = v[i].x * zrow[rid & (FROWS - 1)];
+                    t.y = v[i].y * zrow[(rid >> 8) & (FROWS - 1)];
+                    reinterpret_cast<double2*>(prod)[jp] = t;
+                }
             }
         }
         lds_sync();
@@ -229,7 +256,16 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
                 const int k0 = (int)(pk[i] & 0xfffu), k1 = k0 + (int)((pk[i] >> 12) & 0xffu);
                 if (k1 > k0) {
                     double t = 0.0;
-                    for (int k = k0; k < k1; ++k) t += prod[sperm[k]];
+                    int k = k0;
+                    for (; k + 4 <= k1; k += 4) {          // (loads batched, sums in position order)
+                        const int a0 = sperm[k], a1 = sperm[k + 1], a2 = sperm[k + 2], a3 = sperm[k + 3];
+                        const double p0 = prod[a0], p1 = prod[a1], p2 = prod[a2], p3 = prod[a3];
+                        t += p0;
+                        t += p1;
+                        t += p2;
+                        t += p3;
+                    }
+                    for (; k < k1; ++k) t += prod[sperm[k]];
                     acc[pk[i] >> 20] += t;
                 }
             }
@@ -270,7 +306,18 @@ __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* _
     for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < m; i += (int64_t)gridDim.x * BS) {
         double s = 0.0;
         const int64_t k0 = rs_ptr[i], k1 = rs_ptr[i + 1];
-        for (int64_t k = k0; k < k1; ++k) s += part[rs_slot[k]];
+        int64_t k = k0;
+        for (; k + 8 <= k1; k += 8) {   // 8 slot reads, then 8 partial reads in flight; sums in order
+            int32_t sl[8];
+            double p[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) sl[u] = rs_slot[k + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) p[u] = part[sl[u]];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += p[u];
+        }
+        for (; k < k1; ++k) s += part[rs_slot[k]];
         w[i] = s;
     }
 }
@@ -342,7 +389,8 @@ FusedPlan* fused_plan_build(hgm_ctx* c, const hgm_mat* B, int R) {
     std::vector<Sub> sv;
     for (int64_t s = 0; s < n;) {
         Sub u{rp[s], (int32_t)s, reg[s], 0, 0};
-        while (s < n && reg[s] == u.reg && u.nrow < FROWS && u.len + (rp[s + 1] - rp[s]) <= FCH) {
+        // (an odd first entry costs one coordinate: see FusedSub)
+        while (s < n && reg[s] == u.reg && u.nrow < FROWS && u.len + (rp[s + 1] - rp[s]) <= FCH - (u.e0 & 1)) {
             u.len += (int)(rp[s + 1] - rp[s]);
             ++u.nrow;
             ++s;
@@ -383,8 +431,12 @@ FusedPlan* fused_plan_build(hgm_ctx* c, const hgm_mat* B, int R) {
     std::vector<int32_t> reg_sub(nreg + 1, 0);
     for (const Sub& u : sv) reg_sub[u.reg + 1]++;
     for (int64_t g = 0; g < nreg; ++g) reg_sub[g + 1] += reg_sub[g];
-    // local CSC of every sub-chunk: perm (entries in ray order), distinct rays and their starts
-    std::vector<uint16_t> perm(std::max<int64_t>(nnz, 1));
+    // local CSC of every sub-chunk: perm (entry coordinates in ray order, each sub-chunk's run
+    // padded to 4 entries), distinct rays and their starts
+    std::vector<int64_t> pbase(nsub + 1, 0);
+    for (int64_t i = 0; i < nsub; ++i) pbase[i + 1] = pbase[i] + ((sv[i].len + 3) & ~3);
+    HGM_REQUIRE(pbase[nsub] / 4 < (int64_t(1) << 32), "fused A*(B*q): perm index range");
+    std::vector<uint16_t> perm(std::max<int64_t>(pbase[nsub], 1), 0);
     std::vector<std::vector<int32_t>> lray(nsub);
     std::vector<std::vector<uint16_t>> lpos(nsub);
     parallel_for(nsub, [&](int64_t i) {
@@ -396,7 +448,7 @@ FusedPlan* fused_plan_build(hgm_ctx* c, const hgm_mat* B, int R) {
         auto& lp = lpos[i];
         for (int k = 0; k < u.len; ++k) {
             const int32_t ray = (int32_t)(key[k] >> 16);
-            perm[u.e0 + k] = (uint16_t)(key[k] & 0xffffu);
+            perm[pbase[i] + k] = (uint16_t)((key[k] & 0xffffu) + (u.e0 & 1));
             if (k == 0 || ray != lr.back()) {
                 lr.push_back(ray);
                 lp.push_back((uint16_t)k);
@@ -431,8 +483,8 @@ FusedPlan* fused_plan_build(hgm_ctx* c, const hgm_mat* B, int R) {
     int64_t nlr = 0;
     for (int64_t i = 0; i < nsub; ++i) {
         HGM_REQUIRE(lray[i].size() <= 0xffff, "fused A*(B*q): local rays");
-        subs[i] = FusedSub{sv[i].e0, nlr, sv[i].r0, (uint16_t)sv[i].len, (uint16_t)sv[i].nrow,
-                           (uint16_t)lray[i].size(), 0, 0, 0};
+        subs[i] = FusedSub{sv[i].e0, nlr, sv[i].r0, (uint32_t)(pbase[i] / 4), (uint16_t)sv[i].len,
+                           (uint16_t)sv[i].nrow, (uint16_t)lray[i].size(), 0};
         nlr += (int64_t)lray[i].size();
     }
     // records: first position (12 bits) | entries (8) | region ray index (12); longest first, so

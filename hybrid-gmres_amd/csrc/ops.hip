@@ -26,7 +26,7 @@ hgm_mat* mat_alloc(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, int dtyp
     const size_t vs = dtype == HGM_F32 ? 4 : 8;
     if (hipMalloc(&M->rp, sizeof(int64_t) * (rows + 1)) != hipSuccess ||
         hipMalloc(&M->ci, sizeof(int32_t) * (nnz > 0 ? nnz : 1)) != hipSuccess ||
-        hipMalloc(&M->val, vs * (nnz > 0 ? nnz : 1)) != hipSuccess) {
+        hipMalloc(&M->val, vs * (nnz + 4)) != hipSuccess) {   // (+4: whole 16-byte loads at the end, fused.hip)
         mat_free(M);
         throw Error{HGM_E_NOMEM, "hipMalloc failed for sparse matrix"};
     }
