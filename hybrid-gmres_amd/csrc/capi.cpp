@@ -503,7 +503,7 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             if (!(v == 512 || v == 1024)) return bad("fused_bs is 512 or 1024");
             n.fused_bs = (int)v;
             break;
-        case HGM_OPT_FUSED_PF: if (!b01) return bad("fused_pf is 0 or 1"); n.fused_pf = v != 0; break;
+        case HGM_OPT_FUSED_PF: if (v < 0 || v > 4) return bad("fused_pf is 0..4"); n.fused_pf = v < 1 ? 1 : (int)v; break;
         case HGM_OPT_FUSED_DBG:
             if (!(v >= 0 && v <= 15 && v == std::floor(v))) return bad("fused_dbg is 0..15");
             n.fused_dbg = (int)v;

@@ -99,8 +99,11 @@ __device__ __forceinline__ void lds_sync() {
 // cost the registers two workgroups per CU need (4.39 ms, spilling at 1024 threads).
 // dbg (HGM_OPT_FUSED_DBG, timing experiments only; the results are then wrong): bit 1 skips the
 // q scatter, 2 the row sums, 4 the per-ray sums, 8 the two elementwise passes.
-template <int FBS, int FGR, bool PF>
-__global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 8))) void k_fused_ab(
+// D: sub-chunk batches in registers (1: no prefetch; D > 1: D - 1 batches in flight while one is
+// processed).  Two 1024-thread workgroups per CU leave 64 VGPRs a lane (D = 2); deeper pipelines
+// run one 1024- or two 512-thread workgroups per CU (128 VGPRs).
+template <int FBS, int FGR, int D>
+__global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(D <= 2 ? FBS / 128 : 4, 8))) void k_fused_ab(
     const FusedSub* __restrict__ subs, const int32_t* __restrict__ reg_sub, const int64_t* __restrict__ reg_base,
     const uint16_t* __restrict__ perm, const int32_t* __restrict__ lr_ray, const uint32_t* __restrict__ lr_pk,
     const int64_t* __restrict__ rp, const double* __restrict__ val, const double* __restrict__ q,
@@ -129,21 +132,25 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
         FusedSub sc;
         int32_t ray[RPT];
         uint32_t pk[RPT];
-        int rpv;
+        uint32_t rpv;       // low word of the row pointer (rp - first coordinate fits 32 bits)
         double2 v[VP];
         uint2 pq[PQ];
         double qv[RPT];
     };
-    auto issue = [&](int s, Batch& bt) {
+    // issue(s, bt, live): with !live an empty batch (the same loads against empty ranges: no
+    // memory traffic), so every iteration issues the same memory operations and the compiler's
+    // in-order vmcnt bookkeeping stays exact -- a conditional batch made it wait for everything.
+    auto issue = [&](int s, Batch& bt, bool live) {
+        s = live ? s : s0;
         const int4 w0 = reinterpret_cast<const int4*>(subs + s)[0];   // uniform: scalar loads
         const int4 w1 = reinterpret_cast<const int4*>(subs + s)[1];
         bt.sc.e0 = (int64_t)(uint32_t)w0.x | ((int64_t)w0.y << 32);
         bt.sc.lr0 = (int64_t)(uint32_t)w0.z | ((int64_t)w0.w << 32);
         bt.sc.r0 = w1.x;
         bt.sc.p0q = (uint32_t)w1.y;
-        bt.sc.len = (uint16_t)(w1.z & 0xffff);
-        bt.sc.nrow = (uint16_t)((uint32_t)w1.z >> 16);
-        bt.sc.nlr = (uint16_t)(w1.w & 0xffff);
+        bt.sc.len = live ? (uint16_t)(w1.z & 0xffff) : 0;
+        bt.sc.nrow = live ? (uint16_t)((uint32_t)w1.z >> 16) : 0;
+        bt.sc.nlr = live ? (uint16_t)(w1.w & 0xffff) : 0;
         const int64_t ea = bt.sc.e0 & ~int64_t(1);
         const int span = bt.sc.len + (int)(bt.sc.e0 & 1);   // coordinates in use
         // (values: whole pairs, the last one may end one entry past nnz: the allocation is padded)
@@ -159,7 +166,7 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
 #pragma unroll
         for (int i = 0; i < RPT; ++i)
             bt.pk[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rk, (threadIdx.x + i * FBS) * 4, 0, 0);
-        bt.rpv = (int)(__builtin_bit_cast(int64_t, __builtin_amdgcn_raw_buffer_load_b64(rr, threadIdx.x * 8, 0, 0)) - ea);
+        bt.rpv = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rr, threadIdx.x * 8, 0, 0);
 #pragma unroll
         for (int i = 0; i < VP; ++i)
             bt.v[i] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, (threadIdx.x + i * FBS) * 16, 0, 2));
@@ -181,7 +188,7 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
         const uint2* pq = cur.pq;
         const uint32_t* pk = cur.pk;
         const double* qv = cur.qv;
-        const int rpv = cur.rpv;
+        const int rpv = (int)(cur.rpv - (uint32_t)(sc.e0 & ~int64_t(1)));
         lds_sync();                                   // the previous sub-chunk is done with the LDS
 #pragma unroll
         for (int i = 0; i < PQ; ++i) reinterpret_cast<uint2*>(sperm)[threadIdx.x + i * FBS] = pq[i];
@@ -228,13 +235,14 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
                     rowid[j] = (uint8_t)ri;
                 }
                 t = group_sum<double, FGR>(t);
-                if (gl == 0) {
-                    zrow[ri] = t;
-                    z[sc.r0 + ri] = t;
-                }
+                if (gl == 0) zrow[ri] = t;
             }
         }
         lds_sync();
+        {   // z out: one store per thread, the rows past nrow fall outside the range and are dropped
+            const __amdgpu_buffer_rsrc_t rz = buf_rsrc(z + sc.r0, nrow * 8);
+            buf_store(zrow[threadIdx.x & (FROWS - 1)], rz, threadIdx.x * 8);
+        }
         if (!(dbg & 8)) {
 #pragma unroll
             for (int i = 0; i < VP; ++i) {
@@ -271,28 +279,30 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(FBS / 128, 
             }
         }
     };
-    Batch b0, b1;
-    if (s0 < s1) {
-        issue(s0, b0);
-        gather_q(b0);
-    }
-    if constexpr (PF) {
-        for (int s = s0; s < s1; s += 2) {
-            const bool m1 = s + 1 < s1;
-            if (m1) issue(s + 1, b1);
-            process(b0, b1, m1);
-            if (!m1) break;
-            const bool m2 = s + 2 < s1;
-            if (m2) issue(s + 2, b0);
-            process(b1, b0, m2);
+    Batch b[D > 1 ? D : 2];
+    if constexpr (D > 1) {
+        // b[u] is processed while b[u+1 .. u+D-1] are in flight; the loop is unrolled by D so every
+        // batch index is static (registers) and no register copy of an in-flight load forces a wait
+#pragma unroll
+        for (int i = 0; i < D - 1; ++i) issue(s0 + i, b[i], s0 + i < s1);
+        gather_q(b[0]);
+        for (int s = s0; s < s1; s += D) {
+#pragma unroll
+            for (int u = 0; u < D; ++u) {
+                if (u > 0 && s + u >= s1) break;
+                issue(s + u + D - 1, b[(u + D - 1) % D], s + u + D - 1 < s1);
+                process(b[u], b[(u + 1) % D], true);
+            }
         }
     } else {
+        issue(s0, b[0], s0 < s1);
+        gather_q(b[0]);
         for (int s = s0; s < s1; ++s) {
             if (s > s0) {
-                issue(s, b0);
-                gather_q(b0);
+                issue(s, b[0], true);
+                gather_q(b[0]);
             }
-            process(b0, b1, false);
+            process(b[0], b[1], false);
         }
     }
     lds_sync();
@@ -588,9 +598,19 @@ void fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q,
            (const int32_t*)P->reg_sub, (const int64_t*)P->reg_base, (const uint16_t*)P->perm,                    \
            (const int32_t*)P->lr_ray, (const uint32_t*)P->lr_pk, (const int64_t*)B->rp, (const double*)B->val, q, \
            Bq, P->part, c->num.fused_dbg)
-    // (one lane count per row sum for both sizes: the same summation order, the same bits)
-    if (c->num.fused_bs == 512) { if (c->num.fused_pf) HGM_FUSED_LAUNCH(512, 16, true); else HGM_FUSED_LAUNCH(512, 16, false); }
-    else { if (c->num.fused_pf) HGM_FUSED_LAUNCH(1024, 16, true); else HGM_FUSED_LAUNCH(1024, 16, false); }
+    // (one lane count per row sum for every variant: the same summation order, the same bits)
+    const int d = c->num.fused_pf;
+    if (c->num.fused_bs == 512) {
+        if (d <= 1) HGM_FUSED_LAUNCH(512, 16, 1);
+        else if (d == 2) HGM_FUSED_LAUNCH(512, 16, 2);
+        else if (d == 3) HGM_FUSED_LAUNCH(512, 16, 3);
+        else HGM_FUSED_LAUNCH(512, 16, 4);
+    } else {
+        if (d <= 1) HGM_FUSED_LAUNCH(1024, 16, 1);
+        else if (d == 2) HGM_FUSED_LAUNCH(1024, 16, 2);
+        else if (d == 3) HGM_FUSED_LAUNCH(1024, 16, 3);
+        else HGM_FUSED_LAUNCH(1024, 16, 4);
+    }
 #undef HGM_FUSED_LAUNCH
     launch(c, true, k_fused_reduce, dim3(grid_for(P->m)), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
            (const int32_t*)P->rs_slot, (const double*)P->part, ABq);

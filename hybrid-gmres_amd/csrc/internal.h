@@ -80,7 +80,7 @@ struct Numerics {
     bool fused_ab = true;           // m-space operator A*(B*q) in one pass over B (fused.hip)
     int fused_region = 64;          // ... pixel square per workgroup (its rays accumulate in LDS)
     int fused_bs = 1024;            // ... threads per workgroup (512, 1024)
-    bool fused_pf = true;           // ... next sub-chunk's loads issued during the current one
+    int fused_pf = 2;               // ... sub-chunk batches in registers (pipeline depth 1..4)
     int fused_dbg = 0;              // ... timing experiments: skip phases (wrong results)
 };
 struct FusedPlan;

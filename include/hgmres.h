@@ -128,7 +128,8 @@ enum hgm_ctx_option {
     HGM_OPT_FUSED_REGION = 19,     /* ... pixel square (side) per workgroup of that pass [64] */
     HGM_OPT_FUSED_BS = 20,         /* ... threads per workgroup: 512 or 1024 [1024] (same summation order) */
     HGM_OPT_FUSED_DBG = 21,        /* ... timing experiments only: bits skip its phases, results WRONG [0] */
-    HGM_OPT_FUSED_PF = 22          /* ... the next sub-chunk's loads issued during the current one [1] */
+    HGM_OPT_FUSED_PF = 22          /* ... pipeline depth: sub-chunk batches in registers, 1..4
+                                      (0 = 1: no prefetch) [2] */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for

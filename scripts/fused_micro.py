@@ -4,6 +4,7 @@ results wrong, timing only).  Prints one JSON line per variant.  Run on the GPU 
     python scripts/fused_micro.py [N angles reps]"""
 import ctypes as C
 import json
+import re
 import os
 import sys
 import time
@@ -30,9 +31,16 @@ P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
 two = 2 * 12.0 * A.nnz + 8.0 * (m + 1) + 8.0 * (n + 1) + 16.0 * (m + n)
 ref = None
 for vname in variants:
-    opts = {"two": dict(fused_ab=0), "f1024": dict(fused_ab=1, fused_bs=1024), "f512": dict(fused_ab=1, fused_bs=512),
-            "p1024": dict(fused_ab=1, fused_bs=1024, fused_pf=1), "p512": dict(fused_ab=1, fused_bs=512, fused_pf=1)}
-    o = opts.get(vname, dict(fused_ab=1, fused_dbg=int(vname[1:]) if vname.startswith("d") else 0))
+    # two | f<threads>[x<depth>][r<region>] (fused, pipeline depth [2], region side [64])
+    # | d<bits> (phase-skip timing)
+    mf = re.fullmatch(r"f(\d+)(?:x(\d))?(?:r(\d+))?", vname)
+    if vname == "two":
+        o = dict(fused_ab=0)
+    elif mf:
+        o = dict(fused_ab=1, fused_bs=int(mf.group(1)), fused_pf=int(mf.group(2) or 2),
+                 fused_region=int(mf.group(3) or 64))
+    else:
+        o = dict(fused_ab=1, fused_dbg=int(vname[1:]))
     with ctx.options(**o):
         lib.hgm_spmv_ab(ctx.handle, A._h, B._h, P(q), P(bq), P(abq))      # plan / warm-up
         ctx.synchronize()
