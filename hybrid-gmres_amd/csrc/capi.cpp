@@ -504,6 +504,7 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             n.fused_bs = (int)v;
             break;
         case HGM_OPT_FUSED_PF: if (v < 0 || v > 4) return bad("fused_pf is 0..4"); n.fused_pf = v < 1 ? 1 : (int)v; break;
+        case HGM_OPT_KRYLOV_PAD: if (v < -1 || v > 65536 || v != (double)(int64_t)v || (v > 0 && (int64_t)v % 64)) return bad("krylov_pad is -1 or a multiple of 64 in 0..65536"); n.krylov_pad = (int)v; break;
         case HGM_OPT_FUSED_DBG:
             if (!(v >= 0 && v <= 15 && v == std::floor(v))) return bad("fused_dbg is 0..15");
             n.fused_dbg = (int)v;
@@ -539,6 +540,7 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_FUSED_BS: *v = n.fused_bs; break;
         case HGM_OPT_FUSED_DBG: *v = n.fused_dbg; break;
         case HGM_OPT_FUSED_PF: *v = n.fused_pf; break;
+        case HGM_OPT_KRYLOV_PAD: *v = n.krylov_pad; break;
         default: return HGM_E_ARG;
     }
     return HGM_OK;

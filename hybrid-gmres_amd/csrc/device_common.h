@@ -205,6 +205,14 @@ template <> __device__ __forceinline__ double buf_load<double>(__amdgpu_buffer_r
 template <> __device__ __forceinline__ float buf_load<float>(__amdgpu_buffer_rsrc_t r, int off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
+// a pair (double2 / float2) through a buffer resource
+template <typename T2> __device__ __forceinline__ T2 buf_load2(__amdgpu_buffer_rsrc_t r, int off);
+template <> __device__ __forceinline__ double2 buf_load2<double2>(__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+template <> __device__ __forceinline__ float2 buf_load2<float2>(__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
 __device__ __forceinline__ void buf_store(double x, __amdgpu_buffer_rsrc_t r, int off) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), x),
                                           r, off, 0, 0);

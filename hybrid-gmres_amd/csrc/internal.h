@@ -81,6 +81,7 @@ struct Numerics {
     int fused_region = 64;          // ... pixel square per workgroup (its rays accumulate in LDS)
     int fused_bs = 1024;            // ... threads per workgroup (512, 1024)
     int fused_pf = 2;               // ... sub-chunk batches in registers (pipeline depth 1..4)
+    int krylov_pad = -1;            // Krylov basis column padding (elements; -1 auto, kernels.hip krylov_ld)
     int fused_dbg = 0;              // ... timing experiments: skip phases (wrong results)
 };
 struct FusedPlan;

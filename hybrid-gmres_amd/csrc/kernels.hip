@@ -629,7 +629,11 @@ static bool mgs_single_on(const hgm_ctx* c) { return c->num.mgs_single && !c->nu
 int64_t krylov_ld(const hgm_ctx* c, int64_t dim, bool dist) {
     dim = dim > 0 ? dim : 1;
     if (!dist && dim <= MGS1_MAX && mgs_single_on(c)) return (dim + 4 * MGS1_BS - 1) / (4 * MGS1_BS) * (4 * MGS1_BS);
-    return (dim + 63) / 64 * 64;
+    const int64_t ld = (dim + 63) / 64 * 64;
+    // a column stride that is a multiple of 32 KiB (C3: 2048^2 pixels, 32 MiB) puts element i of
+    // every column in the same HBM channel: the sweeps read k+2 columns at the same i at once
+    const int pad = c->num.krylov_pad < 0 ? 0 : c->num.krylov_pad;   // (auto: none)
+    return ld % 4096 == 0 ? ld + pad : ld;
 }
 
 bool krylov_padded(const hgm_ctx* c, int64_t ldq) {
@@ -677,7 +681,6 @@ static bool mgs_single(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol
 // Multi-GPU: the 2k+1 sums are one all-reduce (the pass form needs k+1 all-reduces per
 // step) between the two halves of k_mgs1_solve.
 // ------------------------------------------------------------------------------
-constexpr int MGS1_CG = 8;       // basis columns per workgroup of the dots pass
 constexpr int MGS1_MAXC = 120;   // k+1 <= 120: the Gram triangle fits 57 KiB of LDS
 
 // HGM_OPT_MGS_FORM: 1 = one-reduction (default), 0 = one launch per pass
@@ -729,100 +732,126 @@ __device__ __forceinline__ void mgs1_substitute(int kk, const T* sr, const T* sG
 
 // hpend (pending normalisation, internal.h PendNorm): Q(:,k) still holds v_k; every block
 // uses q_k = v_k / *hpend (k_mgs1_update writes q_k back once this kernel is done).
+// Tiles of BS*P element pairs per block (block b: tiles b, b + npr, ...).  A tile's w and q_k
+// stay in registers while its columns stream past two at a time, so w and q_k are read once per
+// step (the column-group form read them once per 8 columns) and a block streams two columns at a
+// time.  Per column the tile's partial dot products are wave-summed (DPP, fixed order) and added
+// into the block's LDS accumulators in tile order: fixed order, bitwise reproducible.
 template <typename T>
-__global__ __launch_bounds__(BS) void k_mgs1_dots(int64_t n, const T* Q, int64_t ldq, int kk,
-                                                  const T* __restrict__ w, int npr, T* __restrict__ pr,
-                                                  T* __restrict__ pg, MdotStage<T> side, const T* hpend,
-                                                  const T* __restrict__ xe) {
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_mgs1_dots(
+    int64_t n, const T* Q, int64_t ldq, int kk, const T* __restrict__ w, int npr, T* __restrict__ pr,
+    T* __restrict__ pg, MdotStage<T> side, const T* hpend, const T* __restrict__ xe) {
     using T2 = typename V2<T>::t;
-    __shared__ T sh[4][2 * MGS1_CG + 1];
-    const int ncg = (kk + MGS1_CG) / MGS1_CG;   // ceil((kk+1) / CG)
+    constexpr int P = 4, NW = BS / 64;
+    // acc[row][wave]: rows 0..kk = q_c'w, kk+1.. = q_c'q_k (c < kk; with xe also c = kk, then
+    // q_k'x_true)
+    __shared__ T acc[2 * MGS1_MAXC + 2][NW];
     const int b = (int)blockIdx.x;
-    if (b >= npr * ncg) {   // extra workgroups: the side job
-        mdot_side(side, b - npr * ncg, &sh[0][0]);
+    if (b >= npr) {   // extra workgroups: the side job
+        mdot_side(side, b - npr, &acc[0][0]);
         return;
     }
-    const int g = b / npr, rb = b - g * npr;
-    const int c0 = g * MGS1_CG;
-    const int nc = min(MGS1_CG, kk + 1 - c0);
-    const int64_t n2 = n >> 1, stride = (int64_t)npr * BS;
-    const T2* w2 = reinterpret_cast<const T2*>(w);
-    const T2* qk2 = reinterpret_cast<const T2*>(Q + (int64_t)kk * ldq);
-    const T* qc = Q + (int64_t)c0 * ldq;
-    // Gram error monitor (xe = x_true): the group holding column kk also sums q_kk'x_true
-    // (to pg row kk+1); its ag[kk - c0] = q_kk'q_kk goes to pg row kk
-    const bool gx = xe != nullptr && g == ncg - 1;
-    const T2* xe2 = reinterpret_cast<const T2*>(xe);
-    T ax = 0;
+    const bool gx = xe != nullptr;
+    const int nrow = 2 * kk + 1 + (gx ? 2 : 0);
+    const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
+    for (int r = t; r < nrow * NW; r += BS) (&acc[0][0])[(r / NW) * NW + r % NW] = T(0);
+    __syncthreads();
     const T hp = hpend ? *hpend : T(0);
     auto scale = [&](T v) -> T { return hp != T(0) ? v / hp : v; };   // as k_mgs_normalize
-    T ar[MGS1_CG], ag[MGS1_CG];
+    const int64_t n2 = n >> 1, tp = (int64_t)BS * P, ntile = (n2 + tp - 1) / tp, ld2 = ldq >> 1;
+    auto add = [&](int row, T v) {              // one wave's share of a tile's partial
+        const T sv = wave_sum_dpp(v);
+        if (lane == 0) acc[row][wv] += sv;
+    };
+    for (int64_t tl = b; tl < ntile; tl += npr) {
+        const int lim = (int)min<int64_t>(tp, n2 - tl * tp);
+        int ix[P];
+        bool ok[P];
 #pragma unroll
-    for (int c = 0; c < MGS1_CG; ++c) ar[c] = ag[c] = T(0);
-    for (int64_t i = (int64_t)rb * BS + threadIdx.x; i < n2; i += stride) {
-        const T2 ww = w2[i];
-        T2 qk = qk2[i];
-        if (hpend) {
-            qk.x = scale(qk.x);
-            qk.y = scale(qk.y);
+        for (int p = 0; p < P; ++p) {
+            const int e = t + p * BS;
+            ok[p] = e < lim;
+            ix[p] = ok[p] ? e : lim - 1;
         }
-        T2 q[MGS1_CG];
+        const T2* wt = reinterpret_cast<const T2*>(w) + tl * tp;
+        const T2* qt = reinterpret_cast<const T2*>(Q) + tl * tp;
+        T2 ww[P], qk[P];
 #pragma unroll
-        for (int c = 0; c < MGS1_CG; ++c)
-            if (c < nc) q[c] = (hpend && c0 + c == kk) ? qk : reinterpret_cast<const T2*>(qc + (int64_t)c * ldq)[i];
-#pragma unroll
-        for (int c = 0; c < MGS1_CG; ++c)
-            if (c < nc) {
-                ar[c] = __builtin_fma(q[c].y, ww.y, __builtin_fma(q[c].x, ww.x, ar[c]));
-                ag[c] = __builtin_fma(q[c].y, qk.y, __builtin_fma(q[c].x, qk.x, ag[c]));
+        for (int p = 0; p < P; ++p) {
+            ww[p] = ok[p] ? wt[ix[p]] : T2{0, 0};
+            qk[p] = qt[(int64_t)kk * ld2 + ix[p]];
+            if (hpend) {
+                qk[p].x = scale(qk[p].x);
+                qk[p].y = scale(qk[p].y);
             }
-        if (gx) {
-            const T2 xx = xe2[i];
-            ax = __builtin_fma(qk.y, xx.y, __builtin_fma(qk.x, xx.x, ax));
+            if (!ok[p]) qk[p] = T2{0, 0};
+        }
+        auto col = [&](const T2 (&q)[P], int c) {
+            T a = 0, g = 0;
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                a = __builtin_fma(q[p].y, ww[p].y, __builtin_fma(q[p].x, ww[p].x, a));
+                g = __builtin_fma(q[p].y, qk[p].y, __builtin_fma(q[p].x, qk[p].x, g));
+            }
+            add(c, a);
+            if (c < kk || gx) add(kk + 1 + c, g);
+        };
+        auto load = [&](int c, T2 (&q)[P]) {
+            if (hpend && c == kk) {
+#pragma unroll
+                for (int p = 0; p < P; ++p) q[p] = qk[p];
+                return;
+            }
+            const __amdgpu_buffer_rsrc_t rc = buf_rsrc(qt + (int64_t)c * ld2, lim * (int)sizeof(T2));
+#pragma unroll
+            for (int p = 0; p < P; ++p) q[p] = buf_load2<T2>(rc, (ok[p] ? ix[p] : lim) * (int)sizeof(T2));
+        };
+        int c = 0;
+#pragma unroll 1
+        for (; c + 2 <= kk + 1; c += 2) {
+            T2 qa[P], qb[P];
+            load(c, qa);
+            load(c + 1, qb);
+            col(qa, c);
+            col(qb, c + 1);
+        }
+        if (c <= kk) {
+            T2 qa[P];
+            load(c, qa);
+            col(qa, c);
+        }
+        if (gx) {                                 // q_k'x_true
+            const T2* xt = reinterpret_cast<const T2*>(xe) + tl * tp;
+            T a = 0;
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                const T2 xx = ok[p] ? xt[ix[p]] : T2{0, 0};
+                a = __builtin_fma(qk[p].y, xx.y, __builtin_fma(qk[p].x, xx.x, a));
+            }
+            add(2 * kk + 2, a);
         }
     }
-    if ((n & 1) && rb == npr - 1 && threadIdx.x == 0) {
+    __syncthreads();
+    if ((n & 1) && b == npr - 1 && t == 0) {      // the odd last element, into wave 0's share
         const int64_t i = n - 1;
         const T wi = w[i];
         const T qki = hpend ? scale(Q[(int64_t)kk * ldq + i]) : Q[(int64_t)kk * ldq + i];
-#pragma unroll
-        for (int c = 0; c < MGS1_CG; ++c)
-            if (c < nc) {
-                const T qi = (hpend && c0 + c == kk) ? qki : qc[(int64_t)c * ldq + i];
-                ar[c] = __builtin_fma(qi, wi, ar[c]);
-                ag[c] = __builtin_fma(qi, qki, ag[c]);
-            }
-        if (gx) ax = __builtin_fma(qki, xe[i], ax);
-    }
-    const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
-#pragma unroll
-    for (int c = 0; c < MGS1_CG; ++c)
-        if (c < nc) {
-            const T a = wave_sum_dpp(ar[c]);
-            const T e = wave_sum_dpp(ag[c]);
-            if (lane == 0) {
-                sh[wv][c] = a;
-                sh[wv][MGS1_CG + c] = e;
-            }
+        for (int c2 = 0; c2 <= kk; ++c2) {
+            const T qi = (hpend && c2 == kk) ? qki : Q[(int64_t)c2 * ldq + i];
+            acc[c2][0] = __builtin_fma(qi, wi, acc[c2][0]);
+            if (c2 < kk || gx) acc[kk + 1 + c2][0] = __builtin_fma(qi, qki, acc[kk + 1 + c2][0]);
         }
-    if (gx) {
-        const T a = wave_sum_dpp(ax);
-        if (lane == 0) sh[wv][2 * MGS1_CG] = a;
+        if (gx) acc[2 * kk + 2][0] = __builtin_fma(qki, xe[i], acc[2 * kk + 2][0]);
     }
     __syncthreads();
-    // rows of the group: 0..7 = r_{c0+row}, 8..15 = g_{c0+row-8} (g exists for columns < k)
-    // (with xe also g_kk = q_kk'q_kk, and row 16 = q_kk'x_true to pg row kk+1)
-    auto row_ok = [&](int row) {
-        if (row == 2 * MGS1_CG) return gx;
-        return row < MGS1_CG
-                   ? row < nc
-                   : (row - MGS1_CG < nc && (c0 + row - MGS1_CG < kk || (gx && c0 + row - MGS1_CG == kk)));
-    };
-    auto row_ptr = [&](int row) -> T* {
-        if (row == 2 * MGS1_CG) return pg + (int64_t)(kk + 1) * npr;
-        return row < MGS1_CG ? pr + (int64_t)(c0 + row) * npr : pg + (int64_t)(c0 + row - MGS1_CG) * npr;
-    };
-    if (t <= 2 * MGS1_CG && row_ok(t)) row_ptr(t)[rb] = (sh[0][t] + sh[1][t]) + (sh[2][t] + sh[3][t]);
+    // rows 0..kk -> pr rows; Gram rows kk+1+c -> pg row c (c = kk: q_k'q_k, c = kk+1: q_k'x_true)
+    for (int r = t; r < nrow; r += BS) {
+        T v = acc[r][0];
+#pragma unroll
+        for (int q = 1; q < NW; ++q) v += acc[r][q];
+        if (r <= kk) pr[(int64_t)r * npr + b] = v;
+        else pg[(int64_t)(r - kk - 1) * npr + b] = v;
+    }
 }
 
 // The partial rows of k_mgs1_dots reduced exactly as k_mgs1_solve reduces them (16 lanes per
@@ -906,7 +935,8 @@ __global__ __launch_bounds__(MGS1_SBS) void k_mgs1_solve(int kk, const T* __rest
 template <typename T, bool FUSED>
 // hpend: Q(:,k) still holds v_k (pending normalisation): q_k = v_k / *hpend is used for the
 // last term and written back (each element by the one thread that updates it).
-__global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, T* Q, int64_t ldq, int kk,
+// (4 waves per SIMD: the 1024-block cap is resident at once)
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_mgs1_update(int64_t n, int nb, T* Q, int64_t ldq, int kk,
                                                     const T* w, T* v, const T* __restrict__ hdev, T* Hcol,
                                                     T* __restrict__ pout, MdotStage<T> side, const T* hpend,
                                                     const T* __restrict__ grow, const T* __restrict__ gx, T* qg,
@@ -969,39 +999,79 @@ __global__ __launch_bounds__(BS) void k_mgs1_update(int64_t n, int nb, T* Q, int
     const int jn = hpend ? kk : kk + 1;                               // columns read as stored
     T2* qk2 = reinterpret_cast<T2*>(Q + (int64_t)kk * ldq);
     T acc0 = 0, acc1 = 0;
-    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n2; i += stride) {
-        T2 vv = w2[i];
-        T2 qkk{0, 0};
-        if (hpend) {
-            qkk = qk2[i];
-            qkk.x = scale(qkk.x);
-            qkk.y = scale(qkk.y);
-            qk2[i] = qkk;
+    // Tiles of BS*P element pairs per block, swept column by column (CW columns' loads in flight
+    // at a time): a block streams a few columns at a time instead of touching all k+3 vectors
+    // per element (C3 at k = 19: 4.6 TB/s that way, against 6 TB/s at k = 5).  Every element's
+    // subtraction order is MGS's, j = 0..k.
+    constexpr int P = 4, CW = 4;
+    const int64_t tp = (int64_t)BS * P, ntile = (n2 + tp - 1) / tp;
+    (void)stride;
+    for (int64_t tl = blockIdx.x; tl < ntile; tl += nb) {
+        const T2* wt = w2 + tl * tp;
+        const int lim = (int)min<int64_t>(tp, n2 - tl * tp);   // pairs in this tile
+        int ix[P];
+        T2 vv[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const int e = (int)threadIdx.x + p * BS;
+            ix[p] = e < lim ? e : lim - 1;            // (past the end: a repeated load, not stored)
+            vv[p] = wt[ix[p]];
         }
-        const T* q = Q;
-        int j = 0;
-        for (; j + 4 <= jn; j += 4, q += 4 * ldq) {
-            T2 qq[4];
+        auto sub = [&](const T2* qq, T h) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) qq[u] = reinterpret_cast<const T2*>(q + (int64_t)u * ldq)[i];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const T h = hs[j + u];
-                const T p0 = h * qq[u].x, p1 = h * qq[u].y;
-                vv.x = vv.x - p0;
-                vv.y = vv.y - p1;
+            for (int p = 0; p < P; ++p) {
+                const T p0 = h * qq[p].x, p1 = h * qq[p].y;
+                vv[p].x = vv[p].x - p0;
+                vv[p].y = vv[p].y - p1;
             }
+        };
+        // (buffer loads: one 32-bit offset per pair serves every column, a scalar base per column)
+        const T2* qt = reinterpret_cast<const T2*>(Q) + tl * tp;
+        const int64_t ld2 = ldq >> 1;                 // (ldq is even: a multiple of 64)
+        auto col = [&](int jj) { return buf_rsrc(qt + (int64_t)jj * ld2, lim * (int)sizeof(T2)); };
+        int j = 0;
+#pragma unroll 1
+        for (; j + CW <= jn; j += CW) {
+            T2 r[CW][P];
+#pragma unroll
+            for (int c = 0; c < CW; ++c) {
+                const __amdgpu_buffer_rsrc_t rc = col(j + c);
+#pragma unroll
+                for (int p = 0; p < P; ++p) r[c][p] = buf_load2<T2>(rc, ix[p] * (int)sizeof(T2));
+            }
+#pragma unroll
+            for (int c = 0; c < CW; ++c) sub(r[c], hs[j + c]);
         }
-        for (; j <= kk; ++j, q += ldq) {
-            const T2 qq = (j == kk && hpend) ? qkk : reinterpret_cast<const T2*>(q)[i];
-            const T h = hs[j];
-            const T p0 = h * qq.x, p1 = h * qq.y;
-            vv.x = vv.x - p0;
-            vv.y = vv.y - p1;
+#pragma unroll 1
+        for (; j < jn; ++j) {
+            T2 r[P];
+            const __amdgpu_buffer_rsrc_t rc = col(j);
+#pragma unroll
+            for (int p = 0; p < P; ++p) r[p] = buf_load2<T2>(rc, ix[p] * (int)sizeof(T2));
+            sub(r, hs[j]);
         }
-        v2[i] = vv;
-        acc0 += vv.x * vv.x;
-        acc1 += vv.y * vv.y;
+        if (hpend) {                                  // q_k = v_k / H(k,k-1), written back
+            T2* qkt = qk2 + tl * tp;
+            T2 r[P];
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                r[p] = qkt[ix[p]];
+                r[p].x = scale(r[p].x);
+                r[p].y = scale(r[p].y);
+            }
+#pragma unroll
+            for (int p = 0; p < P; ++p)
+                if ((int)threadIdx.x + p * BS < lim) qkt[ix[p]] = r[p];
+            sub(r, hs[kk]);
+        }
+        T2* vt = v2 + tl * tp;
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+            if ((int)threadIdx.x + p * BS < lim) {
+                vt[ix[p]] = vv[p];
+                acc0 += vv[p].x * vv[p].x;
+                acc1 += vv[p].y * vv[p].y;
+            }
     }
     if ((n & 1) && (int)blockIdx.x == nb - 1 && threadIdx.x == 0) {
         const int64_t i = n - 1;
@@ -1104,14 +1174,13 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
         }
         hipStream_t st = c->stream;
         const int npr = gemv_blocks(n, mgs1_ppl(c));
-        const int ncg = (kk + MGS1_CG) / MGS1_CG;
         T* pr = c->buf<T>("mgs1_pr", (size_t)MGS1_MAXC * MAX_PARTS);
         T* pg = c->buf<T>("mgs1_pg", (size_t)(MGS1_MAXC + 2) * MAX_PARTS);
         T* gx = xe ? c->buf<T>("mgs1_gx", 2) : nullptr;
         T* Gt = c->buf<T>("mgs1_G", (size_t)MGS1_MAXC * MGS1_MAXC / 2 + MGS1_MAXC);
         T* hdev = c->buf<T>("mgs1_h", MGS1_MAXC + 2);
         const size_t lds = sizeof(T) * ((size_t)kk * (kk + 1) / 2 + 1);
-        k_mgs1_dots<T><<<npr * ncg + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1, pend_h, xe);
+        k_mgs1_dots<T><<<npr + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1, pend_h, xe);
         const int nb = gemv_blocks(n, mgs_ppl(c));
         T* pout = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
         const bool fused = !dist && c->num.mgs_fused;

@@ -128,8 +128,11 @@ enum hgm_ctx_option {
     HGM_OPT_FUSED_REGION = 19,     /* ... pixel square (side) per workgroup of that pass [64] */
     HGM_OPT_FUSED_BS = 20,         /* ... threads per workgroup: 512 or 1024 [1024] (same summation order) */
     HGM_OPT_FUSED_DBG = 21,        /* ... timing experiments only: bits skip its phases, results WRONG [0] */
-    HGM_OPT_FUSED_PF = 22          /* ... pipeline depth: sub-chunk batches in registers, 1..4
+    HGM_OPT_FUSED_PF = 22,         /* ... pipeline depth: sub-chunk batches in registers, 1..4
                                       (0 = 1: no prefetch) [2] */
+    HGM_OPT_KRYLOV_PAD = 23        /* elements added to the Krylov basis' leading dimension when it
+                                      is a multiple of 4096 (a power-of-two column stride sends
+                                      every column's element i to the same HBM channel) [-1 = auto] */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for

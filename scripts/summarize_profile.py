@@ -15,6 +15,7 @@ dispatches in stream order —
   * streaming   k_spmv_stream (+ k_stream_fixup) (+ k_band_reduce): A if the group ends
     with the band reduction (only long-row operators are banded), else B;
   * banded      k_spmv_band + k_band_reduce: A.
+  * fused       k_fused_ab + k_fused_reduce: spmv_AB_fused (round 3, fused.hip).
 mgs_pass_sweep = every k_mgs_pass / k_mgs_normalize dispatch.
 """
 import csv
@@ -38,7 +39,14 @@ def groups(dispatches):
     i = 0
     while i < len(dispatches):
         _, nm, val = dispatches[i]
-        if "k_mgs" in nm:
+        if "k_fused_ab" in nm:                      # one pass A*(B*q): main kernel + partial reduction
+            vals = [val]
+            if i + 1 < len(dispatches) and "k_fused_reduce" in dispatches[i + 1][1]:
+                vals.append(dispatches[i + 1][2])
+                i += 1
+            out.append(("spmv_AB_fused", vals))
+            i += 1
+        elif "k_mgs" in nm:
             out.append(("mgs_pass_sweep", [val]))
             i += 1
         elif "k_spmv<" in nm:
