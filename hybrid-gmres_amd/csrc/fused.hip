@@ -366,19 +366,42 @@ T* upload(const std::vector<T>& v) {
 }
 }  // namespace
 
-// Region (R x R pixel square) of every row of B (rows = pixels in B's stored order).
+// The pixel grid of B's rows: the whole tiled N x N grid (row_order), or a pixel shard of whole
+// tile columns of one (row_grid: hgm_mat_row_slice, the multi-GPU path), whose stored positions
+// are then shard-local.  Returns the grid (trivial when neither).
+static PixOrder fused_grid(const hgm_mat* B) {
+    const PixOrder& o = B->row_order;
+    if (!o.trivial()) return (int64_t)o.N * o.N == B->rows ? o : PixOrder{};
+    const PixOrder& g = B->row_grid;
+    if (g.trivial() || g.super > 1 || B->rows % ((int64_t)std::max(g.tile, 1) * g.N) != 0) return PixOrder{};
+    return g;
+}
+
+// Region (R x R pixel square) of every row of B (rows = pixels in B's stored order; for a shard
+// the square grid is laid over the shard's N x W window of pixel columns).
 static std::vector<int32_t> row_regions(const hgm_mat* B, int R, int64_t* nreg) {
-    const PixOrder o = B->row_order;
-    HGM_REQUIRE(!o.trivial() && o.N > 0 && (int64_t)o.N * o.N == B->rows,
-                "fused A*(B*q): B's rows must be the pixels of a tiled N x N grid");
+    const PixOrder o = fused_grid(B);
+    HGM_REQUIRE(!o.trivial() && o.N > 0, "fused A*(B*q): B's rows must be the pixels of a tiled N x N grid or a shard of it");
     const int N = o.N;
-    const int nb = (N + R - 1) / R;
-    *nreg = (int64_t)nb * nb;
-    const std::vector<int64_t> ref = pix_reference_of_stored(o);
+    const int64_t W = B->rows / N;                     // pixel columns (N for the whole grid)
+    const int64_t nbr = (N + R - 1) / R, nbc = (W + R - 1) / R;
+    *nreg = nbr * nbc;
     std::vector<int32_t> reg(B->rows);
-    for (int64_t s = 0; s < B->rows; ++s) {
-        const int64_t r = ref[s] % N, c = ref[s] / N;
-        reg[s] = (int32_t)((c / R) * nb + r / R);
+    if (!B->row_order.trivial()) {
+        const std::vector<int64_t> ref = pix_reference_of_stored(o);
+        for (int64_t s = 0; s < B->rows; ++s) {
+            const int64_t r = ref[s] % N, c = ref[s] / N;
+            reg[s] = (int32_t)((c / R) * nbr + r / R);
+        }
+    } else {
+        // shard: whole tile columns, tile x tile tiles in tile-column-major order, column-major
+        // inside a tile (ops.hip pixel_rc without super-blocks), from the shard's first column
+        const int64_t t = std::max(o.tile, 1), tpc = N / t;
+        for (int64_t s = 0; s < B->rows; ++s) {
+            const int64_t tl = s / (t * t), w = s % (t * t);
+            const int64_t r = (tl % tpc) * t + w % t, c = (tl / tpc) * t + w / t;
+            reg[s] = (int32_t)((c / R) * nbr + r / R);
+        }
     }
     return reg;
 }
@@ -560,13 +583,14 @@ FusedPlan* fused_plan_build(hgm_ctx* c, const hgm_mat* B, int R) {
     return P;
 }
 
-// Whether w = A*(B*q) can run fused for this pair (B = A' value for value, fp64, tiled pixels).
+// Whether w = A*(B*q) can run fused for this pair (B = A' value for value, fp64, tiled pixels or
+// a shard of whole tile columns of them).  On a communicator the caller all-reduces w, as it does
+// A*(B*q) of the two-pass form.
 bool fused_ab_eligible(const hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
-    if (!c->num.fused_ab || c->num.parity || c->world > 1 || c->nccl || c->host_ar) return false;
+    if (!c->num.fused_ab || c->num.parity) return false;
     if (!A || !B || A->dtype != HGM_F64 || B->dtype != HGM_F64) return false;
     if (!(B->transpose_of == A->uid || A->transpose_of == B->uid)) return false;
-    const PixOrder o = B->row_order;
-    return !o.trivial() && (int64_t)o.N * o.N == B->rows && B->nnz > 0;
+    return !fused_grid(B).trivial() && B->nnz > 0;
 }
 
 // The plan of B, built on first use (a failure to plan leaves the two-pass path in place).

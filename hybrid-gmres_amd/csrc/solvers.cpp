@@ -426,6 +426,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             T* w = (ABQ && orth != HGM_CGS2) ? ABQ + (int64_t)kq * ldaq : v;
             if (fplan) {
                 fused_ab(c, B, fplan, qk, Bq, w);                                   // both in one pass over B
+                if (dist_n(c)) allreduce(c, w, m);                                 // (as apply_A)
             } else {
                 apply_B<T>(c, B, qk, Bq, EPI_NONE, T(0), nullptr);                  // B*Q(:,k)
                 apply_A<T>(c, A, Bq, w, EPI_NONE, T(0), nullptr);                   // A*(B*Q(:,k))
@@ -1241,7 +1242,10 @@ int arnoldi(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b_in, 
             apply_A<T>(c, A, qk, t, EPI_NONE, 0.0, nullptr);
             apply_B<T>(c, B, t, v, EPI_NONE, 0.0, nullptr);                    // :22 B*(A*Q(:,k))
         } else if (fplan) {
-            if constexpr (std::is_same_v<T, double>) fused_ab(c, B, fplan, qk, tn, v);   // :20
+            if constexpr (std::is_same_v<T, double>) {
+                fused_ab(c, B, fplan, qk, tn, v);                                 // :20
+                if (dist_n(c)) allreduce(c, v, A->rows);
+            }
         } else {
             apply_B<T>(c, B, qk, tn, EPI_NONE, 0.0, nullptr);
             apply_A<T>(c, A, tn, v, EPI_NONE, 0.0, nullptr);                   // :20 A*(B*Q(:,k))
