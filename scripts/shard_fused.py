@@ -2,7 +2,7 @@
 GPU: rank 0's shard for world = 1, 2, 4, 8 built exactly as bench.py builds it (build_shard), and
 its local A_g*(B_g*q) timed two-pass and one-pass (hgm_spmv_ab; fused.hip on a shard of whole tile
 columns).  The all-reduce of the m-vector that follows on a real communicator is not included.
-usage: python scripts/shard_fused.py [reps] [worlds, e.g. 1,2,4,8]"""
+usage: python scripts/shard_fused.py [reps] [worlds, e.g. 1,2,4,8] [extra fused region sides, e.g. 32,48]"""
 import ctypes as C
 import json
 import os
@@ -33,8 +33,10 @@ def main():
         abq = torch.empty(m, dtype=torch.float64, device=dev)
         out = {"world": world, "shard": [lo, hi], "nnz": A_g.nnz}
         res = {}
-        for name, o in (("two", dict(fused_ab=0)), ("fused", dict(fused_ab=1)), ("two_b", dict(fused_ab=0)),
-                        ("fused_b", dict(fused_ab=1))):
+        regions = [int(r) for r in sys.argv[3].split(",")] if len(sys.argv) > 3 else []
+        runs = [("two", dict(fused_ab=0)), ("fused", dict(fused_ab=1)), ("two_b", dict(fused_ab=0)),
+                ("fused_b", dict(fused_ab=1))] + [(f"fused_r{r}", dict(fused_ab=1, fused_region=r)) for r in regions]
+        for name, o in runs:
             with ctx.options(**o):
                 assert lib.hgm_spmv_ab(ctx.handle, A_g._h, B_g._h, P(q), P(bq), P(abq)) == 0   # plan / warm-up
                 ctx.synchronize()
