@@ -36,6 +36,9 @@ constexpr int FRMAX = 3968;    // rays per region (LDS accumulators; 64 x 64 pix
 constexpr int FLRMAX = 768;    // distinct rays per sub-chunk (C4: <= ~700)
 constexpr int FROWS = 128;     // pixel rows per sub-chunk
 }  // namespace
+#ifndef HGM_FUSED_FGR
+#define HGM_FUSED_FGR 16       // lanes per pixel-row sum (fixes the summation order)
+#endif
 
 // A sub-chunk's entries sit at LDS positions ("coordinates") e - (e0 & ~1): the values are loaded
 // in 16-byte pairs aligned in memory, so with an odd e0 coordinate 0 is the previous sub-chunk's
@@ -625,15 +628,15 @@ void fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q,
     // (one lane count per row sum for every variant: the same summation order, the same bits)
     const int d = c->num.fused_pf;
     if (c->num.fused_bs == 512) {
-        if (d <= 1) HGM_FUSED_LAUNCH(512, 16, 1);
-        else if (d == 2) HGM_FUSED_LAUNCH(512, 16, 2);
-        else if (d == 3) HGM_FUSED_LAUNCH(512, 16, 3);
-        else HGM_FUSED_LAUNCH(512, 16, 4);
+        if (d <= 1) HGM_FUSED_LAUNCH(512, HGM_FUSED_FGR, 1);
+        else if (d == 2) HGM_FUSED_LAUNCH(512, HGM_FUSED_FGR, 2);
+        else if (d == 3) HGM_FUSED_LAUNCH(512, HGM_FUSED_FGR, 3);
+        else HGM_FUSED_LAUNCH(512, HGM_FUSED_FGR, 4);
     } else {
-        if (d <= 1) HGM_FUSED_LAUNCH(1024, 16, 1);
-        else if (d == 2) HGM_FUSED_LAUNCH(1024, 16, 2);
-        else if (d == 3) HGM_FUSED_LAUNCH(1024, 16, 3);
-        else HGM_FUSED_LAUNCH(1024, 16, 4);
+        if (d <= 1) HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 1);
+        else if (d == 2) HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 2);
+        else if (d == 3) HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 3);
+        else HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 4);
     }
 #undef HGM_FUSED_LAUNCH
     launch(c, true, k_fused_reduce, dim3(grid_for(P->m)), dim3(BS), P->m, (const int64_t*)P->rs_ptr,

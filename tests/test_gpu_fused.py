@@ -93,3 +93,34 @@ def test_fused_not_taken_for_unmatched_or_reference_order(gpu_ctx):
             outs.append(hgmres.ABgmres_nonhybrid_bounds(P.A, P.B, P.b, P.x_true, 0.0, 8, ctx=gpu_ctx, return_H=True))
     for a_, b_ in zip(*outs):
         assert np.array_equal(np.asarray(a_), np.asarray(b_))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_fused_on_pixel_shards(gpu_ctx, world):
+    """The multi-GPU path (bench.py build_shard, DESIGN.md §5): rank g holds B_g = B(P_g,:), whole
+    tile columns of the tiled pixels, and A_g = B_g'.  The one-pass A_g*(B_g*q) on each shard (its
+    regions laid over the shard's window of pixel columns) matches the two-pass shard product, repeats
+    bitwise, and the shards' partials sum to the full operator's A*(B*q) (the all-reduce)."""
+    from hgmres.dist import tile_column_shards
+    N, na = 256, 47
+    A = hgmres.SparseOperator.siddon(N, na, ctx=gpu_ctx)
+    B = A.T
+    Nn, tile, sup = A.pixel_order("cols")
+    q = np.random.default_rng(1).standard_normal(A.shape[0])
+    with gpu_ctx.options(fused_ab=0):
+        _, full = hgmres.spmv_ab(A, B, q)
+    total = np.zeros(A.shape[0])
+    for lo, hi in tile_column_shards(N, world, tile):
+        B_g = B.row_slice(lo, hi)
+        A_g = B_g.T
+        with gpu_ctx.options(fused_ab=0):
+            bq2, ab2 = hgmres.spmv_ab(A_g, B_g, q)
+        with gpu_ctx.options(fused_ab=1):
+            bq1, ab1 = hgmres.spmv_ab(A_g, B_g, q)
+            bq1b, ab1b = hgmres.spmv_ab(A_g, B_g, q)
+        assert np.array_equal(ab1, ab1b) and np.array_equal(bq1, bq1b)
+        assert rel(bq1, bq2) <= 1e-14 and rel(ab1, ab2) <= 1e-13
+        total += ab1
+        A_g.close()
+        B_g.close()
+    assert rel(total, full) <= 1e-13
