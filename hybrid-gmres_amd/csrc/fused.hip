@@ -312,26 +312,34 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(D <= 2 ? FB
     for (int r = threadIdx.x; r < nr; r += FBS) part[pb + r] = acc[r];
 }
 
-// w_i = sum of ray i's region partials, in region order
+// w_i = sum of ray i's region partials.  RG lanes per ray: lane l takes the ray's partials l, l+RG,
+// ... in region order (loads batched 4 at a time), then the RG lane sums are added by a fixed
+// tree: the slot indices of a ray are read contiguously across its lanes.
+#ifndef HGM_FUSED_RG
+#define HGM_FUSED_RG 8
+#endif
+template <int RG>
 __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* __restrict__ rs_ptr,
                                                      const int32_t* __restrict__ rs_slot,
                                                      const double* __restrict__ part, double* __restrict__ w) {
-    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < m; i += (int64_t)gridDim.x * BS) {
+    const int gl = threadIdx.x % RG;
+    for (int64_t i = ((int64_t)blockIdx.x * BS + threadIdx.x) / RG; i < m; i += (int64_t)gridDim.x * (BS / RG)) {
         double s = 0.0;
         const int64_t k0 = rs_ptr[i], k1 = rs_ptr[i + 1];
-        int64_t k = k0;
-        for (; k + 8 <= k1; k += 8) {   // 8 slot reads, then 8 partial reads in flight; sums in order
-            int32_t sl[8];
-            double p[8];
+        int64_t k = k0 + gl;
+        for (; k + 3 * RG < k1; k += 4 * RG) {   // 4 slot reads, then 4 partial reads in flight
+            int32_t sl[4];
+            double p[4];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) sl[u] = rs_slot[k + u];
+            for (int u = 0; u < 4; ++u) sl[u] = rs_slot[k + u * RG];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) p[u] = part[sl[u]];
+            for (int u = 0; u < 4; ++u) p[u] = part[sl[u]];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) s += p[u];
+            for (int u = 0; u < 4; ++u) s += p[u];
         }
-        for (; k < k1; ++k) s += part[rs_slot[k]];
-        w[i] = s;
+        for (; k < k1; k += RG) s += part[rs_slot[k]];
+        if constexpr (RG > 1) s = group_sum<double, RG>(s);
+        if (gl == 0) w[i] = s;
     }
 }
 
@@ -639,7 +647,7 @@ void fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q,
         else HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 4);
     }
 #undef HGM_FUSED_LAUNCH
-    launch(c, true, k_fused_reduce, dim3(grid_for(P->m)), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
+    launch(c, true, k_fused_reduce<HGM_FUSED_RG>, dim3(grid_for(P->m * HGM_FUSED_RG)), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
            (const int32_t*)P->rs_slot, (const double*)P->part, ABq);
     HGM_HIP(hipGetLastError());
     // algorithmic bytes of the fused pass: B's CSR once (values, 32-bit indices, row pointers),
