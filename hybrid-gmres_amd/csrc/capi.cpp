@@ -700,7 +700,8 @@ HGM_API int hgm_mat_set_bands(hgm_ctx* c, hgm_mat* M, int64_t band_width, int gr
 
 HGM_API int hgm_mat_tune(hgm_mat* M, int variant, int group) {
     if (!M || variant < 0 || variant > 31) return HGM_E_ARG;
-    if (group != 0 && group != 4 && group != 8 && group != 16 && group != 32 && group != 64) return HGM_E_ARG;
+    if (group != 0 && group != 2 && group != 4 && group != 8 && group != 16 && group != 32 && group != 64) return HGM_E_ARG;
+    if (group == 2 && !(variant & SPMV_STREAM)) return HGM_E_ARG;   // (2 lanes: streaming reduction only)
     if ((variant & SPMV_PAGED) && !M->pg_ptr) {   // page index on demand (over the current stream)
         HGM_TRY(M->ctx, {
             HGM_HIP(hipSetDevice(M->ctx->device));

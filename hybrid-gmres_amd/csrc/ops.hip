@@ -334,6 +334,9 @@ static void build_ci16(hgm_ctx* c, hgm_mat* M) {
     HGM_HIP(hipGetLastError());
 }
 
+#ifndef HGM_B_SGROUP
+#define HGM_B_SGROUP 2
+#endif
 void finalize_operator(hgm_ctx* c, hgm_mat* M) {
     if (M->nnz > 0) build_stream_index(c, M);
     build_ci16(c, M);
@@ -357,10 +360,11 @@ void finalize_operator(hgm_ctx* c, hgm_mat* M) {
         }
     } else {
         if (M->nnz >= 50000000) {
-            // C3/C4 sweeps: 4 lanes per row with nontemporal val/col loads is best for the
-            // ~60-entry pixel rows (C4 2.75 ms = 4.48 TB/s, C3 240 us = 5.35 TB/s)
+            // C3/C4 sweeps: nontemporal val/col loads, and 2 lanes per pixel row in the segment
+            // reduction (round 3, isolated paged kernel: C4 B 2.02 -> 1.93 ms, C3 B 210 -> 207 us
+            // against 4 lanes; profiles/r3_stream_g2.log)
             M->variant = SPMV_STREAM | SPMV_NT;
-            M->sgroup = 4;
+            M->sgroup = HGM_B_SGROUP;
         } else {
             M->variant = 0;
             M->group = avg >= 6 ? 8 : 4;

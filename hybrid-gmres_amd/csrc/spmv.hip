@@ -610,6 +610,7 @@ static void spmv_stream(hgm_ctx* c, bool last, const SegIndex& si, int G, bool n
         case 32: HGM_SG(32) break;
         case 16: HGM_SG(16) break;
         case 8: HGM_SG(8) break;
+        case 2: HGM_SG(2) break;
         default: HGM_SG(4) break;
     }
 #undef HGM_SG
