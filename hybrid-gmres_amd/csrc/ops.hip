@@ -334,6 +334,9 @@ static void build_ci16(hgm_ctx* c, hgm_mat* M) {
     HGM_HIP(hipGetLastError());
 }
 
+#ifndef HGM_A_BSGROUP
+#define HGM_A_BSGROUP 4
+#endif
 #ifndef HGM_B_SGROUP
 #define HGM_B_SGROUP 2
 #endif
@@ -468,7 +471,9 @@ void set_bands(hgm_ctx* c, hgm_mat* M, int64_t W) {
     // profiles/r1_spmv_sweep_c4_*.jsonl: 2.90 ms vs 3.31 ms at 16 lanes).  Set here so that
     // hgm_mat_set_bands keeps it too (a 64-column re-band at 8/16 lanes cost the C4 shards
     // 2.57 vs 2.27 ms, profiles/r2_shard_order.log)
-    if (row_avg >= 64) M->bsgroup = 4;
+    // (round 3: 2 lanes helps fp32 only: C5 A 1.274 -> 1.258 ms in the solve, but C4 A 2.12 ->
+    // 2.17 ms and C3 A 226 -> 230 us in fp64; profiles/r3_ab_a2.log)
+    if (row_avg >= 64) M->bsgroup = M->dtype == HGM_F32 ? 2 : HGM_A_BSGROUP;
     HGM_HIP(hipStreamSynchronize(st));
 }
 
