@@ -509,6 +509,19 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             if (!(v >= 0 && v <= 15 && v == std::floor(v))) return bad("fused_dbg is 0..15");
             n.fused_dbg = (int)v;
             break;
+        case HGM_OPT_FUSED_KIND: if (!b01) return bad("fused_kind is 0 or 1"); n.fused_kind = (int)v; break;
+        case HGM_OPT_FUSED_WREGION:
+            if (!(v >= 4 && v <= 256 && v == std::floor(v))) return bad("fused_wregion is an integer in [4, 256]");
+            n.fused_wregion = (int)v;
+            break;
+        case HGM_OPT_FUSED_WAVES:
+            if (!(v == 1 || v == 2 || v == 4)) return bad("fused_waves is 1, 2 or 4");
+            n.fused_waves = (int)v;
+            break;
+        case HGM_OPT_FUSED_GROUP:
+            if (!(v == 4 || v == 8)) return bad("fused_group is 4 or 8");
+            n.fused_group = (int)v;
+            break;
         default: return bad("unknown option");
     }
     return HGM_OK;
@@ -541,6 +554,10 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_FUSED_DBG: *v = n.fused_dbg; break;
         case HGM_OPT_FUSED_PF: *v = n.fused_pf; break;
         case HGM_OPT_KRYLOV_PAD: *v = n.krylov_pad; break;
+        case HGM_OPT_FUSED_KIND: *v = n.fused_kind; break;
+        case HGM_OPT_FUSED_WREGION: *v = n.fused_wregion; break;
+        case HGM_OPT_FUSED_WAVES: *v = n.fused_waves; break;
+        case HGM_OPT_FUSED_GROUP: *v = n.fused_group; break;
         default: return HGM_E_ARG;
     }
     return HGM_OK;

@@ -22,6 +22,9 @@
 //      in a fixed order): every sum has a fixed order, so products are bitwise reproducible.
 // Per entry the pass reads the value (8 B) and perm (2 B); the local-ray records add ~1.4 B.
 #include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <chrono>
 #include <numeric>
 #include <thread>
@@ -56,8 +59,15 @@ struct FusedSub {
 static_assert(sizeof(FusedSub) == 32, "FusedSub layout");
 
 struct FusedPlan {
-    int region = 0;
+    int kind = 0;                 // 0 sub-chunk pass (k_fused_ab), 1 row-wave pass (k_fused_rw)
+    int region = 0, waves = 0, maxr = 0, group = 0;
     int64_t nreg = 0, nsub = 0, nlr = 0, nslot = 0, m = 0;
+    // kind 1: per (region, wave) a range of row runs; the region's rays; every entry's index
+    // among its region's rays
+    int32_t* wrun = nullptr;      // nreg * waves + 1
+    int2* runs = nullptr;         // (first row, rows)
+    int32_t* ray_tab = nullptr;   // nslot: global ray of each region-local ray
+    uint16_t* lidx = nullptr;     // nnz (+ padding)
     int32_t* reg_sub = nullptr;   // nreg+1
     int64_t* reg_base = nullptr;  // nreg+1
     FusedSub* subs = nullptr;     // nsub
@@ -73,7 +83,8 @@ struct FusedPlan {
 void fused_plan_free(FusedPlan* P) {
     if (!P) return;
     for (void* p : {(void*)P->reg_sub, (void*)P->reg_base, (void*)P->subs, (void*)P->perm, (void*)P->lr_ray,
-                    (void*)P->lr_pk, (void*)P->rs_ptr, (void*)P->rs_slot, (void*)P->part})
+                    (void*)P->lr_pk, (void*)P->rs_ptr, (void*)P->rs_slot, (void*)P->part, (void*)P->wrun,
+                    (void*)P->runs, (void*)P->ray_tab, (void*)P->lidx})
         if (p) (void)hipFree(p);
     delete P;
 }
@@ -344,6 +355,209 @@ __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* _
 }
 
 // ------------------------------------------------------------------------------------------
+// Row-wave pass (kind 1).  One workgroup of W waves per region; the region's rays get LDS
+// slots: q of each ray (shared) and one accumulator per wave (private).  A wave walks its share
+// of the region's pixel rows one row at a time, the row's entries across its 64 lanes (NCH
+// chunks of 64): p = v * q[slot] in registers, z_j = the wave sum of p (fixed tree), then
+// acc[slot] += v * z_j.  A pixel row meets each ray at most once, so the lanes of one row hit
+// distinct slots: no conflicts, no atomics, no barriers; the wave's rows go in a fixed order and
+// the W accumulators are added in wave order at the end, so every sum has a fixed order.
+// Per entry the pass reads the value (8 B) and its slot (2 B) once, and touches the LDS three
+// times (q read, accumulator read and write).
+//
+// Loads are software-pipelined in batches of G rows (never crossing a run of consecutive rows):
+// the row pointers of batch b+2 and the entries of batch b+1 are in flight while batch b is
+// processed.  Every load goes through a buffer resource sized to its row (past the end: 0), so
+// each batch issues the same instructions and the compiler's in-order vmcnt waits stay exact.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Lane exchanges of gfx950 for a transposed reduction (fp64 as two dwords): swap32 swaps lanes
+// 32-63 of a with lanes 0-31 of b, swap16 the odd 16-lane rows of a with the even rows of b.
+__device__ __forceinline__ void swap32(double& a, double& b) {
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false, false);
+    a = __hiloint2double((int)hi[0], (int)lo[0]);
+    b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void swap16(double& a, double& b) {
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false, false);
+    a = __hiloint2double((int)hi[0], (int)lo[0]);
+    b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+// The 64-lane sums of G values at once (G = 4 or 8), by a butterfly that halves the values per
+// lane while it halves the lanes per sum: lane l ends with the sum of P[l / (64 / G)], the same
+// bits in each lane of its group.  Fixed order.  Per row this is ~6 exchanges and adds instead of
+// a full wave reduction each (DPP tree + 8 readlanes).
+template <int G>
+__device__ __forceinline__ double rows_sum_t(double (&P)[G]) {
+    static_assert(G == 4 || G == 8, "rows per batch");
+#pragma unroll
+    for (int i = 0; i < G / 2; ++i) {          // lane bit 5
+        swap32(P[i], P[i + G / 2]);
+        P[i] = P[i] + P[i + G / 2];
+    }
+#pragma unroll
+    for (int i = 0; i < G / 4; ++i) {          // lane bit 4
+        swap16(P[i], P[i + G / 4]);
+        P[i] = P[i] + P[i + G / 4];
+    }
+    if constexpr (G == 8) {                    // lane bit 3: row_ror 8 within 16-lane rows
+        const bool hi = (threadIdx.x & 8) != 0;
+        double s = hi ? P[1] : P[0];
+        const double t = hi ? P[0] : P[1];
+        s = s + dpp_mov<0x128>(t);
+        s += dpp_mov<0xB1>(s);                 // lane ^ 1
+        s += dpp_mov<0x4E>(s);                 // lane ^ 2
+        s += dpp_mov<0x141>(s);                // other quad of the 8-lane half
+        return s;
+    } else {
+        return row16_sum(P[0]);
+    }
+}
+
+template <int W, int MAXR, int G, int NCH>
+__global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__ reg_base, const int32_t* __restrict__ ray_tab,
+                                                     const int32_t* __restrict__ wrun, const int2* __restrict__ runs,
+                                                     const int64_t* __restrict__ rp, const double* __restrict__ val,
+                                                     const uint16_t* __restrict__ lidx, const double* __restrict__ q,
+                                                     double* __restrict__ z, double* __restrict__ part) {
+    __shared__ double qloc[MAXR];           // (the last 64: the lanes' dummy slots)
+    __shared__ double acc[W][MAXR];
+    const int g = blockIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int ln = threadIdx.x & 63;
+    const int64_t pb = reg_base[g];
+    const int nr = (int)(reg_base[g + 1] - pb);
+    for (int k = threadIdx.x; k < nr; k += 64 * W) {
+        qloc[k] = q[ray_tab[pb + k]];
+#pragma unroll
+        for (int w = 0; w < W; ++w) acc[w][k] = 0.0;
+    }
+    if (threadIdx.x < 64) qloc[MAXR - 64 + threadIdx.x] = 0.0;
+    int ua = wrun[g * W + wv];
+    const int ub = wrun[g * W + wv + 1];
+    __syncthreads();
+    double* __restrict__ ac = acc[wv];
+    // the wave's runs (<= 64, the plan checks) in lanes: readlane in the loop, no loads there
+    // (a conditional load makes the compiler wait for every load in flight after it, and scalar
+    // loads' lgkmcnt waits would also wait on the LDS)
+    const int2 runv = ua + ln < ub ? runs[ua + ln] : make_int2(0, 0);
+    int u = ua, o = 0;
+    auto next = [&](int& r0, int& cnt) {
+        r0 = 0;
+        cnt = 0;
+        if (u >= ub) return;
+        const int rr = __builtin_amdgcn_readlane(runv.x, u - ua), rn = __builtin_amdgcn_readlane(runv.y, u - ua);
+        r0 = rr + o;
+        cnt = min(G, rn - o);
+        o += cnt;
+        if (o == rn) {
+            ++u;
+            o = 0;
+        }
+    };
+    // row pointers of a batch: lane j <= cnt holds rp[r0 + j]
+    auto load_rp = [&](int r0, int cnt) -> int64_t {
+        const __amdgpu_buffer_rsrc_t r = buf_rsrc(rp + r0, (cnt + 1) * 8);
+        return __builtin_bit_cast(int64_t, __builtin_amdgcn_raw_buffer_load_b64(r, min(ln, G) * 8, 0, 0));
+    };
+    struct RB {
+        int r0, cnt;
+        int len[G];
+        double v[G][NCH];
+        uint32_t s[G][NCH];
+    };
+    auto issue = [&](RB& b, int r0, int cnt, int64_t rpv) {
+        b.r0 = r0;
+        b.cnt = cnt;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int64_t e0 = readlane64(rpv, min(j, cnt)), e1 = readlane64(rpv, min(j + 1, cnt));
+            const int len = (int)(e1 - e0);
+            b.len[j] = len;
+            const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + e0, len * 8);
+            const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lidx + e0, len * 2);
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                b.v[j][c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, (ln + 64 * c) * 8, 0, 2));
+                b.s[j][c] = (uint32_t)__builtin_bit_cast(uint16_t, __builtin_amdgcn_raw_buffer_load_b16(rl, (ln + 64 * c) * 2, 0, 2));
+            }
+        }
+    };
+    // Branch-free: lanes past a row's end hold v = 0 (the buffer range) and are pointed at a
+    // private dummy slot (MAXR - 64 + lane, q = 0), so every row issues the same instructions and the
+    // compiler can interleave the G rows' product and reduction chains (a branch would end the
+    // basic block).  The accumulator updates stay in row order (consecutive rows share rays).
+    auto process = [&](RB& b) {
+        double P[G];
+        uint32_t k[G][NCH];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            double p = 0.0;
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                k[j][c] = ln + 64 * c < b.len[j] ? b.s[j][c] : (uint32_t)(MAXR - 64 + ln);
+                p += b.v[j][c] * qloc[k[j][c]];
+            }
+            P[j] = p;
+        }
+        constexpr int GL = 64 / G;                // lanes per row sum after the butterfly
+        const double S = rows_sum_t<G>(P);        // lane l: z of row l / GL
+        {   // z out: each group's first lane, rows past cnt fall outside the range
+            const __amdgpu_buffer_rsrc_t rz = buf_rsrc(z + b.r0, b.cnt * 8);
+            buf_store(S, rz, (ln & (GL - 1)) == 0 ? (ln / GL) * 8 : (1 << 30));
+        }
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const double sj = lane_bcast(S, j * GL);
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                const double t = b.v[j][c] * sj;
+                ac[k[j][c]] = ac[k[j][c]] + t;
+            }
+        }
+    };
+    RB b0, b1;
+    int a0, c0, a1, c1;
+    next(a0, c0);
+    int64_t rA = load_rp(a0, c0);
+    next(a1, c1);
+    int64_t rB = load_rp(a1, c1);
+    issue(b0, a0, c0, rA);
+    // one exit, at the bottom: the two halves keep their register sets (a rotated loop with two
+    // exits had the compiler copy in-flight batches, waiting for them); an empty batch is
+    // processed as a no-op (zero-length ranges, dummy slots)
+    // (sched_barrier: the scheduler would sink the next batch's loads into the processing)
+    do {
+        next(a0, c0);
+        rA = load_rp(a0, c0);
+        issue(b1, a1, c1, rB);
+        __builtin_amdgcn_sched_barrier(0);
+        process(b0);
+        __builtin_amdgcn_sched_barrier(0);
+        next(a1, c1);
+        rB = load_rp(a1, c1);
+        issue(b0, a0, c0, rA);
+        __builtin_amdgcn_sched_barrier(0);
+        process(b1);
+        __builtin_amdgcn_sched_barrier(0);
+    } while (b0.cnt > 0);
+    __syncthreads();
+    for (int k = threadIdx.x; k < nr; k += 64 * W) {
+        double t = acc[0][k];
+#pragma unroll
+        for (int w = 1; w < W; ++w) t += acc[w][k];
+        part[pb + k] = t;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // plan (host, from B's CSR structure; once per operator)
 // ------------------------------------------------------------------------------------------
 namespace {
@@ -594,6 +808,146 @@ FusedPlan* fused_plan_build(hgm_ctx* c, const hgm_mat* B, int R) {
     return P;
 }
 
+// The row-wave plan (kind 1): regions of R x R pixels, W waves per region.  Each wave gets a
+// contiguous share (by entries) of the region's rows in stored order, as runs of consecutive
+// rows; each entry gets its ray's index among the region's rays (sorted ray ids).
+namespace {
+constexpr int RW_MAXR[] = {1024, 2048, 4096};   // LDS slots of the instantiated kernels (64 of them dummies)
+constexpr int RW_NCH_MAX = 4;                     // chunks of 64 entries per row (rows <= 256)
+}  // namespace
+
+FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G) {
+    HGM_REQUIRE(B->dtype == HGM_F64, "fused A*(B*q): fp64 operators");
+    HGM_REQUIRE(B->cols < (int64_t(1) << 31) && B->rows < (int64_t(1) << 31), "fused A*(B*q): index range");
+    HGM_REQUIRE(W == 1 || W == 2 || W == 4, "fused A*(B*q): 1, 2 or 4 waves per region");
+    const auto t0 = std::chrono::steady_clock::now();
+    const int64_t n = B->rows, m = B->cols, nnz = B->nnz;
+    int64_t nreg = 0;
+    const std::vector<int32_t> reg = row_regions(B, R, &nreg);
+    std::vector<int64_t> rp(n + 1);
+    std::vector<int32_t> ci(std::max<int64_t>(nnz, 1));
+    HGM_HIP(hipMemcpy(rp.data(), B->rp, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost));
+    if (nnz) HGM_HIP(hipMemcpy(ci.data(), B->ci, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
+    int64_t maxlen = 0;
+    for (int64_t s = 0; s < n; ++s) maxlen = std::max(maxlen, rp[s + 1] - rp[s]);
+    HGM_REQUIRE(maxlen <= 64 * RW_NCH_MAX, "fused A*(B*q): a pixel row longer than the row-wave pass takes");
+    // runs of consecutive stored rows of one region, per region in stored order
+    std::vector<std::vector<int2>> rr(nreg);
+    for (int64_t s = 0; s < n; ++s) {
+        auto& v = rr[reg[s]];
+        if (!v.empty() && v.back().x + v.back().y == s) ++v.back().y;
+        else v.push_back(make_int2((int)s, 1));
+    }
+    // split each region's row sequence into W contiguous shares of about equal entries
+    std::vector<std::vector<int2>> wr((size_t)nreg * W);
+    parallel_for(nreg, [&](int64_t g) {
+        int64_t tot = 0;
+        for (const int2& r : rr[g]) tot += rp[r.x + r.y] - rp[r.x];
+        int w = 0;
+        int64_t done = 0;
+        for (const int2& r : rr[g]) {
+            for (int s = r.x; s < r.x + r.y; ++s) {
+                while (w < W - 1 && done * W >= tot * (w + 1)) ++w;
+                auto& v = wr[(size_t)g * W + w];
+                if (!v.empty() && v.back().x + v.back().y == s) ++v.back().y;
+                else v.push_back(make_int2(s, 1));
+                done += rp[s + 1] - rp[s];
+            }
+        }
+    });
+    std::vector<int32_t> wrun((size_t)nreg * W + 1, 0);
+    for (size_t i = 0; i < wr.size(); ++i) {
+        HGM_REQUIRE(wr[i].size() <= 64, "fused A*(B*q): more than 64 row runs per wave");
+        wrun[i + 1] = wrun[i] + (int32_t)wr[i].size();
+    }
+    std::vector<int2> runs(std::max<int32_t>(wrun.back(), 1));
+    for (size_t i = 0; i < wr.size(); ++i) std::copy(wr[i].begin(), wr[i].end(), runs.begin() + wrun[i]);
+    // region ray sets and every entry's slot among them (a dense map per thread)
+    std::vector<std::vector<int32_t>> rrays(nreg);
+    std::vector<uint16_t> lidx(std::max<int64_t>(nnz, 1) + 256, 0);
+    std::atomic<int> worst{0};
+    {
+        unsigned nt = std::max(1u, std::min(std::thread::hardware_concurrency(), 16u));
+        std::vector<std::thread> th;
+        std::atomic<int64_t> nextg{0};
+        for (unsigned t = 0; t < nt; ++t)
+            th.emplace_back([&]() {
+                std::vector<int32_t> map(m, -1);
+                for (int64_t g; (g = nextg.fetch_add(1)) < nreg;) {
+                    auto& rs = rrays[g];
+                    for (const int2& r : rr[g])
+                        for (int64_t e = rp[r.x]; e < rp[r.x + r.y]; ++e) rs.push_back(ci[e]);
+                    std::sort(rs.begin(), rs.end());
+                    rs.erase(std::unique(rs.begin(), rs.end()), rs.end());
+                    int cur = worst.load();
+                    while ((int)rs.size() > cur && !worst.compare_exchange_weak(cur, (int)rs.size())) {}
+                    if (rs.size() > (size_t)RW_MAXR[2] - 64) continue;
+                    for (size_t k = 0; k < rs.size(); ++k) map[rs[k]] = (int32_t)k;
+                    for (const int2& r : rr[g])
+                        for (int64_t e = rp[r.x]; e < rp[r.x + r.y]; ++e) lidx[e] = (uint16_t)map[ci[e]];
+                    for (int32_t ray : rs) map[ray] = -1;
+                }
+            });
+        for (auto& t : th) t.join();
+    }
+    int maxr = 0;
+    for (int mr : RW_MAXR)
+        if (worst.load() <= mr - 64) {
+            maxr = mr;
+            break;
+        }
+    HGM_REQUIRE(maxr > 0, "fused A*(B*q): a region is crossed by more rays than the LDS holds");
+    HGM_REQUIRE((int64_t)(1 + W) * maxr * 8 <= 160 * 1024 && !(W == 4 && maxr > 2048),
+                "fused A*(B*q): region rays x waves exceed the LDS");
+    std::vector<int64_t> reg_base(nreg + 1, 0);
+    for (int64_t g = 0; g < nreg; ++g) reg_base[g + 1] = reg_base[g] + (int64_t)rrays[g].size();
+    const int64_t nslot = reg_base[nreg];
+    HGM_REQUIRE(nslot < (int64_t(1) << 31), "fused A*(B*q): partial slots");
+    std::vector<int32_t> ray_tab(std::max<int64_t>(nslot, 1));
+    for (int64_t g = 0; g < nreg; ++g) std::copy(rrays[g].begin(), rrays[g].end(), ray_tab.begin() + reg_base[g]);
+    // ray-major reduction index: ray i's slots in region order
+    std::vector<int64_t> rs_ptr(m + 1, 0);
+    for (int64_t g = 0; g < nreg; ++g)
+        for (int32_t ray : rrays[g]) rs_ptr[ray + 1]++;
+    for (int64_t i = 0; i < m; ++i) rs_ptr[i + 1] += rs_ptr[i];
+    std::vector<int32_t> rs_slot(std::max<int64_t>(nslot, 1));
+    {
+        std::vector<int64_t> fill(rs_ptr.begin(), rs_ptr.end() - 1);
+        for (int64_t g = 0; g < nreg; ++g)
+            for (size_t r = 0; r < rrays[g].size(); ++r) rs_slot[fill[rrays[g][r]]++] = (int32_t)(reg_base[g] + r);
+    }
+    FusedPlan* P = new FusedPlan;
+    try {
+        P->kind = 1;
+        P->region = R;
+        P->waves = W;
+        P->group = G;
+        P->maxr = maxr;
+        P->nsub = (maxlen + 63) / 64;      // (kind 1: chunks of 64 entries per row)
+        P->nreg = nreg;
+        P->nslot = nslot;
+        P->m = m;
+        P->reg_base = upload(reg_base);
+        P->wrun = upload(wrun);
+        P->runs = upload(runs);
+        P->ray_tab = upload(ray_tab);
+        P->lidx = upload(lidx);
+        P->rs_ptr = upload(rs_ptr);
+        P->rs_slot = upload(rs_slot);
+        if (hipMalloc(&P->part, sizeof(double) * std::max<int64_t>(nslot, 1)) != hipSuccess)
+            throw Error{HGM_E_NOMEM, "fused plan: hipMalloc failed"};
+    } catch (...) {
+        fused_plan_free(P);
+        throw;
+    }
+    (void)c;
+    P->build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (std::getenv("HGM_FUSED_VERBOSE"))
+        std::fprintf(stderr, "[fused rw plan] region %d waves %d group %d: %lld regions, %lld slots, max rays %d (LDS slots %d), longest row %lld, %d runs, %.2f s\n",
+                     R, W, G, (long long)nreg, (long long)nslot, worst.load(), maxr, (long long)maxlen, wrun.back(), P->build_s);
+    return P;
+}
+
 // Whether w = A*(B*q) can run fused for this pair (B = A' value for value, fp64, tiled pixels or
 // a shard of whole tile columns of them).  On a communicator the caller all-reduces w, as it does
 // A*(B*q) of the two-pass form.
@@ -608,14 +962,22 @@ bool fused_ab_eligible(const hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
 const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
     if (!fused_ab_eligible(c, A, B)) return nullptr;
     hgm_mat* Bm = const_cast<hgm_mat*>(B);
-    if (Bm->fused && Bm->fused->region != c->num.fused_region) {
+    const Numerics& nu = c->num;
+    const bool rw = nu.fused_kind == 1;
+    auto stale = [&](const FusedPlan* P) {
+        if (P->kind != (rw ? 1 : 0)) return true;
+        return rw ? (P->region != nu.fused_wregion || P->waves != nu.fused_waves || P->group != nu.fused_group)
+                  : P->region != nu.fused_region;
+    };
+    if (Bm->fused && stale(Bm->fused)) {
         fused_plan_free(Bm->fused);
         Bm->fused = nullptr;
         Bm->fused_failed = false;
     }
     if (!Bm->fused && !Bm->fused_failed) {
         try {
-            Bm->fused = fused_plan_build(c, B, c->num.fused_region);
+            Bm->fused = rw ? fused_plan_build_rw(c, B, nu.fused_wregion, nu.fused_waves, nu.fused_group)
+                           : fused_plan_build(c, B, nu.fused_region);
         } catch (const Error& e) {
             if (e.code != HGM_E_ARG) throw;
             Bm->fused_failed = true;
@@ -624,10 +986,34 @@ const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
     return Bm->fused;
 }
 
+// kind 1: the row-wave kernel instantiated for the plan's waves, LDS ray slots, row batch and
+// chunks per row
+static void fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq) {
+    const int W = P->waves, MR = P->maxr, G = P->group, NC = P->nsub <= 2 ? 2 : 4;
+#define HGM_RW(WV, MRV, GV, NCV)                                                                                   \
+    if (W == WV && MR == MRV && G == GV && NC == NCV) {                                                            \
+        launch(c, false, k_fused_rw<WV, MRV, GV, NCV>, dim3((unsigned)P->nreg), dim3(64 * WV),                      \
+               (const int64_t*)P->reg_base, (const int32_t*)P->ray_tab, (const int32_t*)P->wrun,                  \
+               (const int2*)P->runs, (const int64_t*)B->rp, (const double*)B->val, (const uint16_t*)P->lidx, q, Bq, \
+               P->part);                                                                                            \
+        return;                                                                                                     \
+    }
+#define HGM_RW_G(WV, MRV) HGM_RW(WV, MRV, 4, 2) HGM_RW(WV, MRV, 8, 2) HGM_RW(WV, MRV, 4, 4) HGM_RW(WV, MRV, 8, 4)
+    HGM_RW_G(1, 1024) HGM_RW_G(1, 2048) HGM_RW_G(1, 4096)
+    HGM_RW_G(2, 1024) HGM_RW_G(2, 2048) HGM_RW_G(2, 4096)
+    HGM_RW_G(4, 1024) HGM_RW_G(4, 2048)
+#undef HGM_RW_G
+#undef HGM_RW
+    throw Error{HGM_E_ARG, "fused A*(B*q): no row-wave kernel for this plan"};
+}
+
 // Bq = B*q (n), ABq = A*(B*q) (m), one pass over B.
 void fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq) {
     hipEvent_t t0 = nullptr;
     timing_begin(c, KC_FUSED, &t0);
+    if (P->kind == 1) {
+        fused_rw_launch(c, B, P, q, Bq);
+    } else {
 #define HGM_FUSED_LAUNCH(FB, FGV, PFV)                                                                          \
     launch(c, false, k_fused_ab<FB, FGV, PFV>, dim3((unsigned)P->nreg), dim3(FB), (const FusedSub*)P->subs,      \
            (const int32_t*)P->reg_sub, (const int64_t*)P->reg_base, (const uint16_t*)P->perm,                    \
@@ -647,6 +1033,7 @@ void fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q,
         else HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 4);
     }
 #undef HGM_FUSED_LAUNCH
+    }
     launch(c, true, k_fused_reduce<HGM_FUSED_RG>, dim3(grid_for(P->m * HGM_FUSED_RG)), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
            (const int32_t*)P->rs_slot, (const double*)P->part, ABq);
     HGM_HIP(hipGetLastError());

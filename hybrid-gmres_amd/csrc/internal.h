@@ -81,6 +81,10 @@ struct Numerics {
     int fused_region = 64;          // ... pixel square per workgroup (its rays accumulate in LDS)
     int fused_bs = 1024;            // ... threads per workgroup (512, 1024)
     int fused_pf = 2;               // ... sub-chunk batches in registers (pipeline depth 1..4)
+    int fused_kind = 1;             // ... 0 sub-chunk pass, 1 row-wave pass
+    int fused_wregion = 32;         // ... row-wave pass: pixel square per workgroup
+    int fused_waves = 4;            // ... row-wave pass: waves per workgroup (1, 2, 4)
+    int fused_group = 8;            // ... row-wave pass: rows per load batch (4, 8)
     int krylov_pad = -1;            // Krylov basis column padding (elements; -1 auto, kernels.hip krylov_ld)
     int fused_dbg = 0;              // ... timing experiments: skip phases (wrong results)
 };

@@ -132,7 +132,12 @@ enum hgm_ctx_option {
                                       (0 = 1: no prefetch) [2] */
     HGM_OPT_KRYLOV_PAD = 23        /* elements added to the Krylov basis' leading dimension when it
                                       is a multiple of 4096 (a power-of-two column stride sends
-                                      every column's element i to the same HBM channel) [-1 = auto] */
+                                      every column's element i to the same HBM channel) [-1 = auto] */,
+    HGM_OPT_FUSED_KIND = 24,       /* ... kernel of the one-pass A*(B*q): 0 sub-chunk pass (options 19-22),
+                                      1 row-wave pass (options 25-27) [1] */
+    HGM_OPT_FUSED_WREGION = 25,    /* ... row-wave pass: pixel square (side) per workgroup [32] */
+    HGM_OPT_FUSED_WAVES = 26,      /* ... row-wave pass: waves per workgroup, 1, 2 or 4 [4] */
+    HGM_OPT_FUSED_GROUP = 27       /* ... row-wave pass: pixel rows per load batch, 4 or 8 [8] */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for

@@ -34,13 +34,17 @@ for vname in variants:
     # two | f<threads>[x<depth>][r<region>] (fused, pipeline depth [2], region side [64])
     # | d<bits> (phase-skip timing)
     mf = re.fullmatch(r"f(\d+)(?:x(\d))?(?:r(\d+))?", vname)
-    if vname == "two":
+    mw = re.fullmatch(r"w(\d)r(\d+)(?:g(\d))?", vname)      # row-wave pass: waves, region, rows per batch
+    if mw:
+        o = dict(fused_ab=1, fused_kind=1, fused_waves=int(mw.group(1)), fused_wregion=int(mw.group(2)),
+                 fused_group=int(mw.group(3) or 4))
+    elif vname == "two":
         o = dict(fused_ab=0)
     elif mf:
-        o = dict(fused_ab=1, fused_bs=int(mf.group(1)), fused_pf=int(mf.group(2) or 2),
+        o = dict(fused_ab=1, fused_kind=0, fused_bs=int(mf.group(1)), fused_pf=int(mf.group(2) or 2),
                  fused_region=int(mf.group(3) or 64))
     else:
-        o = dict(fused_ab=1, fused_dbg=int(vname[1:]))
+        o = dict(fused_ab=1, fused_kind=0, fused_dbg=int(vname[1:]))
     with ctx.options(**o):
         lib.hgm_spmv_ab(ctx.handle, A._h, B._h, P(q), P(bq), P(abq))      # plan / warm-up
         ctx.synchronize()
@@ -54,5 +58,6 @@ for vname in variants:
     if vname == "two":
         ref = (bq.cpu().numpy(), out)
     dev_ = None if ref is None else float(np.linalg.norm(out - ref[1]) / np.linalg.norm(ref[1]))
+    devz = None if ref is None else float(np.linalg.norm(bq.cpu().numpy() - ref[0]) / np.linalg.norm(ref[0]))
     print(json.dumps({"variant": vname, "N": N, "angles": na, "ms": round(dt * 1e3, 4),
-                      "effective_GBps_two_pass": round(two / dt / 1e9, 1), "rel_dev_vs_two_pass": dev_}), flush=True)
+                      "effective_GBps_two_pass": round(two / dt / 1e9, 1), "rel_dev_vs_two_pass": dev_, "bq_rel_dev": devz}), flush=True)

@@ -8,6 +8,9 @@ in another fixed order than the two-pass kernels', so:
   * B*q itself (the kept column, read by x = (B*Q) y): within rounding of the two-pass product,
   * pixel grids whose side is not a multiple of the region, several region sizes, and a region
     crossed by more rays than the LDS holds (the plan is refused: the two-pass path runs).
+Two kernels do the pass (HGM_OPT_FUSED_KIND): the sub-chunk pass (kind 0) and the row-wave pass
+(kind 1, the default); both are held to the same bars over several region shapes, waves and row
+batches.
 The full-size check (C4, 1e9 nnz, 20 iterations vs the oracle fixture) is
 tests/test_gpu_fullsize.py::test_c4_ab_gmres_full_size, which runs with the fused pass on (default).
 """
@@ -39,26 +42,42 @@ def _device_problem(ctx, N, na, seed=0):
     return A, A.T, b0 + e / np.linalg.norm(e) * 1e-2 * np.linalg.norm(b0), xt
 
 
-@pytest.mark.parametrize("N,na,region", [(512, 30, 64), (100, 17, 64), (256, 47, 32), (256, 47, 16), (128, 90, 24)])
-def test_fused_ab_matches_two_pass_and_oracle(gpu_ctx, N, na, region):
+# (N, angles, kind, region, waves, rows per batch): kind 0 the sub-chunk pass (fused_region),
+# kind 1 the row-wave pass (fused_wregion / fused_waves / fused_group)
+CASES = [(512, 30, 0, 64, 0, 0), (100, 17, 0, 64, 0, 0), (256, 47, 0, 32, 0, 0), (256, 47, 0, 16, 0, 0),
+         (128, 90, 0, 24, 0, 0),
+         (512, 30, 1, 32, 4, 8), (100, 17, 1, 32, 4, 4), (256, 47, 1, 24, 4, 8), (256, 47, 1, 16, 1, 8),
+         (256, 47, 1, 32, 2, 4), (128, 90, 1, 16, 2, 8), (200, 60, 1, 20, 1, 4)]
+
+
+def _fused_opts(kind, region, waves, group):
+    if kind == 0:
+        return dict(fused_ab=1, fused_kind=0, fused_region=region)
+    return dict(fused_ab=1, fused_kind=1, fused_wregion=region, fused_waves=waves, fused_group=group)
+
+
+@pytest.mark.parametrize("N,na,kind,region,waves,group", CASES)
+def test_fused_ab_matches_two_pass_and_oracle(gpu_ctx, N, na, kind, region, waves, group):
     A, B, b, xt = _device_problem(gpu_ctx, N, na)
     k = 20
     with gpu_ctx.options(fused_ab=0):
         ref2 = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
-    with gpu_ctx.options(fused_ab=1, fused_region=region):
+    with gpu_ctx.options(**_fused_opts(kind, region, waves, group)):
         out = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
         again = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
         hyb = hgmres.ABgmres_hybrid_bounds(A, B, b, xt, 0.0, k, 1e-2, ctx=gpu_ctx, return_H=True)
-        # the workgroup-size variant keeps the summation order: the same bits
-        with gpu_ctx.options(fused_bs=512):
-            o2 = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
-        assert all(np.array_equal(np.asarray(a_), np.asarray(b_)) for a_, b_ in zip(out, o2))
+        if kind == 0:
+            # the workgroup-size variant keeps the summation order: the same bits
+            with gpu_ctx.options(fused_bs=512):
+                o2 = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
+            assert all(np.array_equal(np.asarray(a_), np.asarray(b_)) for a_, b_ in zip(out, o2))
     with gpu_ctx.options(fused_ab=0):
         hyb2 = hgmres.ABgmres_hybrid_bounds(A, B, b, xt, 0.0, k, 1e-2, ctx=gpu_ctx, return_H=True)
     for a_, b_ in zip(out, again):
         assert np.array_equal(np.asarray(a_), np.asarray(b_))               # bitwise reproducible
     dH = float(np.max(np.abs(out[-1] - ref2[-1])) / np.max(np.abs(ref2[-1])))
-    print(f"[fused N={N} angles={na} region={region}] |dH| vs two-pass {dH:.1e}, x {rel(out[0], ref2[0]):.1e}")
+    print(f"[fused N={N} angles={na} kind={kind} region={region} waves={waves} group={group}] "
+          f"|dH| vs two-pass {dH:.1e}, x {rel(out[0], ref2[0]):.1e}")
     assert dH <= TOL and rel(out[0], ref2[0]) <= TOL
     assert hist_dev(out[1], ref2[1]) <= TOL and hist_dev(out[2], ref2[2]) <= TOL
     assert rel(hyb[0], hyb2[0]) <= TOL and hist_dev(hyb[2], hyb2[2]) <= TOL
@@ -71,13 +90,16 @@ def test_fused_ab_matches_two_pass_and_oracle(gpu_ctx, N, na, region):
     assert rel(out[0], xo) <= TOL and hist_dev(out[1], eo) <= TOL and hist_dev(out[2], ro) <= TOL
 
 
-def test_fused_region_overflow_falls_back(gpu_ctx):
-    """A 128 x 128 region at 47 angles is crossed by ~7,700 rays (> the 4,096 LDS accumulators):
+@pytest.mark.parametrize("kind", [0, 1])
+def test_fused_region_overflow_falls_back(gpu_ctx, kind):
+    """A 128 x 128 region at 47 angles is crossed by ~7,700 rays (> the 3,968 LDS accumulators of
+    the sub-chunk pass); a 64 x 64 region by ~3,900 (> the 1,984 ray slots of four row waves):
     the plan is refused and the two-pass path gives the result, bit for bit."""
     A, B, b, xt = _device_problem(gpu_ctx, 256, 47)
     with gpu_ctx.options(fused_ab=0):
         ref = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True)
-    with gpu_ctx.options(fused_ab=1, fused_region=128):
+    opts = _fused_opts(0, 128, 0, 0) if kind == 0 else _fused_opts(1, 64, 4, 8)
+    with gpu_ctx.options(**opts):
         out = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True)
     for a_, b_ in zip(out, ref):
         assert np.array_equal(np.asarray(a_), np.asarray(b_))
@@ -88,15 +110,17 @@ def test_fused_not_taken_for_unmatched_or_reference_order(gpu_ctx):
     the option changes nothing there."""
     P = tomo_problem(32, 16, noise=1e-2, seed=0, backprojector="pixel")
     outs = []
-    for f in (0, 1):
-        with gpu_ctx.options(fused_ab=f):
+    for f, kd in ((0, 1), (1, 0), (1, 1)):
+        with gpu_ctx.options(fused_ab=f, fused_kind=kd):
             outs.append(hgmres.ABgmres_nonhybrid_bounds(P.A, P.B, P.b, P.x_true, 0.0, 8, ctx=gpu_ctx, return_H=True))
-    for a_, b_ in zip(*outs):
-        assert np.array_equal(np.asarray(a_), np.asarray(b_))
+    for o in outs[1:]:
+        for a_, b_ in zip(outs[0], o):
+            assert np.array_equal(np.asarray(a_), np.asarray(b_))
 
 
+@pytest.mark.parametrize("kind", [0, 1])
 @pytest.mark.parametrize("world", [2, 4])
-def test_fused_on_pixel_shards(gpu_ctx, world):
+def test_fused_on_pixel_shards(gpu_ctx, world, kind):
     """The multi-GPU path (bench.py build_shard, DESIGN.md §5): rank g holds B_g = B(P_g,:), whole
     tile columns of the tiled pixels, and A_g = B_g'.  The one-pass A_g*(B_g*q) on each shard (its
     regions laid over the shard's window of pixel columns) matches the two-pass shard product, repeats
@@ -115,7 +139,7 @@ def test_fused_on_pixel_shards(gpu_ctx, world):
         A_g = B_g.T
         with gpu_ctx.options(fused_ab=0):
             bq2, ab2 = hgmres.spmv_ab(A_g, B_g, q)
-        with gpu_ctx.options(fused_ab=1):
+        with gpu_ctx.options(fused_ab=1, fused_kind=kind):
             bq1, ab1 = hgmres.spmv_ab(A_g, B_g, q)
             bq1b, ab1b = hgmres.spmv_ab(A_g, B_g, q)
         assert np.array_equal(ab1, ab1b) and np.array_equal(bq1, bq1b)
