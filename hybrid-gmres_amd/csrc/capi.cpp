@@ -522,6 +522,11 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             if (!(v == 4 || v == 8)) return bad("fused_group is 4 or 8");
             n.fused_group = (int)v;
             break;
+        case HGM_OPT_FUSED_DEPTH:
+            if (!(v == 2 || v == 3 || v == 4)) return bad("fused_depth is 2, 3 or 4");
+            n.fused_depth = (int)v;
+            break;
+        case HGM_OPT_FUSED_PAIRS: if (!b01) return bad("fused_pairs is 0 or 1"); n.fused_pairs = v != 0; break;
         default: return bad("unknown option");
     }
     return HGM_OK;
@@ -558,6 +563,8 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_FUSED_WREGION: *v = n.fused_wregion; break;
         case HGM_OPT_FUSED_WAVES: *v = n.fused_waves; break;
         case HGM_OPT_FUSED_GROUP: *v = n.fused_group; break;
+        case HGM_OPT_FUSED_DEPTH: *v = n.fused_depth; break;
+        case HGM_OPT_FUSED_PAIRS: *v = n.fused_pairs; break;
         default: return HGM_E_ARG;
     }
     return HGM_OK;

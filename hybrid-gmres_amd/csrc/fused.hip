@@ -60,8 +60,9 @@ static_assert(sizeof(FusedSub) == 32, "FusedSub layout");
 
 struct FusedPlan {
     int kind = 0;                 // 0 sub-chunk pass (k_fused_ab), 1 row-wave pass (k_fused_rw)
-    int region = 0, waves = 0, maxr = 0, group = 0;
-    int64_t nreg = 0, nsub = 0, nlr = 0, nslot = 0, m = 0;
+    int region = 0, waves = 0, maxr = 0, group = 0, depth = 0;
+    bool pairs = false;
+    int64_t nreg = 0, nsub = 0, nlr = 0, nslot = 0, m = 0, maxlen = 0;
     // kind 1: per (region, wave) a range of row runs; the region's rays; every entry's index
     // among its region's rays
     int32_t* wrun = nullptr;      // nreg * waves + 1
@@ -421,12 +422,28 @@ __device__ __forceinline__ double rows_sum_t(double (&P)[G]) {
     }
 }
 
-template <int W, int MAXR, int G, int NCH>
+// acc += t in the LDS unit (ds_add_f64, no return): the update needs no round trip, and the
+// LDS performs one wave's operations in issue order, so with a wave-private accumulator and
+// distinct addresses within each instruction (a pixel row meets a ray once; dummies are per lane)
+// the sums keep a fixed order: no atomicity is needed, only the read-modify-write in place.
+__device__ __forceinline__ void lds_add(double* p, double t) {
+    (void)__hip_atomic_fetch_add(p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+// DBG (timing experiments only, HGM_OPT_FUSED_DBG with the row-wave pass; results WRONG): bit 1
+// skips the q reads, 2 the accumulator updates, 4 the row-sum butterfly.
+// D: batches in the ring (D - 1 in flight while one is processed).  PR: two entries per lane (a
+// 16-byte value pair and a 4-byte slot pair per lane from the row's 16-byte-aligned start, chunks
+// of 128 entries): half the load instructions of one entry per lane (chunks of 64).
+template <int W, int MAXR, int G, int NCH, int D, bool PR, int DBG = 0>
 __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__ reg_base, const int32_t* __restrict__ ray_tab,
                                                      const int32_t* __restrict__ wrun, const int2* __restrict__ runs,
                                                      const int64_t* __restrict__ rp, const double* __restrict__ val,
                                                      const uint16_t* __restrict__ lidx, const double* __restrict__ q,
                                                      double* __restrict__ z, double* __restrict__ part) {
+    static_assert(D >= 2 && D <= 4, "ring depth");
+    constexpr int EPL = PR ? 2 : 1;              // entries per lane per chunk
+    constexpr int CH = 64 * EPL;                 // entries per chunk
     __shared__ double qloc[MAXR];           // (the last 64: the lanes' dummy slots)
     __shared__ double acc[W][MAXR];
     const int g = blockIdx.x;
@@ -469,8 +486,8 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     };
     struct RB {
         int r0, cnt;
-        int len[G];
-        double v[G][NCH];
+        int len[G], off[G];
+        double v[G][NCH][EPL];
         uint32_t s[G][NCH];
     };
     auto issue = [&](RB& b, int r0, int cnt, int64_t rpv) {
@@ -481,34 +498,58 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
             const int64_t e0 = readlane64(rpv, min(j, cnt)), e1 = readlane64(rpv, min(j + 1, cnt));
             const int len = (int)(e1 - e0);
             b.len[j] = len;
-            const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + e0, len * 8);
-            const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lidx + e0, len * 2);
+            if constexpr (PR) {
+                const int64_t ea = e0 & ~int64_t(1);
+                const int off = (int)(e0 & 1), span = (len + off + 1) & ~1;
+                b.off[j] = off;
+                const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + ea, span * 8);
+                const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lidx + ea, span * 2);
 #pragma unroll
-            for (int c = 0; c < NCH; ++c) {
-                b.v[j][c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, (ln + 64 * c) * 8, 0, 2));
-                b.s[j][c] = (uint32_t)__builtin_bit_cast(uint16_t, __builtin_amdgcn_raw_buffer_load_b16(rl, (ln + 64 * c) * 2, 0, 2));
+                for (int c = 0; c < NCH; ++c) {
+                    const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, (2 * ln + CH * c) * 8, 0, 2));
+                    b.v[j][c][0] = t.x;
+                    b.v[j][c][EPL - 1] = t.y;
+                    b.s[j][c] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, (2 * ln + CH * c) * 2, 0, 2);
+                }
+            } else {
+                b.off[j] = 0;
+                const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + e0, len * 8);
+                const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lidx + e0, len * 2);
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) {
+                    b.v[j][c][0] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, (ln + CH * c) * 8, 0, 2));
+                    b.s[j][c] = (uint32_t)__builtin_bit_cast(uint16_t, __builtin_amdgcn_raw_buffer_load_b16(rl, (ln + CH * c) * 2, 0, 2));
+                }
             }
         }
     };
-    // Branch-free: lanes past a row's end hold v = 0 (the buffer range) and are pointed at a
-    // private dummy slot (MAXR - 64 + lane, q = 0), so every row issues the same instructions and the
-    // compiler can interleave the G rows' product and reduction chains (a branch would end the
-    // basic block).  The accumulator updates stay in row order (consecutive rows share rays).
+    // Branch-free: entries outside the row (past its end; with PR also the previous row's entry
+    // in the first pair) are pointed at the lane's private dummy slot (MAXR - 64 + lane, q = 0),
+    // so every row issues the same instructions and the compiler can interleave the G rows'
+    // product and reduction chains (a branch would end the basic block).  The accumulator
+    // updates stay in row order (consecutive rows share rays).
     auto process = [&](RB& b) {
         double P[G];
-        uint32_t k[G][NCH];
+        uint32_t k[G][NCH][EPL];
 #pragma unroll
         for (int j = 0; j < G; ++j) {
             double p = 0.0;
 #pragma unroll
-            for (int c = 0; c < NCH; ++c) {
-                k[j][c] = ln + 64 * c < b.len[j] ? b.s[j][c] : (uint32_t)(MAXR - 64 + ln);
-                p += b.v[j][c] * qloc[k[j][c]];
-            }
+            for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                for (int e = 0; e < EPL; ++e) {
+                    const int pos = EPL * ln + CH * c + e - b.off[j];
+                    const uint32_t sl = PR ? (e ? b.s[j][c] >> 16 : b.s[j][c] & 0xffffu) : b.s[j][c];
+                    k[j][c][e] = (uint32_t)pos < (uint32_t)b.len[j] ? sl : (uint32_t)(MAXR - 64 + ln);
+                    if constexpr (DBG & 1) p += b.v[j][c][e] * (double)k[j][c][e];
+                    else p += b.v[j][c][e] * qloc[k[j][c][e]];
+                }
             P[j] = p;
         }
         constexpr int GL = 64 / G;                // lanes per row sum after the butterfly
-        const double S = rows_sum_t<G>(P);        // lane l: z of row l / GL
+        double S;                                 // lane l: z of row l / GL
+        if constexpr (DBG & 4) S = P[0] + P[G - 1];
+        else S = rows_sum_t<G>(P);
         {   // z out: each group's first lane, rows past cnt fall outside the range
             const __amdgpu_buffer_rsrc_t rz = buf_rsrc(z + b.r0, b.cnt * 8);
             buf_store(S, rz, (ln & (GL - 1)) == 0 ? (ln / GL) * 8 : (1 << 30));
@@ -517,37 +558,45 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
         for (int j = 0; j < G; ++j) {
             const double sj = lane_bcast(S, j * GL);
 #pragma unroll
-            for (int c = 0; c < NCH; ++c) {
-                const double t = b.v[j][c] * sj;
-                ac[k[j][c]] = ac[k[j][c]] + t;
-            }
+            for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                for (int e = 0; e < EPL; ++e) {
+                    const double t = b.v[j][c][e] * sj;
+                    if constexpr (DBG & 2) S += t;
+                    else lds_add(&ac[k[j][c][e]], t);
+                }
         }
     };
-    RB b0, b1;
-    int a0, c0, a1, c1;
-    next(a0, c0);
-    int64_t rA = load_rp(a0, c0);
-    next(a1, c1);
-    int64_t rB = load_rp(a1, c1);
-    issue(b0, a0, c0, rA);
-    // one exit, at the bottom: the two halves keep their register sets (a rotated loop with two
-    // exits had the compiler copy in-flight batches, waiting for them); an empty batch is
-    // processed as a no-op (zero-length ranges, dummy slots)
-    // (sched_barrier: the scheduler would sink the next batch's loads into the processing)
+    // Ring of D batches: while batch i is processed, batches i+1 .. i+D-1 are in flight and the
+    // row pointers of batch i+D load.  The loop is unrolled by D so every ring index is static
+    // (registers; a register copy of an in-flight load would force a wait), with one exit at the
+    // bottom (a rotated loop with two exits had the compiler copy in-flight batches); an empty
+    // batch is processed as a no-op (zero-length ranges, dummy slots).  sched_barrier: the
+    // scheduler would sink the next batch's loads into the processing.
+    RB b[D];
+    int a[D], cn[D];
+    int64_t r[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        next(a[i], cn[i]);
+        r[i] = load_rp(a[i], cn[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < D - 1; ++i) issue(b[i], a[i], cn[i], r[i]);
     do {
-        next(a0, c0);
-        rA = load_rp(a0, c0);
-        issue(b1, a1, c1, rB);
-        __builtin_amdgcn_sched_barrier(0);
-        process(b0);
-        __builtin_amdgcn_sched_barrier(0);
-        next(a1, c1);
-        rB = load_rp(a1, c1);
-        issue(b0, a0, c0, rA);
-        __builtin_amdgcn_sched_barrier(0);
-        process(b1);
-        __builtin_amdgcn_sched_barrier(0);
-    } while (b0.cnt > 0);
+#pragma unroll
+        for (int t = 0; t < D; ++t) {
+            // the row pointers of batch i+D first: issuing batch i+D-1 then waits only for its
+            // own row pointers (loaded before batch i+D-2's entries), not for the entries
+            const int ti = (t + D - 1) % D;
+            next(a[t], cn[t]);
+            r[t] = load_rp(a[t], cn[t]);
+            issue(b[ti], a[ti], cn[ti], r[ti]);
+            __builtin_amdgcn_sched_barrier(0);
+            process(b[t]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } while (b[0].cnt > 0);
     __syncthreads();
     for (int k = threadIdx.x; k < nr; k += 64 * W) {
         double t = acc[0][k];
@@ -812,9 +861,15 @@ FusedPlan* fused_plan_build(hgm_ctx* c, const hgm_mat* B, int R) {
 // contiguous share (by entries) of the region's rows in stored order, as runs of consecutive
 // rows; each entry gets its ray's index among the region's rays (sorted ray ids).
 namespace {
-constexpr int RW_MAXR[] = {1024, 2048, 4096};   // LDS slots of the instantiated kernels (64 of them dummies)
-constexpr int RW_NCH_MAX = 4;                     // chunks of 64 entries per row (rows <= 256)
+// (waves, LDS ray slots) of the instantiated kernels, 64 slots of each being the lanes' dummies;
+// the plan takes the fewest slots that hold its regions' rays (more workgroups per CU)
+#define HGM_RW_SHAPES(X) X(1, 1088) X(1, 2048) X(1, 4096) X(2, 1088) X(2, 1536) X(2, 2048) X(2, 4096) \
+    X(4, 1088) X(4, 1344) X(4, 1536) X(4, 2048)
+constexpr int RW_SLOTS_MAX = 4096;
+constexpr int RW_ROW_MAX = 255;                   // entries per pixel row (two chunks of 128, pairs)
 }  // namespace
+
+static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, bool dry);
 
 FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G) {
     HGM_REQUIRE(B->dtype == HGM_F64, "fused A*(B*q): fp64 operators");
@@ -830,7 +885,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
     if (nnz) HGM_HIP(hipMemcpy(ci.data(), B->ci, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
     int64_t maxlen = 0;
     for (int64_t s = 0; s < n; ++s) maxlen = std::max(maxlen, rp[s + 1] - rp[s]);
-    HGM_REQUIRE(maxlen <= 64 * RW_NCH_MAX, "fused A*(B*q): a pixel row longer than the row-wave pass takes");
+    HGM_REQUIRE(maxlen <= RW_ROW_MAX, "fused A*(B*q): a pixel row longer than the row-wave pass takes");
     // runs of consecutive stored rows of one region, per region in stored order
     std::vector<std::vector<int2>> rr(nreg);
     for (int64_t s = 0; s < n; ++s) {
@@ -881,7 +936,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
                     rs.erase(std::unique(rs.begin(), rs.end()), rs.end());
                     int cur = worst.load();
                     while ((int)rs.size() > cur && !worst.compare_exchange_weak(cur, (int)rs.size())) {}
-                    if (rs.size() > (size_t)RW_MAXR[2] - 64) continue;
+                    if (rs.size() > (size_t)RW_SLOTS_MAX - 64) continue;
                     for (size_t k = 0; k < rs.size(); ++k) map[rs[k]] = (int32_t)k;
                     for (const int2& r : rr[g])
                         for (int64_t e = rp[r.x]; e < rp[r.x + r.y]; ++e) lidx[e] = (uint16_t)map[ci[e]];
@@ -891,14 +946,11 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
         for (auto& t : th) t.join();
     }
     int maxr = 0;
-    for (int mr : RW_MAXR)
-        if (worst.load() <= mr - 64) {
-            maxr = mr;
-            break;
-        }
-    HGM_REQUIRE(maxr > 0, "fused A*(B*q): a region is crossed by more rays than the LDS holds");
-    HGM_REQUIRE((int64_t)(1 + W) * maxr * 8 <= 160 * 1024 && !(W == 4 && maxr > 2048),
-                "fused A*(B*q): region rays x waves exceed the LDS");
+#define HGM_RW_PICK(WV, MRV) \
+    if (W == WV && worst.load() <= MRV - 64 && (maxr == 0 || MRV < maxr)) maxr = MRV;
+    HGM_RW_SHAPES(HGM_RW_PICK)
+#undef HGM_RW_PICK
+    HGM_REQUIRE(maxr > 0, "fused A*(B*q): a region is crossed by more rays than the LDS of its waves holds");
     std::vector<int64_t> reg_base(nreg + 1, 0);
     for (int64_t g = 0; g < nreg; ++g) reg_base[g + 1] = reg_base[g] + (int64_t)rrays[g].size();
     const int64_t nslot = reg_base[nreg];
@@ -922,8 +974,10 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
         P->region = R;
         P->waves = W;
         P->group = G;
+        P->depth = c->num.fused_depth;
+        P->pairs = c->num.fused_pairs;
         P->maxr = maxr;
-        P->nsub = (maxlen + 63) / 64;      // (kind 1: chunks of 64 entries per row)
+        P->maxlen = maxlen;
         P->nreg = nreg;
         P->nslot = nslot;
         P->m = m;
@@ -940,8 +994,11 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
         fused_plan_free(P);
         throw;
     }
-    (void)c;
     P->build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!fused_rw_launch(c, B, P, nullptr, nullptr, true)) {
+        fused_plan_free(P);
+        throw Error{HGM_E_ARG, "fused A*(B*q): no row-wave kernel for this plan's shape and the options"};
+    }
     if (std::getenv("HGM_FUSED_VERBOSE"))
         std::fprintf(stderr, "[fused rw plan] region %d waves %d group %d: %lld regions, %lld slots, max rays %d (LDS slots %d), longest row %lld, %d runs, %.2f s\n",
                      R, W, G, (long long)nreg, (long long)nslot, worst.load(), maxr, (long long)maxlen, wrun.back(), P->build_s);
@@ -966,7 +1023,8 @@ const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
     const bool rw = nu.fused_kind == 1;
     auto stale = [&](const FusedPlan* P) {
         if (P->kind != (rw ? 1 : 0)) return true;
-        return rw ? (P->region != nu.fused_wregion || P->waves != nu.fused_waves || P->group != nu.fused_group)
+        return rw ? (P->region != nu.fused_wregion || P->waves != nu.fused_waves || P->group != nu.fused_group ||
+                     P->depth != nu.fused_depth || P->pairs != nu.fused_pairs)
                   : P->region != nu.fused_region;
     };
     if (Bm->fused && stale(Bm->fused)) {
@@ -988,23 +1046,54 @@ const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
 
 // kind 1: the row-wave kernel instantiated for the plan's waves, LDS ray slots, row batch and
 // chunks per row
-static void fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq) {
-    const int W = P->waves, MR = P->maxr, G = P->group, NC = P->nsub <= 2 ? 2 : 4;
-#define HGM_RW(WV, MRV, GV, NCV)                                                                                   \
-    if (W == WV && MR == MRV && G == GV && NC == NCV) {                                                            \
-        launch(c, false, k_fused_rw<WV, MRV, GV, NCV>, dim3((unsigned)P->nreg), dim3(64 * WV),                      \
-               (const int64_t*)P->reg_base, (const int32_t*)P->ray_tab, (const int32_t*)P->wrun,                  \
-               (const int2*)P->runs, (const int64_t*)B->rp, (const double*)B->val, (const uint16_t*)P->lidx, q, Bq, \
-               P->part);                                                                                            \
-        return;                                                                                                     \
+// Launch the instantiation for the plan and the options (dry: only report whether one exists;
+// the plan is refused at build time when none does, so the two-pass path runs instead).
+static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, bool dry) {
+    const int W = P->waves, MR = P->maxr, G = P->group, D = c->num.fused_depth;
+    const bool PRm = c->num.fused_pairs;
+    // chunks per row: 64 entries (128 with pairs, whose first pair may start one entry early)
+    const int64_t ml = P->maxlen + (PRm ? 1 : 0);
+    const int NC = ml <= (PRm ? 128 : 64) ? 1 : ml <= (PRm ? 256 : 128) ? 2 : 4;
+    const int dbg = c->num.fused_dbg;
+#define HGM_RWL(WV, MRV, GV, NCV, DV, PV, DBV)                                                                       \
+    {                                                                                                                 \
+        if (!dry)                                                                                                     \
+            launch(c, false, k_fused_rw<WV, MRV, GV, NCV, DV, PV, DBV>, dim3((unsigned)P->nreg), dim3(64 * WV),     \
+                   (const int64_t*)P->reg_base, (const int32_t*)P->ray_tab, (const int32_t*)P->wrun,              \
+                   (const int2*)P->runs, (const int64_t*)B->rp, (const double*)B->val, (const uint16_t*)P->lidx, q, \
+                   Bq, P->part);                                                                                    \
+        return true;                                                                                                  \
     }
-#define HGM_RW_G(WV, MRV) HGM_RW(WV, MRV, 4, 2) HGM_RW(WV, MRV, 8, 2) HGM_RW(WV, MRV, 4, 4) HGM_RW(WV, MRV, 8, 4)
-    HGM_RW_G(1, 1024) HGM_RW_G(1, 2048) HGM_RW_G(1, 4096)
-    HGM_RW_G(2, 1024) HGM_RW_G(2, 2048) HGM_RW_G(2, 4096)
-    HGM_RW_G(4, 1024) HGM_RW_G(4, 2048)
-#undef HGM_RW_G
+    if (dbg) {   // timing experiments: the default shape only
+        if (W == 4 && MR == 2048 && G == 8 && NC == 1 && PRm && D == 2) {
+#define HGM_RWD(DV) if (dbg == DV) HGM_RWL(4, 2048, 8, 1, 2, true, DV)
+            HGM_RWD(1) HGM_RWD(2) HGM_RWD(3) HGM_RWD(4) HGM_RWD(5) HGM_RWD(6) HGM_RWD(7)
+#undef HGM_RWD
+        }
+        if (dry) return false;
+        throw Error{HGM_E_ARG, "fused_dbg with the row-wave pass: waves 4, 2048 slots, 8 rows, pairs, depth 2, one chunk"};
+    }
+    // production: pairs, 8-row batches, depth 2 (every shape, 1 or 2 chunks); the other
+    // variants for the default shape only (measurements)
+#define HGM_RW(WV, MRV)                                                                                              \
+    if (W == WV && MR == MRV && G == 8 && PRm && D == 2) {                                                           \
+        if (NC == 1) HGM_RWL(WV, MRV, 8, 1, 2, true, 0)                                                             \
+        if (NC == 2) HGM_RWL(WV, MRV, 8, 2, 2, true, 0)                                                             \
+    }
+    HGM_RW_SHAPES(HGM_RW)
 #undef HGM_RW
-    throw Error{HGM_E_ARG, "fused A*(B*q): no row-wave kernel for this plan"};
+    if (W == 4 && MR == 2048 && NC == 1 && PRm) {
+        if (G == 8 && D == 3) HGM_RWL(4, 2048, 8, 1, 3, true, 0)
+        if (G == 4 && D == 2) HGM_RWL(4, 2048, 4, 1, 2, true, 0)
+        if (G == 4 && D == 3) HGM_RWL(4, 2048, 4, 1, 3, true, 0)
+    }
+    if (W == 4 && MR == 2048 && NC == 2 && !PRm && D == 2) {
+        if (G == 8) HGM_RWL(4, 2048, 8, 2, 2, false, 0)
+        if (G == 4) HGM_RWL(4, 2048, 4, 2, 2, false, 0)
+    }
+#undef HGM_RWL
+    if (dry) return false;
+    throw Error{HGM_E_ARG, "fused A*(B*q): no row-wave kernel for this plan and options"};
 }
 
 // Bq = B*q (n), ABq = A*(B*q) (m), one pass over B.
@@ -1012,7 +1101,7 @@ void fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q,
     hipEvent_t t0 = nullptr;
     timing_begin(c, KC_FUSED, &t0);
     if (P->kind == 1) {
-        fused_rw_launch(c, B, P, q, Bq);
+        fused_rw_launch(c, B, P, q, Bq, false);
     } else {
 #define HGM_FUSED_LAUNCH(FB, FGV, PFV)                                                                          \
     launch(c, false, k_fused_ab<FB, FGV, PFV>, dim3((unsigned)P->nreg), dim3(FB), (const FusedSub*)P->subs,      \

@@ -85,6 +85,8 @@ struct Numerics {
     int fused_wregion = 32;         // ... row-wave pass: pixel square per workgroup
     int fused_waves = 4;            // ... row-wave pass: waves per workgroup (1, 2, 4)
     int fused_group = 8;            // ... row-wave pass: rows per load batch (4, 8)
+    int fused_depth = 2;            // ... row-wave pass: batches in the load ring (2..4)
+    bool fused_pairs = true;        // ... row-wave pass: two entries per lane
     int krylov_pad = -1;            // Krylov basis column padding (elements; -1 auto, kernels.hip krylov_ld)
     int fused_dbg = 0;              // ... timing experiments: skip phases (wrong results)
 };

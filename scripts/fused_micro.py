@@ -34,10 +34,14 @@ for vname in variants:
     # two | f<threads>[x<depth>][r<region>] (fused, pipeline depth [2], region side [64])
     # | d<bits> (phase-skip timing)
     mf = re.fullmatch(r"f(\d+)(?:x(\d))?(?:r(\d+))?", vname)
-    mw = re.fullmatch(r"w(\d)r(\d+)(?:g(\d))?", vname)      # row-wave pass: waves, region, rows per batch
-    if mw:
+    # row-wave pass: waves, region, rows per batch, ring depth, pairs
+    mw = re.fullmatch(r"w(\d)r(\d+)(?:g(\d))?(?:d(\d))?(?:p(\d))?", vname)
+    if vname.startswith("e"):                                   # row-wave pass, phase-skip timing
+        o = dict(fused_ab=1, fused_kind=1, fused_dbg=int(vname[1:]))
+    elif mw:
         o = dict(fused_ab=1, fused_kind=1, fused_waves=int(mw.group(1)), fused_wregion=int(mw.group(2)),
-                 fused_group=int(mw.group(3) or 4))
+                 fused_group=int(mw.group(3) or 8), fused_depth=int(mw.group(4) or 2),
+                 fused_pairs=int(mw.group(5) or 1))
     elif vname == "two":
         o = dict(fused_ab=0)
     elif mf:

@@ -42,27 +42,32 @@ def _device_problem(ctx, N, na, seed=0):
     return A, A.T, b0 + e / np.linalg.norm(e) * 1e-2 * np.linalg.norm(b0), xt
 
 
-# (N, angles, kind, region, waves, rows per batch): kind 0 the sub-chunk pass (fused_region),
-# kind 1 the row-wave pass (fused_wregion / fused_waves / fused_group)
-CASES = [(512, 30, 0, 64, 0, 0), (100, 17, 0, 64, 0, 0), (256, 47, 0, 32, 0, 0), (256, 47, 0, 16, 0, 0),
-         (128, 90, 0, 24, 0, 0),
-         (512, 30, 1, 32, 4, 8), (100, 17, 1, 32, 4, 4), (256, 47, 1, 24, 4, 8), (256, 47, 1, 16, 1, 8),
-         (256, 47, 1, 32, 2, 4), (128, 90, 1, 16, 2, 8), (200, 60, 1, 20, 1, 4)]
+# (N, angles, kind, region, waves, rows per batch, ring depth, pairs): kind 0 the sub-chunk pass
+# (fused_region), kind 1 the row-wave pass (fused_wregion / _waves / _group / _depth / _pairs);
+# the row-wave variants other than the default (8 rows, depth 2, pairs) exist for 4 waves and
+# <= 1,984 rays per region (the 32 x 32 regions at 47 angles)
+CASES = [(512, 30, 0, 64, 0, 0, 0, 0), (100, 17, 0, 64, 0, 0, 0, 0), (256, 47, 0, 32, 0, 0, 0, 0),
+         (256, 47, 0, 16, 0, 0, 0, 0), (128, 90, 0, 24, 0, 0, 0, 0),
+         (512, 30, 1, 32, 4, 8, 2, 1), (100, 17, 1, 32, 4, 8, 2, 1), (256, 47, 1, 24, 4, 8, 2, 1),
+         (256, 47, 1, 16, 1, 8, 2, 1), (256, 47, 1, 32, 2, 8, 2, 1), (128, 90, 1, 16, 2, 8, 2, 1),
+         (200, 60, 1, 20, 1, 8, 2, 1), (256, 47, 1, 32, 4, 4, 3, 1), (256, 47, 1, 32, 4, 8, 3, 1),
+         (256, 47, 1, 32, 4, 4, 2, 1), (256, 47, 1, 32, 4, 8, 2, 0), (256, 47, 1, 32, 4, 4, 2, 0)]
 
 
-def _fused_opts(kind, region, waves, group):
+def _fused_opts(kind, region, waves=4, group=8, depth=2, pairs=1):
     if kind == 0:
         return dict(fused_ab=1, fused_kind=0, fused_region=region)
-    return dict(fused_ab=1, fused_kind=1, fused_wregion=region, fused_waves=waves, fused_group=group)
+    return dict(fused_ab=1, fused_kind=1, fused_wregion=region, fused_waves=waves, fused_group=group,
+                fused_depth=depth, fused_pairs=pairs)
 
 
-@pytest.mark.parametrize("N,na,kind,region,waves,group", CASES)
-def test_fused_ab_matches_two_pass_and_oracle(gpu_ctx, N, na, kind, region, waves, group):
+@pytest.mark.parametrize("N,na,kind,region,waves,group,depth,pairs", CASES)
+def test_fused_ab_matches_two_pass_and_oracle(gpu_ctx, N, na, kind, region, waves, group, depth, pairs):
     A, B, b, xt = _device_problem(gpu_ctx, N, na)
     k = 20
     with gpu_ctx.options(fused_ab=0):
         ref2 = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
-    with gpu_ctx.options(**_fused_opts(kind, region, waves, group)):
+    with gpu_ctx.options(**_fused_opts(kind, region, waves, group, depth, pairs)):
         out = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
         again = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
         hyb = hgmres.ABgmres_hybrid_bounds(A, B, b, xt, 0.0, k, 1e-2, ctx=gpu_ctx, return_H=True)
@@ -76,7 +81,8 @@ def test_fused_ab_matches_two_pass_and_oracle(gpu_ctx, N, na, kind, region, wave
     for a_, b_ in zip(out, again):
         assert np.array_equal(np.asarray(a_), np.asarray(b_))               # bitwise reproducible
     dH = float(np.max(np.abs(out[-1] - ref2[-1])) / np.max(np.abs(ref2[-1])))
-    print(f"[fused N={N} angles={na} kind={kind} region={region} waves={waves} group={group}] "
+    print(f"[fused N={N} angles={na} kind={kind} region={region} waves={waves} group={group} depth={depth} "
+          f"pairs={pairs}] "
           f"|dH| vs two-pass {dH:.1e}, x {rel(out[0], ref2[0]):.1e}")
     assert dH <= TOL and rel(out[0], ref2[0]) <= TOL
     assert hist_dev(out[1], ref2[1]) <= TOL and hist_dev(out[2], ref2[2]) <= TOL
@@ -98,7 +104,7 @@ def test_fused_region_overflow_falls_back(gpu_ctx, kind):
     A, B, b, xt = _device_problem(gpu_ctx, 256, 47)
     with gpu_ctx.options(fused_ab=0):
         ref = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True)
-    opts = _fused_opts(0, 128, 0, 0) if kind == 0 else _fused_opts(1, 64, 4, 8)
+    opts = _fused_opts(0, 128) if kind == 0 else _fused_opts(1, 64)
     with gpu_ctx.options(**opts):
         out = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True)
     for a_, b_ in zip(out, ref):
