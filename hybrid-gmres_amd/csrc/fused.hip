@@ -479,10 +479,10 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
             o = 0;
         }
     };
-    // row pointers of a batch: lane j <= cnt holds rp[r0 + j]
+    // row pointers of a batch: lane j holds rp[r0 + min(j, cnt)] (rows past cnt are empty)
     auto load_rp = [&](int r0, int cnt) -> int64_t {
         const __amdgpu_buffer_rsrc_t r = buf_rsrc(rp + r0, (cnt + 1) * 8);
-        return __builtin_bit_cast(int64_t, __builtin_amdgcn_raw_buffer_load_b64(r, min(ln, G) * 8, 0, 0));
+        return __builtin_bit_cast(int64_t, __builtin_amdgcn_raw_buffer_load_b64(r, min(ln, cnt) * 8, 0, 0));
     };
     struct RB {
         int r0, cnt;
@@ -493,25 +493,37 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     auto issue = [&](RB& b, int r0, int cnt, int64_t rpv) {
         b.r0 = r0;
         b.cnt = cnt;
+        // (pairs) the batch's entries from its first row's first pair; inside a batch the row
+        // pointers are 32-bit offsets from it
+        const int64_t eb = readlane64(rpv, 0) & ~int64_t(1);
+        const int bspan = PR ? (int)((readlane64(rpv, G) - eb + 1) & ~int64_t(1)) : 0;
+        const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + eb, bspan * 8);
+        const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lidx + eb, bspan * 2);
 #pragma unroll
         for (int j = 0; j < G; ++j) {
-            const int64_t e0 = readlane64(rpv, min(j, cnt)), e1 = readlane64(rpv, min(j + 1, cnt));
-            const int len = (int)(e1 - e0);
-            b.len[j] = len;
             if constexpr (PR) {
-                const int64_t ea = e0 & ~int64_t(1);
-                const int off = (int)(e0 & 1), span = (len + off + 1) & ~1;
+                // one resource per batch (its rows are consecutive): a row is an SGPR offset into
+                // it, and the lanes past the row's last pair get an offset past every range (no
+                // memory access, zeros), instead of a resource of their own per row
+                const int64_t e0 = readlane64(rpv, j), e1 = readlane64(rpv, j + 1);
+                const int len = (int)(e1 - e0);
+                b.len[j] = len;
+                const int off = (int)(e0 & 1);
+                const int rel = (int)(e0 - eb) - off;            // even: the row's first pair
                 b.off[j] = off;
-                const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + ea, span * 8);
-                const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lidx + ea, span * 2);
 #pragma unroll
                 for (int c = 0; c < NCH; ++c) {
-                    const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, (2 * ln + CH * c) * 8, 0, 2));
+                    const bool in = 2 * ln + CH * c < len + off;
+                    const int vo = in ? (2 * ln + CH * c) * 8 : (1 << 30), lo = in ? (2 * ln + CH * c) * 2 : (1 << 30);
+                    const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, vo, rel * 8, 2));
                     b.v[j][c][0] = t.x;
                     b.v[j][c][EPL - 1] = t.y;
-                    b.s[j][c] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, (2 * ln + CH * c) * 2, 0, 2);
+                    b.s[j][c] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, lo, rel * 2, 2);
                 }
             } else {
+                const int64_t e0 = readlane64(rpv, j), e1 = readlane64(rpv, j + 1);
+                const int len = (int)(e1 - e0);
+                b.len[j] = len;
                 b.off[j] = 0;
                 const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + e0, len * 8);
                 const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lidx + e0, len * 2);
