@@ -513,7 +513,10 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                 b.off[j] = off;
 #pragma unroll
                 for (int c = 0; c < NCH; ++c) {
-                    const bool in = 2 * ln + CH * c < len + off;
+#ifndef HGM_RW_MASK_LOADS
+#define HGM_RW_MASK_LOADS 1
+#endif
+                    const bool in = !HGM_RW_MASK_LOADS || 2 * ln + CH * c < len + off;
                     const int vo = in ? (2 * ln + CH * c) * 8 : (1 << 30), lo = in ? (2 * ln + CH * c) * 2 : (1 << 30);
                     const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, vo, rel * 8, 2));
                     b.v[j][c][0] = t.x;

@@ -1,0 +1,14 @@
+#!/bin/bash
+# A/B of experiment builds of libhgmres (HGM_LIB) on the C4 fused pass micro-benchmark,
+# alternating library / default twice.
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=gpurun_out/r3libab
+mkdir -p $O
+for rep in 1 2; do
+  for lib in default $LIBS; do
+    if [ $lib = default ]; then unset HGM_LIB; else export HGM_LIB=$PWD/exp/$lib; fi
+    timeout -k 10 300 python -u scripts/fused_micro.py 4096 47 20 ${VARIANTS:-w4r32g8d2p1} > $O/$lib.$rep.log 2>&1 || { tail -20 $O/$lib.$rep.log; exit 1; }
+    grep '^{' $O/$lib.$rep.log | sed "s/^/$lib /"
+  done
+done
