@@ -68,7 +68,7 @@ struct FusedPlan {
     int32_t* wrun = nullptr;      // nreg * waves + 1
     int2* runs = nullptr;         // (first row, rows)
     int32_t* ray_tab = nullptr;   // nslot: global ray of each region-local ray
-    uint16_t* lidx = nullptr;     // nnz (+ padding)
+    uint16_t* lidx = nullptr;     // nnz (+ padding): the slot as an LDS byte offset (index * 8)
     int32_t* reg_sub = nullptr;   // nreg+1
     int64_t* reg_base = nullptr;  // nreg+1
     FusedSub* subs = nullptr;     // nsub
@@ -553,11 +553,14 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
             for (int c = 0; c < NCH; ++c)
 #pragma unroll
                 for (int e = 0; e < EPL; ++e) {
-                    const int pos = EPL * ln + CH * c + e - b.off[j];
+                    // slots are LDS byte offsets (the plan stores slot * 8); pos0 is the lane's first
+                    // entry in the row (-1: the previous row's last entry in the first pair)
+                    const int pos0 = EPL * ln + CH * c - b.off[j];
+                    const bool ok = e == 0 ? (uint32_t)pos0 < (uint32_t)b.len[j] : pos0 < b.len[j] - 1;
                     const uint32_t sl = PR ? (e ? b.s[j][c] >> 16 : b.s[j][c] & 0xffffu) : b.s[j][c];
-                    k[j][c][e] = (uint32_t)pos < (uint32_t)b.len[j] ? sl : (uint32_t)(MAXR - 64 + ln);
+                    k[j][c][e] = ok ? sl : (uint32_t)(MAXR - 64 + ln) * 8u;
                     if constexpr (DBG & 1) p += b.v[j][c][e] * (double)k[j][c][e];
-                    else p += b.v[j][c][e] * qloc[k[j][c][e]];
+                    else p += b.v[j][c][e] * *reinterpret_cast<const double*>(reinterpret_cast<const char*>(qloc) + k[j][c][e]);
                 }
             P[j] = p;
         }
@@ -578,7 +581,7 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                 for (int e = 0; e < EPL; ++e) {
                     const double t = b.v[j][c][e] * sj;
                     if constexpr (DBG & 2) S += t;
-                    else lds_add(&ac[k[j][c][e]], t);
+                    else lds_add(reinterpret_cast<double*>(reinterpret_cast<char*>(ac) + k[j][c][e]), t);
                 }
         }
     };
@@ -954,7 +957,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
                     if (rs.size() > (size_t)RW_SLOTS_MAX - 64) continue;
                     for (size_t k = 0; k < rs.size(); ++k) map[rs[k]] = (int32_t)k;
                     for (const int2& r : rr[g])
-                        for (int64_t e = rp[r.x]; e < rp[r.x + r.y]; ++e) lidx[e] = (uint16_t)map[ci[e]];
+                        for (int64_t e = rp[r.x]; e < rp[r.x + r.y]; ++e) lidx[e] = (uint16_t)(map[ci[e]] * 8);
                     for (int32_t ray : rs) map[ray] = -1;
                 }
             });
