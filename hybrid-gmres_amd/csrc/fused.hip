@@ -78,6 +78,7 @@ struct FusedPlan {
     int64_t* rs_ptr = nullptr;    // m+1
     int32_t* rs_slot = nullptr;   // nslot
     double* part = nullptr;       // nslot
+    double* zx_part = nullptr;    // kind 1: nreg (the regions' shares of the side dot x_true'(B*q))
     double build_s = 0;
 };
 
@@ -85,7 +86,7 @@ void fused_plan_free(FusedPlan* P) {
     if (!P) return;
     for (void* p : {(void*)P->reg_sub, (void*)P->reg_base, (void*)P->subs, (void*)P->perm, (void*)P->lr_ray,
                     (void*)P->lr_pk, (void*)P->rs_ptr, (void*)P->rs_slot, (void*)P->part, (void*)P->wrun,
-                    (void*)P->runs, (void*)P->ray_tab, (void*)P->lidx})
+                    (void*)P->runs, (void*)P->ray_tab, (void*)P->lidx, (void*)P->zx_part})
         if (p) (void)hipFree(p);
     delete P;
 }
@@ -330,10 +331,18 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(D <= 2 ? FB
 #ifndef HGM_FUSED_RG
 #define HGM_FUSED_RG 8
 #endif
+// With zx_out, block 0 first adds the nzx regional shares of the side dot x_true'(B*q) (fixed
+// order) into *zx_out.
 template <int RG>
 __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* __restrict__ rs_ptr,
                                                      const int32_t* __restrict__ rs_slot,
-                                                     const double* __restrict__ part, double* __restrict__ w) {
+                                                     const double* __restrict__ part, double* __restrict__ w,
+                                                     const double* __restrict__ zx_part, int nzx, double* zx_out) {
+    if (zx_out && blockIdx.x == 0) {
+        __shared__ double sh[4];
+        const double t = reduce_parts<double, false>(zx_part, nzx, sh);
+        if (threadIdx.x == 0) st_sys(zx_out, t);           // (the host ring: system scope, device_common.h)
+    }
     const int gl = threadIdx.x % RG;
     for (int64_t i = ((int64_t)blockIdx.x * BS + threadIdx.x) / RG; i < m; i += (int64_t)gridDim.x * (BS / RG)) {
         double s = 0.0;
@@ -440,7 +449,8 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                                                      const int32_t* __restrict__ wrun, const int2* __restrict__ runs,
                                                      const int64_t* __restrict__ rp, const double* __restrict__ val,
                                                      const uint16_t* __restrict__ lidx, const double* __restrict__ q,
-                                                     double* __restrict__ z, double* __restrict__ part) {
+                                                     double* __restrict__ z, double* __restrict__ part,
+                                                     const double* __restrict__ xt, double* __restrict__ zx_part) {
     static_assert(D >= 2 && D <= 4, "ring depth");
     constexpr int EPL = PR ? 2 : 1;              // entries per lane per chunk
     constexpr int CH = 64 * EPL;                 // entries per chunk
@@ -484,15 +494,21 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
         const __amdgpu_buffer_rsrc_t r = buf_rsrc(rp + r0, (cnt + 1) * 8);
         return __builtin_bit_cast(int64_t, __builtin_amdgcn_raw_buffer_load_b64(r, min(ln, cnt) * 8, 0, 0));
     };
+    constexpr int GL = 64 / G;                    // lanes per row sum after the butterfly
     struct RB {
         int r0, cnt;
         int len[G], off[G];
         double v[G][NCH][EPL];
         uint32_t s[G][NCH];
+        double xv;                                // x_true of row l / GL at lane l (side dot)
     };
     auto issue = [&](RB& b, int r0, int cnt, int64_t rpv) {
         b.r0 = r0;
         b.cnt = cnt;
+        {   // (no xt: an empty range, no memory access)
+            const __amdgpu_buffer_rsrc_t rx = buf_rsrc(xt + r0, xt ? cnt * 8 : 0);
+            b.xv = buf_load<double>(rx, (ln & (GL - 1)) == 0 ? (ln / GL) * 8 : (1 << 30));
+        }
         // (pairs) the batch's entries from its first row's first pair; inside a batch the row
         // pointers are 32-bit offsets from it
         const int64_t eb = readlane64(rpv, 0) & ~int64_t(1);
@@ -543,6 +559,7 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     // so every row issues the same instructions and the compiler can interleave the G rows'
     // product and reduction chains (a branch would end the basic block).  The accumulator
     // updates stay in row order (consecutive rows share rays).
+    double zx = 0.0;                              // this lane's share of x_true'(B*q), batches in order
     auto process = [&](RB& b) {
         double P[G];
         uint32_t k[G][NCH][EPL];
@@ -564,7 +581,6 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                 }
             P[j] = p;
         }
-        constexpr int GL = 64 / G;                // lanes per row sum after the butterfly
         double S;                                 // lane l: z of row l / GL
         if constexpr (DBG & 4) S = P[0] + P[G - 1];
         else S = rows_sum_t<G>(P);
@@ -572,6 +588,7 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
             const __amdgpu_buffer_rsrc_t rz = buf_rsrc(z + b.r0, b.cnt * 8);
             buf_store(S, rz, (ln & (GL - 1)) == 0 ? (ln / GL) * 8 : (1 << 30));
         }
+        zx = zx + S * b.xv;                       // (other lanes: xv = 0)
 #pragma unroll
         for (int j = 0; j < G; ++j) {
             const double sj = lane_bcast(S, j * GL);
@@ -615,12 +632,25 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
             __builtin_amdgcn_sched_barrier(0);
         }
     } while (b[0].cnt > 0);
+    if (zx_part) zx = wave_sum(zx);
     __syncthreads();
+    // (the waves' side-dot sums go through qloc, free once every wave has left the loop: an
+    // array of their own would push the workgroup past half the LDS, one workgroup per CU)
+    if (zx_part && ln == 0) qloc[wv] = zx;
     for (int k = threadIdx.x; k < nr; k += 64 * W) {
         double t = acc[0][k];
 #pragma unroll
         for (int w = 1; w < W; ++w) t += acc[w][k];
         part[pb + k] = t;
+    }
+    if (zx_part) {
+        __syncthreads();
+        if (threadIdx.x == 0) {                   // waves in order
+            double t = qloc[0];
+#pragma unroll
+            for (int w = 1; w < W; ++w) t += qloc[w];
+            zx_part[g] = t;
+        }
     }
 }
 
@@ -887,7 +917,8 @@ constexpr int RW_SLOTS_MAX = 4096;
 constexpr int RW_ROW_MAX = 255;                   // entries per pixel row (two chunks of 128, pairs)
 }  // namespace
 
-static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, bool dry);
+static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, bool dry,
+                            const double* xt = nullptr);
 
 FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G) {
     HGM_REQUIRE(B->dtype == HGM_F64, "fused A*(B*q): fp64 operators");
@@ -1004,6 +1035,8 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
         P->runs = upload(runs);
         P->ray_tab = upload(ray_tab);
         P->lidx = upload(lidx);
+        if (hipMalloc(&P->zx_part, sizeof(double) * std::max<int64_t>(nreg, 1)) != hipSuccess)
+            throw Error{HGM_E_NOMEM, "fused plan: hipMalloc failed"};
         P->rs_ptr = upload(rs_ptr);
         P->rs_slot = upload(rs_slot);
         if (hipMalloc(&P->part, sizeof(double) * std::max<int64_t>(nslot, 1)) != hipSuccess)
@@ -1066,7 +1099,8 @@ const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
 // chunks per row
 // Launch the instantiation for the plan and the options (dry: only report whether one exists;
 // the plan is refused at build time when none does, so the two-pass path runs instead).
-static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, bool dry) {
+static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, bool dry,
+                            const double* xt) {
     const int W = P->waves, MR = P->maxr, G = P->group, D = c->num.fused_depth;
     const bool PRm = c->num.fused_pairs;
     // chunks per row: 64 entries (128 with pairs, whose first pair may start one entry early)
@@ -1079,7 +1113,7 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
             launch(c, false, k_fused_rw<WV, MRV, GV, NCV, DV, PV, DBV>, dim3((unsigned)P->nreg), dim3(64 * WV),     \
                    (const int64_t*)P->reg_base, (const int32_t*)P->ray_tab, (const int32_t*)P->wrun,              \
                    (const int2*)P->runs, (const int64_t*)B->rp, (const double*)B->val, (const uint16_t*)P->lidx, q, \
-                   Bq, P->part);                                                                                    \
+                   Bq, P->part, xt, xt ? P->zx_part : nullptr);                                                       \
         return true;                                                                                                  \
     }
     if (dbg) {   // timing experiments: the default shape only
@@ -1115,11 +1149,13 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
 }
 
 // Bq = B*q (n), ABq = A*(B*q) (m), one pass over B.
-void fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq) {
+bool fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq,
+              const double* xt, double* zx_out) {
+    const bool zx = xt && zx_out && P->kind == 1;
     hipEvent_t t0 = nullptr;
     timing_begin(c, KC_FUSED, &t0);
     if (P->kind == 1) {
-        fused_rw_launch(c, B, P, q, Bq, false);
+        fused_rw_launch(c, B, P, q, Bq, false, zx ? xt : nullptr);
     } else {
 #define HGM_FUSED_LAUNCH(FB, FGV, PFV)                                                                          \
     launch(c, false, k_fused_ab<FB, FGV, PFV>, dim3((unsigned)P->nreg), dim3(FB), (const FusedSub*)P->subs,      \
@@ -1142,12 +1178,14 @@ void fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q,
 #undef HGM_FUSED_LAUNCH
     }
     launch(c, true, k_fused_reduce<HGM_FUSED_RG>, dim3(grid_for(P->m * HGM_FUSED_RG)), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
-           (const int32_t*)P->rs_slot, (const double*)P->part, ABq);
+           (const int32_t*)P->rs_slot, (const double*)P->part, ABq, (const double*)P->zx_part, (int)P->nreg,
+           zx ? zx_out : nullptr);
     HGM_HIP(hipGetLastError());
     // algorithmic bytes of the fused pass: B's CSR once (values, 32-bit indices, row pointers),
     // q read, z and w written (SURVEY.md §8(d)'s SpMV count for one pass over the operator)
     const double bytes = 12.0 * (double)B->nnz + 8.0 * (B->rows + 1) + 8.0 * B->cols + 8.0 * B->rows + 8.0 * B->cols;
     timing_end(c, KC_FUSED, t0, bytes);
+    return zx;
 }
 
 }  // namespace hgm

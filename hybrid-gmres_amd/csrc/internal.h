@@ -424,7 +424,10 @@ std::vector<int64_t> pix_reference_of_stored(const PixOrder& o);
 // pair / context does not qualify (the two-pass path then runs).
 bool fused_ab_eligible(const hgm_ctx* c, const hgm_mat* A, const hgm_mat* B);
 const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B);
-void fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq);
+// With xt and zx_out (the row-wave kernel only; returns whether it did): also *zx_out =
+// x_true'(B*q), the m-space Gram error monitor's side dot, from the row sums as they form.
+bool fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq,
+              const double* xt = nullptr, double* zx_out = nullptr);
 void fused_plan_free(FusedPlan* P);
 
 // ---------------- comm / scalars (capi.cpp) ----------------

@@ -399,6 +399,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     T* pn_h = c->buf<T>("pn_h", 2);
     // Enqueue Arnoldi step kq: operator application + orthogonalisation (+ Gram column).
     auto enqueue_step = [&](int kq) {
+        bool zx_fused = false;                            // x_true'(B*q_k) formed by the fused pass
         T* qk = Q + (int64_t)kq * ldq;
         T* v = Q + (int64_t)(kq + 1) * ldq;
         const bool pending_in = pend.np > 0;
@@ -425,7 +426,15 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             // orthogonalised vector to Q(:,k+1), no copy), or in Q(:,k+1) for CGS2
             T* w = (ABQ && orth != HGM_CGS2) ? ABQ + (int64_t)kq * ldaq : v;
             if (fplan) {
-                fused_ab(c, B, fplan, qk, Bq, w);                                   // both in one pass over B
+                // both in one pass over B; with the m-space Gram error monitor the pass also forms
+                // the side dot x_true'(B*Q(:,k)) (else the MGS sweep's extra workgroups do)
+#ifndef HGM_FUSED_ZX
+#define HGM_FUSED_ZX 1
+#endif
+                const bool zxf = HGM_FUSED_ZX && gem_ab;
+                if constexpr (std::is_same_v<T, double>)
+                    zx_fused = fused_ab(c, B, fplan, qk, Bq, w, zxf ? xt : nullptr,
+                                        zxf ? dr + offQG + (size_t)kq * LQ + kq + 2 : nullptr);
                 if (dist_n(c)) allreduce(c, w, m);                                 // (as apply_A)
             } else {
                 apply_B<T>(c, B, qk, Bq, EPI_NONE, T(0), nullptr);                  // B*Q(:,k)
@@ -466,7 +475,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             }
             // the Gram row's extra dot: x_true (n-space) or b (m-space, unused: the row is for L)
             mgs<T>(c, dim, Q, ldq, kq, Hcol, dist, (!nspace && ABQ) ? ABQ + (int64_t)kq * ldaq : nullptr,
-                   gem_ab ? &zx : side, defer, pending_in ? (const T*)pn_h : nullptr,
+                   gem_ab ? (zx_fused ? nullptr : &zx) : side, defer, pending_in ? (const T*)pn_h : nullptr,
                    gem ? (gem_n ? xt : b) : nullptr, gem ? dr + offQG + (size_t)kq * LQ : nullptr);
             if (gem_ab && dist_n(c)) allreduce(c, zx.out, 1);   // x_true'(B*q_k) over the pixel shards
         }
