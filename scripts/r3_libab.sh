@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/r3libab
 mkdir -p $O
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for lib in default $LIBS; do
     if [ $lib = default ]; then unset HGM_LIB; else export HGM_LIB=$PWD/exp/$lib; fi
     if [ "${BENCH:-0}" = 1 ]; then
