@@ -1148,6 +1148,14 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
     throw Error{HGM_E_ARG, "fused A*(B*q): no row-wave kernel for this plan and options"};
 }
 
+__global__ void k_copy_sys(const double* __restrict__ src, double* dst) {
+    if (threadIdx.x == 0) st_sys(dst, *src);
+}
+void copy_sys(hgm_ctx* c, const double* src, double* dst) {
+    hipLaunchKernelGGL(k_copy_sys, dim3(1), dim3(64), 0, c->stream, src, dst);
+    HGM_HIP(hipGetLastError());
+}
+
 // Bq = B*q (n), ABq = A*(B*q) (m), one pass over B.
 bool fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq,
               const double* xt, double* zx_out) {

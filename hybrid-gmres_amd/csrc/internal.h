@@ -428,6 +428,8 @@ const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B);
 // x_true'(B*q), the m-space Gram error monitor's side dot, from the row sums as they form.
 bool fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq,
               const double* xt = nullptr, double* zx_out = nullptr);
+// *dst = *src (one scalar, device to the host-visible ring, system scope), on the context stream
+void copy_sys(hgm_ctx* c, const double* src, double* dst);
 void fused_plan_free(FusedPlan* P);
 
 // ---------------- comm / scalars (capi.cpp) ----------------

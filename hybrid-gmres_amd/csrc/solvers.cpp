@@ -400,6 +400,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // Enqueue Arnoldi step kq: operator application + orthogonalisation (+ Gram column).
     auto enqueue_step = [&](int kq) {
         bool zx_fused = false;                            // x_true'(B*q_k) formed by the fused pass
+        bool zx_rode = false;                             // ... and summed over the ranks with A*(B*q_k)
         T* qk = Q + (int64_t)kq * ldq;
         T* v = Q + (int64_t)(kq + 1) * ldq;
         const bool pending_in = pend.np > 0;
@@ -432,10 +433,17 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
 #define HGM_FUSED_ZX 1
 #endif
                 const bool zxf = HGM_FUSED_ZX && gem_ab;
+                T* zx_dst = zxf ? dr + offQG + (size_t)kq * LQ + kq + 2 : nullptr;
+                // on a communicator the side dot rides the m-vector all-reduce as its element m
+                // (when the column's stride leaves room past m): one collective per step, not two
+                const int64_t wld = (ABQ && orth != HGM_CGS2) ? ldaq : ldq;
+                const bool ride = zxf && dist_n(c) && wld > m;
                 if constexpr (std::is_same_v<T, double>)
-                    zx_fused = fused_ab(c, B, fplan, qk, Bq, w, zxf ? xt : nullptr,
-                                        zxf ? dr + offQG + (size_t)kq * LQ + kq + 2 : nullptr);
-                if (dist_n(c)) allreduce(c, w, m);                                 // (as apply_A)
+                    zx_fused = fused_ab(c, B, fplan, qk, Bq, w, zxf ? xt : nullptr, ride ? w + m : zx_dst);
+                zx_rode = ride && zx_fused;
+                if (dist_n(c)) allreduce(c, w, zx_rode ? m + 1 : m);             // (as apply_A)
+                if constexpr (std::is_same_v<T, double>)
+                    if (zx_rode) copy_sys(c, w + m, zx_dst);
             } else {
                 apply_B<T>(c, B, qk, Bq, EPI_NONE, T(0), nullptr);                  // B*Q(:,k)
                 apply_A<T>(c, A, Bq, w, EPI_NONE, T(0), nullptr);                   // A*(B*Q(:,k))
@@ -477,7 +485,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             mgs<T>(c, dim, Q, ldq, kq, Hcol, dist, (!nspace && ABQ) ? ABQ + (int64_t)kq * ldaq : nullptr,
                    gem_ab ? (zx_fused ? nullptr : &zx) : side, defer, pending_in ? (const T*)pn_h : nullptr,
                    gem ? (gem_n ? xt : b) : nullptr, gem ? dr + offQG + (size_t)kq * LQ : nullptr);
-            if (gem_ab && dist_n(c)) allreduce(c, zx.out, 1);   // x_true'(B*q_k) over the pixel shards
+            if (gem_ab && dist_n(c) && !zx_rode) allreduce(c, zx.out, 1);   // x_true'(B*q_k) over the pixel shards
         }
         // Step kq-1's column is complete (H(kq,kq-1) came from this step's A product).  The
         // event goes at the end of the step: a marker between two kernels costs a bubble.
