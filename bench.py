@@ -126,8 +126,11 @@ def build_shard(ctx, wl, rank, world):
     gather locality and the 64-column bands of the single-GPU kernels.  Parallel-beam nnz per
     pixel is uniform: equal pixel counts balance nnz to 0.02 % at 8 shards (512^2 check).
     x_true (and the returned x) are the shard's stored-order pixels; b (replicated) is formed
-    from the full operator before it is released."""
+    from the full operator before it is released.  fp32 workloads (configs[4]): b from the fp64
+    operator, as build_problem does, then the shards are cut from the fp32 operator and its
+    fp32 transpose (the solve's dtype is the shards')."""
     import hgmres
+    from hgmres import _lib as L
     from hgmres.core import stored_pixel_index
     from hgmres.problems import shepp_logan
     from hgmres.dist import tile_column_shards
@@ -139,6 +142,9 @@ def build_shard(ctx, wl, rank, world):
     rng = np.random.default_rng(0)                         # same noise on every rank
     e = rng.standard_normal(Af.shape[0])
     e = e / np.linalg.norm(e) * 1e-2 * np.linalg.norm(b_exact)
+    if wl.get("f32"):
+        Af.close()
+        Af = hgmres.SparseOperator.siddon(N, na, ctx=ctx, dtype=L.HGM_F32)
     Bf = Af.T
     n = Af.shape[1]
     lo, hi = tile_column_shards(N, world, tile)[rank]     # whole tile columns of stored pixels
@@ -174,6 +180,11 @@ def launch_ranks(n):
     return subprocess.call(cmd, env=env)
 
 
+def wl_dtype(wl):
+    """The arithmetic type of the workload's operator and vectors (the line's `dtype`)."""
+    return "f32" if wl.get("f32") else "f64"
+
+
 def plan(args, world):
     """What a rank will run: the workload, the world and every rank's pixel shard (stored
     positions, whole tile columns).  Host only."""
@@ -184,6 +195,7 @@ def plan(args, world):
     shard = (world > 1 and not args.replicas) or args.shard1
     tile = auto_pixel_order(N)[0]
     return {"workload": args.workload, "solver": wl["solver"], "N": N, "angles": wl["angles"], "world": world,
+            "dtype": wl_dtype(wl),
             "mode": "pixel-sharded" if shard else ("replicas" if world > 1 else "single GPU"),
             "shards": tile_column_shards(N, world, tile) if shard else [(0, N * N)] * world}
 
@@ -242,6 +254,10 @@ def main():
             B.close()
             B = hgmres.SparseOperator.pixel_backprojector(wl["N"], wl["angles"], ctx=ctx, dtype=A.dtype)
         lo, hi, full = 0, A.shape[1], A.shape
+    # the line's dtype is the operator's: a workload's fp32 must reach the shards / operator it solves
+    got = "f32" if A.dtype == L.HGM_F32 else "f64"
+    if got != wl_dtype(wl) or B.dtype != A.dtype:
+        raise RuntimeError(f"bench.py: {args.workload} is {wl_dtype(wl)} but the operators are {got}/{B.dtype}")
     for o in args.opt:
         name, val = o.split("=", 1)
         ctx.set_option(name, float(val))
@@ -283,8 +299,9 @@ def main():
         if gcv:
             _check(lib.hgm_arnoldi(ctx.handle, A._h, B._h, b.ctypes.data_as(L.dp), kg, L.HGM_SIDE_BA, 1e-12, o_orth,
                                    Hg.ctypes.data_as(L.dp), C.byref(beta_g), C.byref(kdone)), ctx)
-            # k = size(H,2) = k_gcv (gcv_function.m:33): the columns past a breakdown are zero
-            rc = lib.hgm_gcv_fminbnd(Hg.ctypes.data_as(L.dp), kg, beta_g.value, float(n), gcv["lo"],
+            # k = size(H,2) = k_gcv (gcv_function.m:33): the columns past a breakdown are zero.
+            # trace term n (gcv_function.m:46-50, 'ba'): the GLOBAL pixel count, not the shard's
+            rc = lib.hgm_gcv_fminbnd(Hg.ctypes.data_as(L.dp), kg, beta_g.value, float(full[1]), gcv["lo"],
                                      gcv["hi"], gcv["tolx"], C.byref(lam_c), C.byref(g_c))
             if rc != 0:
                 raise RuntimeError(f"hgm_gcv_fminbnd failed ({rc})")
@@ -363,9 +380,14 @@ def main():
                 traffic = None
         if dom_name == "spmv_AB_fused":
             # the one pass replaces the two SpMVs B*q and A*(B*q): their algorithmic bytes (SURVEY
-            # §8(d)) over the same time give the effective rate of the pair it replaces
-            mm, nn, nz = full[0], full[1], A.nnz
-            two = (12.0 * nz + 8.0 * (nn + 1) + 8.0 * mm + 8.0 * nn) + (12.0 * nz + 8.0 * (mm + 1) + 8.0 * nn + 8.0 * mm)
+            # §8(d)) over the same time give the effective rate of the pair it replaces (this
+            # rank's operator: a shard's local shape with its own nnz)
+            mm, nn, nz = A.shape[0], A.shape[1], A.nnz
+            s = 4.0 if got == "f32" else 8.0
+            two = (((s + 4) * nz + 8.0 * (nn + 1) + s * mm + s * nn) +
+                   ((s + 4) * nz + 8.0 * (mm + 1) + s * nn + s * mm))
+            if wl["solver"] in UNITS:
+                two += s * nn      # the Golub-Kahan B product's epilogue read of v (A'*u - beta*v)
             d["two_pass_bytes"] = two
             d["effective_GBps_two_pass"] = two / (d["avg_us"] * 1e-6) / 1e9
         roof = {"bound": "hbm", "kernel": dom_name, "achieved": round(d["GBps"], 1), "peak": HBM_PEAK_GBS,
@@ -393,7 +415,7 @@ def main():
             # total work is fixed, so the N = 1 line of that series is strong scaling too
             "scaling": "weak" if args.replicas else "strong",
             "vs_baseline": None,
-            "dtype": "f32" if wl.get("f32") else "f64",
+            "dtype": got,
             "data": "synthetic (Siddon parallel-beam A generated on device, Shepp-Logan phantom, 1% noise"
                     + (", unmatched pixel-driven B" if args.unmatched and wl["solver"] not in UNITS else ", B = A'")
                     + ")",

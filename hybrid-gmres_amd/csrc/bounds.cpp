@@ -80,6 +80,7 @@ int gmres_bounds_filter(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const h
                         const double* xt, double tol, int maxit, double lambda, int side, int hybrid,
                         const hgm_mat* dML, const hgm_mat* dMR, int ritz_steps, double* x_out, double* err_out,
                         double* res_out, int* niters, double* phi, double* dphi, double* mu_out, double* ritz_res) {
+    solver_guard(c);
     HGM_REQUIRE(A != nullptr && B != nullptr, "A and B are required");
     HGM_REQUIRE(c->world == 1, "filter-factor bounds: single rank");
     HGM_REQUIRE(dML != nullptr, "DeltaM is required");

@@ -828,20 +828,28 @@ HGM_API int hgm_spmv_ab(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const vo
         HGM_REQUIRE(A->dtype == B->dtype, "spmv_ab: A and B share the dtype");
         HGM_REQUIRE(A->col_order == B->row_order && A->row_order.trivial() && B->col_order.trivial(),
                     "spmv_ab: A's columns and B's rows share the pixel order");
-        if (A->dtype == HGM_F64) {
-            double* bq = B->row_order.trivial() ? (double*)Bq : c->buf<double>("spmv_ab_bq", B->rows);
+        // one rank: on a communicator (a pixel shard) the product would be this rank's partial
+        // A_g*(B_g*q) before the all-reduce, which this single-operator call does not perform
+        HGM_REQUIRE(c->world == 1 && c->nccl == nullptr, "spmv_ab: a single-rank context (no communicator)");
+        auto run = [&](auto tag) {
+            using T = decltype(tag);
+            T* bq = B->row_order.trivial() ? (T*)Bq : c->buf<T>("spmv_ab_bq", B->rows);
             const FusedPlan* P = fused_ab_plan(c, A, B);
+            if (P && !fused_gk_ok(c, B, P) && sizeof(T) == 4) P = nullptr;
             if (P) {
-                fused_ab(c, B, P, (const double*)q, bq, (double*)ABq);
+                FusedArgs<T> fa;
+                fa.q = (const T*)q;
+                fa.zraw = bq;
+                fa.w = (T*)ABq;
+                fused_pass<T>(c, B, P, fa);
             } else {
-                spmv<double>(c, B, (const double*)q, bq, EPI_NONE, 0.0, nullptr, KC_SPMV_B);
-                spmv<double>(c, A, bq, (double*)ABq, EPI_NONE, 0.0, nullptr, KC_SPMV_A);
+                spmv<T>(c, B, (const T*)q, bq, EPI_NONE, T(0), nullptr, KC_SPMV_B);
+                spmv<T>(c, A, bq, (T*)ABq, EPI_NONE, T(0), nullptr, KC_SPMV_A);
             }
-            if (!B->row_order.trivial()) pix_permute<double>(c, B->row_order, bq, (double*)Bq, 1);
-        } else {
-            spmv_ref<float>(c, B, (const float*)q, (float*)Bq);
-            spmv_ref<float>(c, A, (const float*)Bq, (float*)ABq);
-        }
+            if (!B->row_order.trivial()) pix_permute<T>(c, B->row_order, bq, (T*)Bq, 1);
+        };
+        if (A->dtype == HGM_F64) run(double(0));
+        else run(float(0));
     });
     return HGM_OK;
 }

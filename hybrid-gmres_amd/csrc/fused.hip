@@ -60,6 +60,7 @@ static_assert(sizeof(FusedSub) == 32, "FusedSub layout");
 
 struct FusedPlan {
     int kind = 0;                 // 0 sub-chunk pass (k_fused_ab), 1 row-wave pass (k_fused_rw)
+    int elem = 8;                 // value size (kind 1: fp64 or fp32; the slots are byte offsets)
     int region = 0, waves = 0, maxr = 0, group = 0, depth = 0;
     bool pairs = false;
     int64_t nreg = 0, nsub = 0, nlr = 0, nslot = 0, m = 0, maxlen = 0;
@@ -68,7 +69,7 @@ struct FusedPlan {
     int32_t* wrun = nullptr;      // nreg * waves + 1
     int2* runs = nullptr;         // (first row, rows)
     int32_t* ray_tab = nullptr;   // nslot: global ray of each region-local ray
-    uint16_t* lidx = nullptr;     // nnz (+ padding): the slot as an LDS byte offset (index * 8)
+    uint16_t* lidx = nullptr;     // nnz (+ padding): the slot as an LDS byte offset (index * elem)
     int32_t* reg_sub = nullptr;   // nreg+1
     int64_t* reg_base = nullptr;  // nreg+1
     FusedSub* subs = nullptr;     // nsub
@@ -77,8 +78,8 @@ struct FusedPlan {
     uint32_t* lr_pk = nullptr;    // nlr: first position | entries << 12 | region ray index << 20
     int64_t* rs_ptr = nullptr;    // m+1
     int32_t* rs_slot = nullptr;   // nslot
-    double* part = nullptr;       // nslot
-    double* zx_part = nullptr;    // kind 1: nreg (the regions' shares of the side dot x_true'(B*q))
+    double* part = nullptr;       // nslot (fp32 plans use it as float)
+    double* zx_part = nullptr;    // kind 1: nreg (the regions' side sums; fp32 plans: float)
     double build_s = 0;
 };
 
@@ -333,24 +334,24 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(D <= 2 ? FB
 #endif
 // With zx_out, block 0 first adds the nzx regional shares of the side dot x_true'(B*q) (fixed
 // order) into *zx_out.
-template <int RG>
+template <int RG, typename T>
 __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* __restrict__ rs_ptr,
                                                      const int32_t* __restrict__ rs_slot,
-                                                     const double* __restrict__ part, double* __restrict__ w,
-                                                     const double* __restrict__ zx_part, int nzx, double* zx_out) {
+                                                     const T* __restrict__ part, T* __restrict__ w,
+                                                     const T* __restrict__ zx_part, int nzx, T* zx_out) {
     if (zx_out && blockIdx.x == 0) {
-        __shared__ double sh[4];
-        const double t = reduce_parts<double, false>(zx_part, nzx, sh);
+        __shared__ T sh[4];
+        const T t = reduce_parts<T, false>(zx_part, nzx, sh);
         if (threadIdx.x == 0) st_sys(zx_out, t);           // (the host ring: system scope, device_common.h)
     }
     const int gl = threadIdx.x % RG;
     for (int64_t i = ((int64_t)blockIdx.x * BS + threadIdx.x) / RG; i < m; i += (int64_t)gridDim.x * (BS / RG)) {
-        double s = 0.0;
+        T s = T(0);
         const int64_t k0 = rs_ptr[i], k1 = rs_ptr[i + 1];
         int64_t k = k0 + gl;
         for (; k + 3 * RG < k1; k += 4 * RG) {   // 4 slot reads, then 4 partial reads in flight
             int32_t sl[4];
-            double p[4];
+            T p[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) sl[u] = rs_slot[k + u * RG];
 #pragma unroll
@@ -359,7 +360,7 @@ __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* _
             for (int u = 0; u < 4; ++u) s += p[u];
         }
         for (; k < k1; k += RG) s += part[rs_slot[k]];
-        if constexpr (RG > 1) s = group_sum<double, RG>(s);
+        if constexpr (RG > 1) s = group_sum<T, RG>(s);
         if (gl == 0) w[i] = s;
     }
 }
@@ -400,12 +401,22 @@ __device__ __forceinline__ void swap16(double& a, double& b) {
     a = __hiloint2double((int)hi[0], (int)lo[0]);
     b = __hiloint2double((int)hi[1], (int)lo[1]);
 }
+__device__ __forceinline__ void swap32(float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void swap16(float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
 // The 64-lane sums of G values at once (G = 4 or 8), by a butterfly that halves the values per
 // lane while it halves the lanes per sum: lane l ends with the sum of P[l / (64 / G)], the same
 // bits in each lane of its group.  Fixed order.  Per row this is ~6 exchanges and adds instead of
 // a full wave reduction each (DPP tree + 8 readlanes).
-template <int G>
-__device__ __forceinline__ double rows_sum_t(double (&P)[G]) {
+template <int G, typename T>
+__device__ __forceinline__ T rows_sum_t(T (&P)[G]) {
     static_assert(G == 4 || G == 8, "rows per batch");
 #pragma unroll
     for (int i = 0; i < G / 2; ++i) {          // lane bit 5
@@ -419,8 +430,8 @@ __device__ __forceinline__ double rows_sum_t(double (&P)[G]) {
     }
     if constexpr (G == 8) {                    // lane bit 3: row_ror 8 within 16-lane rows
         const bool hi = (threadIdx.x & 8) != 0;
-        double s = hi ? P[1] : P[0];
-        const double t = hi ? P[0] : P[1];
+        T s = hi ? P[1] : P[0];
+        const T t = hi ? P[0] : P[1];
         s = s + dpp_mov<0x128>(t);
         s += dpp_mov<0xB1>(s);                 // lane ^ 1
         s += dpp_mov<0x4E>(s);                 // lane ^ 2
@@ -431,31 +442,53 @@ __device__ __forceinline__ double rows_sum_t(double (&P)[G]) {
     }
 }
 
-// acc += t in the LDS unit (ds_add_f64, no return): the update needs no round trip, and the
-// LDS performs one wave's operations in issue order, so with a wave-private accumulator and
-// distinct addresses within each instruction (a pixel row meets a ray once; dummies are per lane)
-// the sums keep a fixed order: no atomicity is needed, only the read-modify-write in place.
-__device__ __forceinline__ void lds_add(double* p, double t) {
+// acc += t in the LDS unit (ds_add_f64 / ds_add_f32, no return value): the update needs no round
+// trip.  DETERMINISM INVARIANT: the order of the adds into one accumulator is
+// fixed because (1) the accumulator array is private to the wave (acc[wv]), (2) the LDS executes
+// one wave's DS instructions in issue order, and (3) within one instruction the 64 lanes address
+// distinct slots (a pixel row meets a ray at most once; out-of-row lanes use their own dummy slot).
+// So no atomicity is involved -- only an in-place read-modify-write in program order -- and the
+// sums are bitwise reproducible (test_gpu_fused.py repeats every product and solve bit for bit).
+// Breaking any of (1)-(3) (shared accumulators, a second wave, duplicate slots per row) would
+// make the order depend on timing.
+template <typename T>
+__device__ __forceinline__ void lds_add(T* p, T t) {
     (void)__hip_atomic_fetch_add(p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
 // DBG (timing experiments only, HGM_OPT_FUSED_DBG with the row-wave pass; results WRONG): bit 1
 // skips the q reads, 2 the accumulator updates, 4 the row-sum butterfly.
 // D: batches in the ring (D - 1 in flight while one is processed).  PR: two entries per lane (a
-// 16-byte value pair and a 4-byte slot pair per lane from the row's 16-byte-aligned start, chunks
-// of 128 entries): half the load instructions of one entry per lane (chunks of 64).
-template <int W, int MAXR, int G, int NCH, int D, bool PR, int DBG = 0>
+// 16-byte value pair (8-byte in fp32) and a 4-byte slot pair per lane from the row's pair-aligned
+// start, chunks of 128 entries): half the load instructions of one entry per lane (chunks of 64).
+//
+// T: double (the GMRES family) or float (BASELINE configs[4], the Golub-Kahan path in fp32): the
+// values, q, the row sums, the LDS slots and the partials are T; slots are LDS byte offsets
+// (slot * sizeof(T), the plan's element size).
+//
+// Row epilogue (the Golub-Kahan step v_hat = A'*u - beta*v of lsqr_solver.m:26 / lsmr_solver.m:38
+// with q = u): zs_j = z_j - a * ev[j] with a = (T)sqrt((double)*easq), two roundings (no FMA, as
+// the two-pass EPI_SUB epilogue); the scatter then forms A*zs, i.e. A*v_hat, so the next step's
+// A*v_{k+1} = (A*v_hat)/alpha needs no second pass over the operator.  Without ev: zs = z - 0*0,
+// the same bits as z.  Outputs (either may be null): zraw[j] = z_j, zout[j] = zs_j (zout may be ev:
+// a row is read and written by the same lanes of one wave, read first).
+// Side sum (one value per region, in zx_part): side_sq == 0: sum_j zs_j * xt[j] (the m-space Gram
+// error monitor's x_true'(B*q)); side_sq == 1: sum_j zs_j^2 (alpha^2 of the Golub-Kahan step).
+// GK: the row epilogue / zout / side_sq code exists (false: the GMRES family's instruction stream).
+template <typename T, bool GK, int W, int MAXR, int G, int NCH, int D, bool PR, int DBG = 0>
 __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__ reg_base, const int32_t* __restrict__ ray_tab,
                                                      const int32_t* __restrict__ wrun, const int2* __restrict__ runs,
-                                                     const int64_t* __restrict__ rp, const double* __restrict__ val,
-                                                     const uint16_t* __restrict__ lidx, const double* __restrict__ q,
-                                                     double* __restrict__ z, double* __restrict__ part,
-                                                     const double* __restrict__ xt, double* __restrict__ zx_part) {
+                                                     const int64_t* __restrict__ rp, const T* __restrict__ val,
+                                                     const uint16_t* __restrict__ lidx, const T* __restrict__ q,
+                                                     T* __restrict__ zraw, T* __restrict__ part,
+                                                     const T* __restrict__ xt, T* __restrict__ zx_part,
+                                                     const T* ev, const T* __restrict__ easq, T* zout, int side_sq) {
     static_assert(D >= 2 && D <= 4, "ring depth");
     constexpr int EPL = PR ? 2 : 1;              // entries per lane per chunk
     constexpr int CH = 64 * EPL;                 // entries per chunk
-    __shared__ double qloc[MAXR];           // (the last 64: the lanes' dummy slots)
-    __shared__ double acc[W][MAXR];
+    constexpr int ES = (int)sizeof(T);
+    __shared__ T qloc[MAXR];                     // (the last 64: the lanes' dummy slots)
+    __shared__ T acc[W][MAXR];
     const int g = blockIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int ln = threadIdx.x & 63;
@@ -464,13 +497,15 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     for (int k = threadIdx.x; k < nr; k += 64 * W) {
         qloc[k] = q[ray_tab[pb + k]];
 #pragma unroll
-        for (int w = 0; w < W; ++w) acc[w][k] = 0.0;
+        for (int w = 0; w < W; ++w) acc[w][k] = T(0);
     }
-    if (threadIdx.x < 64) qloc[MAXR - 64 + threadIdx.x] = 0.0;
+    if (threadIdx.x < 64) qloc[MAXR - 64 + threadIdx.x] = T(0);
+    // the epilogue coefficient: the bits the host takes from the same sum of squares
+    const T ea = (GK && easq) ? (T)sqrt((double)*easq) : T(0);
     int ua = wrun[g * W + wv];
     const int ub = wrun[g * W + wv + 1];
     __syncthreads();
-    double* __restrict__ ac = acc[wv];
+    T* __restrict__ ac = acc[wv];
     // the wave's runs (<= 64, the plan checks) in lanes: readlane in the loop, no loads there
     // (a conditional load makes the compiler wait for every load in flight after it, and scalar
     // loads' lgkmcnt waits would also wait on the LDS)
@@ -498,22 +533,31 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     struct RB {
         int r0, cnt;
         int len[G], off[G];
-        double v[G][NCH][EPL];
+        T v[G][NCH][EPL];
         uint32_t s[G][NCH];
-        double xv;                                // x_true of row l / GL at lane l (side dot)
+        T xv;                                     // x_true of row l / GL at lane l (side dot)
+        T evv;                                    // ev of row l / GL at lane l (row epilogue)
     };
+    // lane l / GL's row of the batch at the group's first lane, past every range elsewhere
+    auto row_off = [&]() { return (ln & (GL - 1)) == 0 ? (ln / GL) * ES : (1 << 30); };
     auto issue = [&](RB& b, int r0, int cnt, int64_t rpv) {
         b.r0 = r0;
         b.cnt = cnt;
-        {   // (no xt: an empty range, no memory access)
-            const __amdgpu_buffer_rsrc_t rx = buf_rsrc(xt + r0, xt ? cnt * 8 : 0);
-            b.xv = buf_load<double>(rx, (ln & (GL - 1)) == 0 ? (ln / GL) * 8 : (1 << 30));
+        {   // (no xt / ev: an empty range, no memory access)
+            const __amdgpu_buffer_rsrc_t rx = buf_rsrc(xt + r0, xt ? cnt * ES : 0);
+            b.xv = buf_load<T>(rx, row_off());
+            if constexpr (GK) {
+                const __amdgpu_buffer_rsrc_t re = buf_rsrc(ev + r0, ev ? cnt * ES : 0);
+                b.evv = buf_load<T>(re, row_off());
+            } else {
+                b.evv = T(0);
+            }
         }
         // (pairs) the batch's entries from its first row's first pair; inside a batch the row
         // pointers are 32-bit offsets from it
         const int64_t eb = readlane64(rpv, 0) & ~int64_t(1);
         const int bspan = PR ? (int)((readlane64(rpv, G) - eb + 1) & ~int64_t(1)) : 0;
-        const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + eb, bspan * 8);
+        const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + eb, bspan * ES);
         const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lidx + eb, bspan * 2);
 #pragma unroll
         for (int j = 0; j < G; ++j) {
@@ -533,10 +577,16 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
 #define HGM_RW_MASK_LOADS 1
 #endif
                     const bool in = !HGM_RW_MASK_LOADS || 2 * ln + CH * c < len + off;
-                    const int vo = in ? (2 * ln + CH * c) * 8 : (1 << 30), lo = in ? (2 * ln + CH * c) * 2 : (1 << 30);
-                    const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, vo, rel * 8, 2));
-                    b.v[j][c][0] = t.x;
-                    b.v[j][c][EPL - 1] = t.y;
+                    const int vo = in ? (2 * ln + CH * c) * ES : (1 << 30), lo = in ? (2 * ln + CH * c) * 2 : (1 << 30);
+                    if constexpr (ES == 8) {
+                        const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, vo, rel * ES, 2));
+                        b.v[j][c][0] = t.x;
+                        b.v[j][c][EPL - 1] = t.y;
+                    } else {
+                        const float2 t = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rv, vo, rel * ES, 2));
+                        b.v[j][c][0] = t.x;
+                        b.v[j][c][EPL - 1] = t.y;
+                    }
                     b.s[j][c] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, lo, rel * 2, 2);
                 }
             } else {
@@ -544,11 +594,14 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                 const int len = (int)(e1 - e0);
                 b.len[j] = len;
                 b.off[j] = 0;
-                const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + e0, len * 8);
+                const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + e0, len * ES);
                 const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lidx + e0, len * 2);
 #pragma unroll
                 for (int c = 0; c < NCH; ++c) {
-                    b.v[j][c][0] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, (ln + CH * c) * 8, 0, 2));
+                    if constexpr (ES == 8)
+                        b.v[j][c][0] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, (ln + CH * c) * 8, 0, 2));
+                    else
+                        b.v[j][c][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rv, (ln + CH * c) * 4, 0, 2));
                     b.s[j][c] = (uint32_t)__builtin_bit_cast(uint16_t, __builtin_amdgcn_raw_buffer_load_b16(rl, (ln + CH * c) * 2, 0, 2));
                 }
             }
@@ -559,46 +612,63 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     // so every row issues the same instructions and the compiler can interleave the G rows'
     // product and reduction chains (a branch would end the basic block).  The accumulator
     // updates stay in row order (consecutive rows share rays).
-    double zx = 0.0;                              // this lane's share of x_true'(B*q), batches in order
+    T zx = T(0);                                  // this lane's share of the side sum, batches in order
+    const bool first_lane = (ln & (GL - 1)) == 0;
+    (void)first_lane;
     auto process = [&](RB& b) {
-        double P[G];
+        T P[G];
         uint32_t k[G][NCH][EPL];
 #pragma unroll
         for (int j = 0; j < G; ++j) {
-            double p = 0.0;
+            T p = T(0);
 #pragma unroll
             for (int c = 0; c < NCH; ++c)
 #pragma unroll
                 for (int e = 0; e < EPL; ++e) {
-                    // slots are LDS byte offsets (the plan stores slot * 8); pos0 is the lane's first
-                    // entry in the row (-1: the previous row's last entry in the first pair)
+                    // slots are LDS byte offsets (the plan stores slot * sizeof(T)); pos0 is the lane's
+                    // first entry in the row (-1: the previous row's last entry in the first pair)
                     const int pos0 = EPL * ln + CH * c - b.off[j];
                     const bool ok = e == 0 ? (uint32_t)pos0 < (uint32_t)b.len[j] : pos0 < b.len[j] - 1;
                     const uint32_t sl = PR ? (e ? b.s[j][c] >> 16 : b.s[j][c] & 0xffffu) : b.s[j][c];
-                    k[j][c][e] = ok ? sl : (uint32_t)(MAXR - 64 + ln) * 8u;
-                    if constexpr (DBG & 1) p += b.v[j][c][e] * (double)k[j][c][e];
-                    else p += b.v[j][c][e] * *reinterpret_cast<const double*>(reinterpret_cast<const char*>(qloc) + k[j][c][e]);
+                    k[j][c][e] = ok ? sl : (uint32_t)(MAXR - 64 + ln) * (uint32_t)ES;
+                    if constexpr (DBG & 1) p += b.v[j][c][e] * (T)k[j][c][e];
+                    else p += b.v[j][c][e] * *reinterpret_cast<const T*>(reinterpret_cast<const char*>(qloc) + k[j][c][e]);
                 }
             P[j] = p;
         }
-        double S;                                 // lane l: z of row l / GL
+        T S;                                      // lane l: z of row l / GL
         if constexpr (DBG & 4) S = P[0] + P[G - 1];
         else S = rows_sum_t<G>(P);
-        {   // z out: each group's first lane, rows past cnt fall outside the range
-            const __amdgpu_buffer_rsrc_t rz = buf_rsrc(z + b.r0, b.cnt * 8);
-            buf_store(S, rz, (ln & (GL - 1)) == 0 ? (ln / GL) * 8 : (1 << 30));
+        T zs = S;
+        if constexpr (GK) {
+            const T sa = ea * b.evv;              // row epilogue: zs = z - a*ev (two roundings)
+            zs = S - sa;
         }
-        zx = zx + S * b.xv;                       // (other lanes: xv = 0)
+        {   // z out: each group's first lane, rows past cnt fall outside the range
+            const __amdgpu_buffer_rsrc_t rz = buf_rsrc(zraw + b.r0, zraw ? b.cnt * ES : 0);
+            buf_store(S, rz, row_off());
+            if constexpr (GK) {
+                const __amdgpu_buffer_rsrc_t ro = buf_rsrc(zout + b.r0, zout ? b.cnt * ES : 0);
+                buf_store(zs, ro, row_off());
+            }
+        }
+        // side: zs * x_true (other lanes: xv = 0), or zs^2 at the first lanes (rows past cnt: zs = 0)
+        if constexpr (GK) {
+            const T f = side_sq ? (first_lane ? zs : T(0)) : b.xv;
+            zx = zx + zs * f;
+        } else {
+            zx = zx + zs * b.xv;
+        }
 #pragma unroll
         for (int j = 0; j < G; ++j) {
-            const double sj = lane_bcast(S, j * GL);
+            const T sj = lane_bcast(zs, j * GL);
 #pragma unroll
             for (int c = 0; c < NCH; ++c)
 #pragma unroll
                 for (int e = 0; e < EPL; ++e) {
-                    const double t = b.v[j][c][e] * sj;
+                    const T t = b.v[j][c][e] * sj;
                     if constexpr (DBG & 2) S += t;
-                    else lds_add(reinterpret_cast<double*>(reinterpret_cast<char*>(ac) + k[j][c][e]), t);
+                    else lds_add(reinterpret_cast<T*>(reinterpret_cast<char*>(ac) + k[j][c][e]), t);
                 }
         }
     };
@@ -634,11 +704,11 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     } while (b[0].cnt > 0);
     if (zx_part) zx = wave_sum(zx);
     __syncthreads();
-    // (the waves' side-dot sums go through qloc, free once every wave has left the loop: an
+    // (the waves' side sums go through qloc, free once every wave has left the loop: an
     // array of their own would push the workgroup past half the LDS, one workgroup per CU)
     if (zx_part && ln == 0) qloc[wv] = zx;
     for (int k = threadIdx.x; k < nr; k += 64 * W) {
-        double t = acc[0][k];
+        T t = acc[0][k];
 #pragma unroll
         for (int w = 1; w < W; ++w) t += acc[w][k];
         part[pb + k] = t;
@@ -646,7 +716,7 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     if (zx_part) {
         __syncthreads();
         if (threadIdx.x == 0) {                   // waves in order
-            double t = qloc[0];
+            T t = qloc[0];
 #pragma unroll
             for (int w = 1; w < W; ++w) t += qloc[w];
             zx_part[g] = t;
@@ -917,11 +987,12 @@ constexpr int RW_SLOTS_MAX = 4096;
 constexpr int RW_ROW_MAX = 255;                   // entries per pixel row (two chunks of 128, pairs)
 }  // namespace
 
-static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, bool dry,
-                            const double* xt = nullptr);
+template <typename T, bool GK>
+static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArgs<T>& fa, bool dry);
 
 FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G) {
-    HGM_REQUIRE(B->dtype == HGM_F64, "fused A*(B*q): fp64 operators");
+    const int es = B->dtype == HGM_F32 ? 4 : 8;       // slots as LDS byte offsets of T
+
     HGM_REQUIRE(B->cols < (int64_t(1) << 31) && B->rows < (int64_t(1) << 31), "fused A*(B*q): index range");
     HGM_REQUIRE(W == 1 || W == 2 || W == 4, "fused A*(B*q): 1, 2 or 4 waves per region");
     const auto t0 = std::chrono::steady_clock::now();
@@ -988,7 +1059,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
                     if (rs.size() > (size_t)RW_SLOTS_MAX - 64) continue;
                     for (size_t k = 0; k < rs.size(); ++k) map[rs[k]] = (int32_t)k;
                     for (const int2& r : rr[g])
-                        for (int64_t e = rp[r.x]; e < rp[r.x + r.y]; ++e) lidx[e] = (uint16_t)(map[ci[e]] * 8);
+                        for (int64_t e = rp[r.x]; e < rp[r.x + r.y]; ++e) lidx[e] = (uint16_t)(map[ci[e]] * es);
                     for (int32_t ray : rs) map[ray] = -1;
                 }
             });
@@ -1020,6 +1091,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
     FusedPlan* P = new FusedPlan;
     try {
         P->kind = 1;
+        P->elem = es;
         P->region = R;
         P->waves = W;
         P->group = G;
@@ -1046,7 +1118,9 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
         throw;
     }
     P->build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (!fused_rw_launch(c, B, P, nullptr, nullptr, true)) {
+    const bool have = es == 4 ? fused_rw_launch<float, true>(c, B, P, FusedArgs<float>{}, true)
+                              : fused_rw_launch<double, false>(c, B, P, FusedArgs<double>{}, true);
+    if (!have) {
         fused_plan_free(P);
         throw Error{HGM_E_ARG, "fused A*(B*q): no row-wave kernel for this plan's shape and the options"};
     }
@@ -1056,14 +1130,24 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
     return P;
 }
 
-// Whether w = A*(B*q) can run fused for this pair (B = A' value for value, fp64, tiled pixels or
-// a shard of whole tile columns of them).  On a communicator the caller all-reduces w, as it does
-// A*(B*q) of the two-pass form.
+// Whether w = A*(B*q) can run fused for this pair (B = A' value for value, tiled pixels or a shard
+// of whole tile columns of them; fp64, or fp32 with the row-wave pass).  On a communicator the
+// caller all-reduces w, as it does A*(B*q) of the two-pass form.
 bool fused_ab_eligible(const hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
     if (!c->num.fused_ab || c->num.parity) return false;
-    if (!A || !B || A->dtype != HGM_F64 || B->dtype != HGM_F64) return false;
+    if (!A || !B || A->dtype != B->dtype) return false;
+    if (A->dtype != HGM_F64 && !(A->dtype == HGM_F32 && c->num.fused_kind == 1)) return false;
     if (!(B->transpose_of == A->uid || A->transpose_of == B->uid)) return false;
     return !fused_grid(B).trivial() && B->nnz > 0;
+}
+
+// The option tuple a plan is built for (a refused tuple is remembered per operator, so it is not
+// re-planned on every solve, while any other tuple plans afresh)
+static int64_t fused_key(const Numerics& nu) {
+    const bool rw = nu.fused_kind == 1;
+    if (!rw) return ((int64_t)nu.fused_region << 1);
+    return 1 | ((int64_t)nu.fused_wregion << 1) | ((int64_t)nu.fused_waves << 10) | ((int64_t)nu.fused_group << 13) |
+           ((int64_t)nu.fused_depth << 17) | ((int64_t)nu.fused_pairs << 20);
 }
 
 // The plan of B, built on first use (a failure to plan leaves the two-pass path in place).
@@ -1072,24 +1156,20 @@ const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
     hgm_mat* Bm = const_cast<hgm_mat*>(B);
     const Numerics& nu = c->num;
     const bool rw = nu.fused_kind == 1;
-    auto stale = [&](const FusedPlan* P) {
-        if (P->kind != (rw ? 1 : 0)) return true;
-        return rw ? (P->region != nu.fused_wregion || P->waves != nu.fused_waves || P->group != nu.fused_group ||
-                     P->depth != nu.fused_depth || P->pairs != nu.fused_pairs)
-                  : P->region != nu.fused_region;
-    };
-    if (Bm->fused && stale(Bm->fused)) {
+    const int64_t key = fused_key(nu);
+    if (Bm->fused && Bm->fused_key != key) {          // options changed since the plan was built
         fused_plan_free(Bm->fused);
         Bm->fused = nullptr;
-        Bm->fused_failed = false;
     }
-    if (!Bm->fused && !Bm->fused_failed) {
+    if (!Bm->fused && Bm->fused_failed_key != key) {   // (a refused tuple is not re-planned)
         try {
             Bm->fused = rw ? fused_plan_build_rw(c, B, nu.fused_wregion, nu.fused_waves, nu.fused_group)
                            : fused_plan_build(c, B, nu.fused_region);
+            Bm->fused_key = key;
+            Bm->fused_failed_key = -1;
         } catch (const Error& e) {
             if (e.code != HGM_E_ARG) throw;
-            Bm->fused_failed = true;
+            Bm->fused_failed_key = key;
         }
     }
     return Bm->fused;
@@ -1099,53 +1179,86 @@ const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
 // chunks per row
 // Launch the instantiation for the plan and the options (dry: only report whether one exists;
 // the plan is refused at build time when none does, so the two-pass path runs instead).
-static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, bool dry,
-                            const double* xt) {
+// T = double, GK = false: every shape and the measured variants (the GMRES family); GK = true
+// (the row epilogue of the Golub-Kahan step, and every fp32 pass): the production kernel with
+// four waves per region (a plan of another shape keeps the two-pass path).
+#define HGM_RW_SHAPES_GK(X) X(4, 1088) X(4, 1344) X(4, 1536) X(4, 2048)
+template <typename T, bool GK>
+static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArgs<T>& fa, bool dry) {
     const int W = P->waves, MR = P->maxr, G = P->group, D = c->num.fused_depth;
     const bool PRm = c->num.fused_pairs;
     // chunks per row: 64 entries (128 with pairs, whose first pair may start one entry early)
     const int64_t ml = P->maxlen + (PRm ? 1 : 0);
     const int NC = ml <= (PRm ? 128 : 64) ? 1 : ml <= (PRm ? 256 : 128) ? 2 : 4;
     const int dbg = c->num.fused_dbg;
+    const bool side = fa.side_out != nullptr && (fa.xt != nullptr || fa.side_sq);
 #define HGM_RWL(WV, MRV, GV, NCV, DV, PV, DBV)                                                                       \
     {                                                                                                                 \
         if (!dry)                                                                                                     \
-            launch(c, false, k_fused_rw<WV, MRV, GV, NCV, DV, PV, DBV>, dim3((unsigned)P->nreg), dim3(64 * WV),     \
-                   (const int64_t*)P->reg_base, (const int32_t*)P->ray_tab, (const int32_t*)P->wrun,              \
-                   (const int2*)P->runs, (const int64_t*)B->rp, (const double*)B->val, (const uint16_t*)P->lidx, q, \
-                   Bq, P->part, xt, xt ? P->zx_part : nullptr);                                                       \
+            launch(c, false, k_fused_rw<T, GK, WV, MRV, GV, NCV, DV, PV, DBV>, dim3((unsigned)P->nreg),             \
+                   dim3(64 * WV), (const int64_t*)P->reg_base, (const int32_t*)P->ray_tab, (const int32_t*)P->wrun, \
+                   (const int2*)P->runs, (const int64_t*)B->rp, (const T*)B->val, (const uint16_t*)P->lidx, fa.q,  \
+                   fa.zraw, (T*)P->part, side ? fa.xt : nullptr, side ? (T*)P->zx_part : nullptr, fa.ev, fa.easq,  \
+                   fa.zout, fa.side_sq ? 1 : 0);                                                                    \
         return true;                                                                                                  \
     }
-    if (dbg) {   // timing experiments: the default shape only
-        if (W == 4 && MR == 2048 && G == 8 && NC == 1 && PRm && D == 2) {
+    if constexpr (GK) {
+        if (dbg) {   // timing experiments (hgm_spmv_ab only): the default shape
+            if (W == 4 && MR == 2048 && G == 8 && NC == 1 && PRm && D == 2) {
 #define HGM_RWD(DV) if (dbg == DV) HGM_RWL(4, 2048, 8, 1, 2, true, DV)
-            HGM_RWD(1) HGM_RWD(2) HGM_RWD(3) HGM_RWD(4) HGM_RWD(5) HGM_RWD(6) HGM_RWD(7)
+                HGM_RWD(1) HGM_RWD(2) HGM_RWD(4) HGM_RWD(7)
 #undef HGM_RWD
+            }
+            if (dry) return false;
+            throw Error{HGM_E_ARG, "fused_dbg (Golub-Kahan / fp32 pass): waves 4, 2048 slots, 8 rows, pairs, depth 2, one chunk; 1, 2, 4 or 7"};
         }
-        if (dry) return false;
-        throw Error{HGM_E_ARG, "fused_dbg with the row-wave pass: waves 4, 2048 slots, 8 rows, pairs, depth 2, one chunk"};
-    }
-    // production: pairs, 8-row batches, depth 2 (every shape, 1 or 2 chunks); the other
-    // variants for the default shape only (measurements)
 #define HGM_RW(WV, MRV)                                                                                              \
     if (W == WV && MR == MRV && G == 8 && PRm && D == 2) {                                                           \
         if (NC == 1) HGM_RWL(WV, MRV, 8, 1, 2, true, 0)                                                             \
         if (NC == 2) HGM_RWL(WV, MRV, 8, 2, 2, true, 0)                                                             \
     }
-    HGM_RW_SHAPES(HGM_RW)
+        HGM_RW_SHAPES_GK(HGM_RW)
 #undef HGM_RW
-    if (W == 4 && MR == 2048 && NC == 1 && PRm) {
-        if (G == 8 && D == 3) HGM_RWL(4, 2048, 8, 1, 3, true, 0)
-        if (G == 4 && D == 2) HGM_RWL(4, 2048, 4, 1, 2, true, 0)
-        if (G == 4 && D == 3) HGM_RWL(4, 2048, 4, 1, 3, true, 0)
+    } else {
+        if (dbg) {   // timing experiments: the default shape only
+            if (W == 4 && MR == 2048 && G == 8 && NC == 1 && PRm && D == 2) {
+#define HGM_RWD(DV) if (dbg == DV) HGM_RWL(4, 2048, 8, 1, 2, true, DV)
+                HGM_RWD(1) HGM_RWD(2) HGM_RWD(3) HGM_RWD(4) HGM_RWD(5) HGM_RWD(6) HGM_RWD(7)
+#undef HGM_RWD
+            }
+            if (dry) return false;
+            throw Error{HGM_E_ARG, "fused_dbg with the row-wave pass: waves 4, 2048 slots, 8 rows, pairs, depth 2, one chunk"};
+        }
+        // production: pairs, 8-row batches, depth 2 (every shape, 1 or 2 chunks); the other
+        // variants for the default shape only (measurements)
+#define HGM_RW(WV, MRV)                                                                                              \
+    if (W == WV && MR == MRV && G == 8 && PRm && D == 2) {                                                           \
+        if (NC == 1) HGM_RWL(WV, MRV, 8, 1, 2, true, 0)                                                             \
+        if (NC == 2) HGM_RWL(WV, MRV, 8, 2, 2, true, 0)                                                             \
     }
-    if (W == 4 && MR == 2048 && NC == 2 && !PRm && D == 2) {
-        if (G == 8) HGM_RWL(4, 2048, 8, 2, 2, false, 0)
-        if (G == 4) HGM_RWL(4, 2048, 4, 2, 2, false, 0)
+        HGM_RW_SHAPES(HGM_RW)
+#undef HGM_RW
+        if (W == 4 && MR == 2048 && NC == 1 && PRm) {
+            if (G == 8 && D == 3) HGM_RWL(4, 2048, 8, 1, 3, true, 0)
+            if (G == 4 && D == 2) HGM_RWL(4, 2048, 4, 1, 2, true, 0)
+            if (G == 4 && D == 3) HGM_RWL(4, 2048, 4, 1, 3, true, 0)
+        }
+        if (W == 4 && MR == 2048 && NC == 2 && !PRm && D == 2) {
+            if (G == 8) HGM_RWL(4, 2048, 8, 2, 2, false, 0)
+            if (G == 4) HGM_RWL(4, 2048, 4, 2, 2, false, 0)
+        }
     }
 #undef HGM_RWL
     if (dry) return false;
     throw Error{HGM_E_ARG, "fused A*(B*q): no row-wave kernel for this plan and options"};
+}
+
+// Whether the Golub-Kahan form of the pass (row epilogue, side sum of squares; every fp32 pass)
+// has a kernel for this plan and the options.
+bool fused_gk_ok(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P) {
+    if (!P || P->kind != 1) return false;
+    if (P->elem == 4) return fused_rw_launch<float, true>(c, B, P, FusedArgs<float>{}, true);
+    return fused_rw_launch<double, true>(c, B, P, FusedArgs<double>{}, true);
 }
 
 __global__ void k_copy_sys(const double* __restrict__ src, double* dst) {
@@ -1156,46 +1269,69 @@ void copy_sys(hgm_ctx* c, const double* src, double* dst) {
     HGM_HIP(hipGetLastError());
 }
 
-// Bq = B*q (n), ABq = A*(B*q) (m), one pass over B.
-bool fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq,
-              const double* xt, double* zx_out) {
-    const bool zx = xt && zx_out && P->kind == 1;
+// One pass over B (fa: internal.h FusedArgs): z = B*q, the row epilogue zs, w = A*zs, the side sum.
+template <typename T>
+bool fused_pass(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArgs<T>& fa) {
+    HGM_REQUIRE((int)sizeof(T) == P->elem && (int)sizeof(T) == (B->dtype == HGM_F32 ? 4 : 8), "fused pass: dtype");
+    const bool gk = fa.ev || fa.zout || fa.side_sq || sizeof(T) == 4;
+    const bool side = fa.side_out != nullptr && (fa.xt != nullptr || fa.side_sq) && P->kind == 1;
     hipEvent_t t0 = nullptr;
     timing_begin(c, KC_FUSED, &t0);
     if (P->kind == 1) {
-        fused_rw_launch(c, B, P, q, Bq, false, zx ? xt : nullptr);
+        if (gk) fused_rw_launch<T, true>(c, B, P, fa, false);
+        else if constexpr (sizeof(T) == 8) fused_rw_launch<T, false>(c, B, P, fa, false);
     } else {
+        HGM_REQUIRE(!gk && sizeof(T) == 8, "fused pass: the sub-chunk kernel is fp64 without epilogues");
+        if constexpr (sizeof(T) == 8) {
 #define HGM_FUSED_LAUNCH(FB, FGV, PFV)                                                                          \
     launch(c, false, k_fused_ab<FB, FGV, PFV>, dim3((unsigned)P->nreg), dim3(FB), (const FusedSub*)P->subs,      \
            (const int32_t*)P->reg_sub, (const int64_t*)P->reg_base, (const uint16_t*)P->perm,                    \
-           (const int32_t*)P->lr_ray, (const uint32_t*)P->lr_pk, (const int64_t*)B->rp, (const double*)B->val, q, \
-           Bq, P->part, c->num.fused_dbg)
-    // (one lane count per row sum for every variant: the same summation order, the same bits)
-    const int d = c->num.fused_pf;
-    if (c->num.fused_bs == 512) {
-        if (d <= 1) HGM_FUSED_LAUNCH(512, HGM_FUSED_FGR, 1);
-        else if (d == 2) HGM_FUSED_LAUNCH(512, HGM_FUSED_FGR, 2);
-        else if (d == 3) HGM_FUSED_LAUNCH(512, HGM_FUSED_FGR, 3);
-        else HGM_FUSED_LAUNCH(512, HGM_FUSED_FGR, 4);
-    } else {
-        if (d <= 1) HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 1);
-        else if (d == 2) HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 2);
-        else if (d == 3) HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 3);
-        else HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 4);
-    }
+           (const int32_t*)P->lr_ray, (const uint32_t*)P->lr_pk, (const int64_t*)B->rp, (const double*)B->val, fa.q, \
+           fa.zraw, P->part, c->num.fused_dbg)
+            // (one lane count per row sum for every variant: the same summation order, the same bits)
+            const int d = c->num.fused_pf;
+            if (c->num.fused_bs == 512) {
+                if (d <= 1) HGM_FUSED_LAUNCH(512, HGM_FUSED_FGR, 1);
+                else if (d == 2) HGM_FUSED_LAUNCH(512, HGM_FUSED_FGR, 2);
+                else if (d == 3) HGM_FUSED_LAUNCH(512, HGM_FUSED_FGR, 3);
+                else HGM_FUSED_LAUNCH(512, HGM_FUSED_FGR, 4);
+            } else {
+                if (d <= 1) HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 1);
+                else if (d == 2) HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 2);
+                else if (d == 3) HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 3);
+                else HGM_FUSED_LAUNCH(1024, HGM_FUSED_FGR, 4);
+            }
 #undef HGM_FUSED_LAUNCH
+        }
     }
     // one lane group per ray, no grid-stride cap (C4: 8,508 blocks; the 4,096 cap measured 5 us slower)
     const unsigned rgrid = (unsigned)std::max<int64_t>(1, (P->m * HGM_FUSED_RG + BS - 1) / BS);
-    launch(c, true, k_fused_reduce<HGM_FUSED_RG>, dim3(rgrid), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
-           (const int32_t*)P->rs_slot, (const double*)P->part, ABq, (const double*)P->zx_part, (int)P->nreg,
-           zx ? zx_out : nullptr);
+    launch(c, true, k_fused_reduce<HGM_FUSED_RG, T>, dim3(rgrid), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
+           (const int32_t*)P->rs_slot, (const T*)P->part, fa.w, (const T*)P->zx_part, (int)P->nreg,
+           side ? fa.side_out : nullptr);
     HGM_HIP(hipGetLastError());
     // algorithmic bytes of the fused pass: B's CSR once (values, 32-bit indices, row pointers),
-    // q read, z and w written (SURVEY.md §8(d)'s SpMV count for one pass over the operator)
-    const double bytes = 12.0 * (double)B->nnz + 8.0 * (B->rows + 1) + 8.0 * B->cols + 8.0 * B->rows + 8.0 * B->cols;
+    // q read, z and w written (SURVEY.md §8(d)'s SpMV count for one pass over the operator), and
+    // with the row epilogue its read of ev (the two-pass form's EPI_SUB operand)
+    const double s = (double)sizeof(T);
+    const double bytes = (s + 4.0) * (double)B->nnz + 8.0 * (B->rows + 1) + s * B->cols + s * B->rows + s * B->cols +
+                         (fa.ev ? s * B->rows : 0.0);
     timing_end(c, KC_FUSED, t0, bytes);
-    return zx;
+    return side;
+}
+template bool fused_pass<double>(hgm_ctx*, const hgm_mat*, const FusedPlan*, const FusedArgs<double>&);
+template bool fused_pass<float>(hgm_ctx*, const hgm_mat*, const FusedPlan*, const FusedArgs<float>&);
+
+// Bq = B*q (n), ABq = A*(B*q) (m), one pass over B.
+bool fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq,
+              const double* xt, double* zx_out) {
+    FusedArgs<double> fa;
+    fa.q = q;
+    fa.zraw = Bq;
+    fa.w = ABq;
+    fa.xt = xt;
+    fa.side_out = zx_out;
+    return fused_pass<double>(c, B, P, fa);
 }
 
 }  // namespace hgm

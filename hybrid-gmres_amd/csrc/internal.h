@@ -204,7 +204,8 @@ struct hgm_mat {
     uint16_t* pg_lidx = nullptr;
     // one-pass A*(B*q) plan over this pixel-major operator (fused.hip), built on first use
     hgm::FusedPlan* fused = nullptr;
-    bool fused_failed = false;
+    int64_t fused_key = -1;          // the option tuple the plan was built for (fused.hip fused_key)
+    int64_t fused_failed_key = -1;   // the last tuple whose plan was refused (-1: none)
 };
 
 namespace hgm {
@@ -363,6 +364,10 @@ template <typename T>
 void lsqr_step(hgm_ctx* c, int64_t n, T* x, T* w, T* v, const T* ssa, const T* coef, const double* st, int k,
                const T* xt, T* err_out);
 template <typename T> void div_sqrt(hgm_ctx* c, int64_t n, const T* in, T* out, const T* ss);
+// m-space half of a Golub-Kahan step after the one-pass w = A*v_hat (fused_pass): av = w / alpha
+// (optional: the kept A*v_k), t = av - alpha*u, *ss_out = ||t||^2 (alpha = sqrt(*ssa), device)
+template <typename T>
+void gkb_mstep(hgm_ctx* c, int64_t n, const T* w, const T* ssa, const T* u, T* t, T* av, T* ss_out);
 template <typename T>
 void lsmr_update(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, const T* v, T c_hbar, T c_x, T c_h,
                  bool first);
@@ -428,9 +433,39 @@ const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B);
 // x_true'(B*q), the m-space Gram error monitor's side dot, from the row sums as they form.
 bool fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq,
               const double* xt = nullptr, double* zx_out = nullptr);
+// The general pass (T = double or float; fp32 and every epilogue: the row-wave kernel).  Over B's
+// rows j (pixels) and columns i (rays):
+//   z_j = B(j,:) q ; zs_j = z_j - a ev_j with a = (T)sqrt((double)*easq) (no ev: zs = z) ;
+//   zraw = z, zout = zs (either optional; zout may alias ev) ; w_i = sum_j B(j,i) zs_j ;
+//   side_out (optional) = sum_j zs_j x_true_j, or sum_j zs_j^2 with side_sq.
+// The Golub-Kahan step of lsqr_solver.m:26-27 / lsmr_solver.m:38-39 is q = u_{k+1}, ev = v_k,
+// easq = beta^2: zout = v_hat, side_out = alpha^2 and w = A*v_hat, so A*v_{k+1} = w / alpha needs
+// no second pass over the operator.  Returns whether the side sum was formed.
+template <typename T>
+struct FusedArgs {
+    const T* q = nullptr;
+    T* zraw = nullptr;
+    T* w = nullptr;
+    const T* xt = nullptr;
+    const T* ev = nullptr;
+    const T* easq = nullptr;
+    T* zout = nullptr;
+    bool side_sq = false;
+    T* side_out = nullptr;
+};
+template <typename T>
+bool fused_pass(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArgs<T>& fa);
+// whether the Golub-Kahan form (row epilogue / side sum of squares, or fp32) runs for this plan
+bool fused_gk_ok(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P);
 // *dst = *src (one scalar, device to the host-visible ring, system scope), on the context stream
 void copy_sys(hgm_ctx* c, const double* src, double* dst);
 void fused_plan_free(FusedPlan* P);
+
+// Solver entry check: HGM_OPT_FUSED_DBG skips phases of the one-pass kernel (timing experiments of
+// hgm_spmv_ab only, scripts/fused_micro.py): a solve would return wrong results, so it is refused.
+inline void solver_guard(const hgm_ctx* c) {
+    HGM_REQUIRE(c->num.fused_dbg == 0, "fused_dbg is a timing experiment (hgm_spmv_ab only): set it to 0 to solve");
+}
 
 // ---------------- comm / scalars (capi.cpp) ----------------
 void allreduce(hgm_ctx* c, double* dev, int64_t count);

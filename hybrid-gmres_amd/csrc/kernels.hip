@@ -1488,6 +1488,47 @@ void div_sqrt(hgm_ctx* c, int64_t n, const T* in, T* out, const T* ss) {
     HGM_HIP(hipGetLastError());
 }
 
+// The m-space half of a Golub-Kahan step after the one-pass w = A*(A'*u - beta*v) (fused.hip):
+// A*v_k = w / alpha_k (alpha = (T)sqrt((double)*ssa); a zero alpha leaves w, as lsmr_solver.m:16/40
+// leave v undivided), kept in av when given, then t = A*v_k - alpha*u (lsqr_solver.m:22,
+// lsmr_solver.m:34; two roundings, as the two-pass EPI_SUB epilogue), with the partials of ||t||^2
+// in k_reduce_partial<T, 1>'s layout (parts == nullptr: none).
+template <typename T>
+__global__ __launch_bounds__(BS) void k_gkb_mstep(int64_t n, const T* __restrict__ w, const T* ssa,
+                                                  const T* __restrict__ u, T* __restrict__ t, T* __restrict__ av,
+                                                  T* __restrict__ parts) {
+    __shared__ T sh[4];
+    const T a = (T)sqrt((double)*ssa);
+    T acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
+        const T wi = w[i];
+        const T avi = a != T(0) ? wi / a : wi;
+        if (av) av[i] = avi;
+        const T s = a * u[i];
+        const T ti = avi - s;
+        t[i] = ti;
+        acc += ti * ti;
+    }
+    if (parts) {
+        const T tot = block_sum_all(acc, sh);
+        if (threadIdx.x == 0) parts[blockIdx.x] = tot;
+    }
+}
+
+template <typename T>
+void gkb_mstep(hgm_ctx* c, int64_t n, const T* w, const T* ssa, const T* u, T* t, T* av, T* ss_out) {
+    const bool fuse = n > SINGLE_MAX && !c->num.parity;
+    const int np = fuse ? parts_for(n) : grid_for(n);
+    T* parts = fuse ? c->buf<T>("red_parts", MAX_PARTS) : nullptr;
+    k_gkb_mstep<T><<<np, BS, 0, c->stream>>>(n, w, ssa, u, t, av, parts);
+    if (fuse) k_finalize<T><<<1, BS, 0, c->stream>>>(parts, np, ss_out);
+    HGM_HIP(hipGetLastError());
+    if (!fuse) sumsq<T>(c, n, t, ss_out);
+}
+template void gkb_mstep<double>(hgm_ctx*, int64_t, const double*, const double*, const double*, double*, double*,
+                                double*);
+template void gkb_mstep<float>(hgm_ctx*, int64_t, const float*, const float*, const float*, float*, float*, float*);
+
 // lsmr_solver.m:61-67
 template <typename T, bool FIRST>
 __global__ __launch_bounds__(BS) void k_lsmr_update(int64_t n, T* __restrict__ x, T* __restrict__ h,

@@ -230,6 +230,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
                  const double* b_in, const double* xt_in, double tol, int maxit, double lambda, double* x_out,
                  double* err_out, double* res_out, int* niters) {
     check_dims(A, B);
+    solver_guard(c);
     HGM_REQUIRE(B != nullptr, "B is NULL");
     const PixOrder po = n_order(c, A, B);
     HGM_REQUIRE(b_in != nullptr && xt_in != nullptr, "b and x_true are required");
@@ -275,12 +276,15 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // Per-iteration exchange ring in pinned host memory: slot k holds
     // [H(:,k) | Gram column k, AQk'b] (LH doubles), the monitors [res^2, err^2] of
     // iteration k, and the projected solution y_k.  Single GPU: the kernels write the
-    // slots in place and read y from it (zero-copy, no copy kernels).  Multi-GPU: the
-    // all-reduced scalars live in a device mirror and each slot is copied out once.
+    // slots in place and read y from it (zero-copy, no copy kernels).  Multi-GPU m-space side
+    // (the sharded AB-GMRES of configs[3]): the same, since the m-space sweep is replicated and
+    // every ring entry is written after its all-reduce (a sum that is all-reduced is formed in a
+    // device slot, all-reduced there and copied into the ring by copy_sys).  Multi-GPU n-space
+    // side: the all-reduced sweep scalars live in a device mirror and each slot is copied out once.
     const size_t LH = 2 * (size_t)(maxit + 2);
     const size_t offM = (size_t)maxit * LH, offY = offM + 2 * (size_t)maxit;
     const size_t offS = offY + (size_t)maxit * maxit;   // [beta, ||b||^2, ||x_true||^2] (polling)
-    const bool zc = !dist_n(c);
+    const bool zc = !dist_n(c) || !nspace;
     // Gram error monitor: step k's MGS sweep appends [Q(:,k)'Q(:,0:k-1),
     // Q(:,k)'Q(:,k), Q(:,k)'x_true] to the ring (LQ doubles) and the host evaluates
     // ||Q y_k - x_true||^2 from them, so an iteration's reconstruction reads only the kept A*Q.
@@ -310,11 +314,15 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // so it stays on the aux stream at any n: C3 1,376 vs 1,368 iters/s serialised)
     bool recon_serial = !gem && (int64_t)n >= c->num.recon_serial_n;
     if (c->num.recon_serial >= 0) recon_serial = c->num.recon_serial != 0;
-    hipStream_t rs_stream = (zc && !recon_serial) ? aux_stream(c) : st;
+    // (a communicator's solve keeps one stream whatever the ring)
+    hipStream_t rs_stream = (zc && !recon_serial && !dist_n(c)) ? aux_stream(c) : st;
     if (rs_stream != st) HGM_HIP(hipStreamSynchronize(rs_stream));
     pinned_ring(c, sizeof(double) * ring_n);
     const double* hr = c->hring;
     const bool poll = zc && c->num.ring_poll && !parity;
+    // the reconstruction's pipeline event: not needed when the host polls the ring and the
+    // reconstruction runs on the step stream (an event there is a bubble between two kernels)
+    const bool pipe_ev = !(poll && rs_stream == st);
     if (zc) {
         // the kernels store into the mapped ring with system-scope stores, and the pipeline
         // events carry no system-scope release, so a store may land after its kernel's event
@@ -352,6 +360,11 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         StreamScope scope(c, rs_stream, "aux:");
         sumsq<T>(c, m, b, dr + offS + 1);
         sumsq<T>(c, n, reinterpret_cast<const T*>(xt_in), dr + offS + 2);   // ||x_true - 0||^2
+    } else if (poll && dist_n(c)) {
+        sumsq<T>(c, m, b, dr + offS + 1);                    // (m: replicated)
+        sumsq<T>(c, n, xt, dslot<T>(c, S_NXT));              // ||x_true - 0||^2 over the pixel shards
+        allreduce(c, dslot<T>(c, S_NXT), 1);
+        copy_sys(c, dslot<T>(c, S_NXT), dr + offS + 2);
     } else if (poll) {
         sumsq<T>(c, m, b, dr + offS + 1);
         sumsq<T>(c, n, xt, dr + offS + 2);                   // ||x_true - 0||^2
@@ -433,7 +446,8 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
 #define HGM_FUSED_ZX 1
 #endif
                 const bool zxf = HGM_FUSED_ZX && gem_ab;
-                T* zx_dst = zxf ? dr + offQG + (size_t)kq * LQ + kq + 2 : nullptr;
+                // (on a communicator the rank-local dot goes to a device slot, all-reduced below)
+                T* zx_dst = zxf ? (dist_n(c) ? dslot<T>(c, S_AUX2) : dr + offQG + (size_t)kq * LQ + kq + 2) : nullptr;
                 // on a communicator the side dot rides the m-vector all-reduce as its element m
                 // (when the column's stride leaves room past m): one collective per step, not two
                 const int64_t wld = (ABQ && orth != HGM_CGS2) ? ldaq : ldq;
@@ -443,7 +457,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
                 zx_rode = ride && zx_fused;
                 if (dist_n(c)) allreduce(c, w, zx_rode ? m + 1 : m);             // (as apply_A)
                 if constexpr (std::is_same_v<T, double>)
-                    if (zx_rode) copy_sys(c, w + m, zx_dst);
+                    if (zx_rode) copy_sys(c, w + m, dr + offQG + (size_t)kq * LQ + kq + 2);
             } else {
                 apply_B<T>(c, B, qk, Bq, EPI_NONE, T(0), nullptr);                  // B*Q(:,k)
                 apply_A<T>(c, A, Bq, w, EPI_NONE, T(0), nullptr);                   // A*(B*Q(:,k))
@@ -475,17 +489,21 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             PendNorm<T>* defer = (pn_ok && kq + 1 < maxit) ? &pend : nullptr;
             if (!defer) pend.np = 0;
             MdotJob<T> zx;                                // gem_ab: x_true'(B*q_k) -> row entry k+2
+            T* zx_ring = dr + offQG + (size_t)kq * LQ + kq + 2;
             if (gem_ab) {
                 zx.n = n;
                 zx.w = BQ + (int64_t)kq * ldbq;
                 zx.e = xt;
-                zx.out = dr + offQG + (size_t)kq * LQ + kq + 2;
+                zx.out = dist_n(c) ? dslot<T>(c, S_AUX2) : zx_ring;   // (the fused pass's zx_dst too)
             }
             // the Gram row's extra dot: x_true (n-space) or b (m-space, unused: the row is for L)
             mgs<T>(c, dim, Q, ldq, kq, Hcol, dist, (!nspace && ABQ) ? ABQ + (int64_t)kq * ldaq : nullptr,
                    gem_ab ? (zx_fused ? nullptr : &zx) : side, defer, pending_in ? (const T*)pn_h : nullptr,
                    gem ? (gem_n ? xt : b) : nullptr, gem ? dr + offQG + (size_t)kq * LQ : nullptr);
-            if (gem_ab && dist_n(c) && !zx_rode) allreduce(c, zx.out, 1);   // x_true'(B*q_k) over the pixel shards
+            if (gem_ab && dist_n(c) && !zx_rode) {        // x_true'(B*q_k) over the pixel shards
+                allreduce(c, zx.out, 1);
+                if constexpr (std::is_same_v<T, double>) copy_sys(c, zx.out, zx_ring);
+            }
         }
         // Step kq-1's column is complete (H(kq,kq-1) came from this step's A product).  The
         // event goes at the end of the step: a marker between two kernels costs a bubble.
@@ -511,6 +529,14 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         const T* yk = c->hring_dev + offY + (size_t)kq * maxit;
         T* rslot = dr + offM + 2 * (size_t)kq;
         T* eslot = rslot + 1;
+        // an error sum over the pixel shards is all-reduced in a device slot, then copied into the
+        // (host-mapped) ring
+        T* eloc = (dist_n(c) && zc) ? dslot<T>(c, S_ERR) : eslot;
+        auto err_done = [&](bool reduce) {
+            if (reduce && dist_n(c)) allreduce(c, eloc, 1);
+            if constexpr (std::is_same_v<T, double>)
+                if (eloc != eslot) copy_sys(c, eloc, eslot);
+        };
         // ---- reconstruction (hybrid_*_rtp.m:30/33 ; *_bounds.m:37-38) ----
         if (aq_res) {
             // x = Q(:,1:k)*yk with ||x - x_true||^2 (:33/:36) and ||b - A*x||^2 (:32/:35)
@@ -520,18 +546,18 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             x_pending = want_x ? -1 : kq;
             if (dist_n(c)) allreduce(c, eslot, 1);
             publish(offM + 2 * (size_t)kq, 2);
-            pipe_record(c);
+            if (pipe_ev) pipe_record(c);
             return;
         }
         if (bq_res) {
             // xk = B*(Q(:,1:k)*yk) = (B*Q(:,1:k))*yk with ||xk - x_true||^2, and
             // ||b - A*xk||^2 = ||b - (A*B*Q(:,1:k))*yk||^2 (*_bounds.m:37-40), one launch
             // (want_x false: the m-space Gram error monitor has the error, x is formed at the end)
-            recon<T>(c, n, kk, BQ, ldbq, yk, want_x ? x : nullptr, xt, eslot, m, ABQ, ldaq, b, rslot);
+            recon<T>(c, n, kk, BQ, ldbq, yk, want_x ? x : nullptr, xt, eloc, m, ABQ, ldaq, b, rslot);
             x_pending = want_x ? -1 : kq;
-            if (dist_n(c) && want_x) allreduce(c, eslot, 1);
+            if (want_x) err_done(true);
             publish(offM + 2 * (size_t)kq, 2);
-            pipe_record(c);
+            if (pipe_ev) pipe_record(c);
             return;
         }
         if (nspace) {
@@ -541,7 +567,8 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         } else {
             gemv<T>(c, m, kk, Q, ldq, yk, z, 0);                 // zk = Q(:,1:k)*yk
             apply_B<T>(c, B, z, x, EPI_NONE, T(0), nullptr);     // xk = B*zk
-            nsumsq_diff<T>(c, n, x, xt, eslot);
+            sumsq_diff<T>(c, n, x, xt, eloc);
+            err_done(true);
         }
         // ---- monitors (hybrid_*_rtp.m:32-33 / :35-36): norm(b - A*x) ----
         if (!dist_n(c)) {
@@ -551,7 +578,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             sumsq<T>(c, m, tr, rslot);
         }
         publish(offM + 2 * (size_t)kq, 2);
-        pipe_record(c);
+        if (pipe_ev) pipe_record(c);
     };
     // Software pipeline over two streams, L = HGM_OPT_PIPE_DEPTH:
     //     main: S0 S1 S2 S3 ...          (S_k: Arnoldi step k -> H(:,k), Q(:,k+1))
@@ -586,7 +613,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     bool done = false;
     for (k = 0; k < maxit; ++k) {
         if (k >= 1) {                                    // R_{k-1}
-            pipe_wait(c);
+            if (pipe_ev) pipe_wait(c);
             wait_mon(k - 1);
         }
         if (poll) {
@@ -718,7 +745,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
             StreamScope scope(c, rs_stream, "aux:");
             stage_out_n<T>(c, x_out, x, n, dev, po);     // ends with a sync of the aux stream
             staged = true;
-        } else {
+        } else if (pipe_ev) {
             pipe_wait(c);
         }
         k = maxit - 1;
@@ -752,6 +779,7 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
            const double* xt_in, double tol, int maxit, bool hybrid, double lambda, double* x_out,
            double* err_out, double* res_out, int* niters) {
     check_dims(A, At);
+    solver_guard(c);
     HGM_REQUIRE(At != nullptr, "At is NULL");
     const PixOrder po = n_order(c, A, At);
     HGM_REQUIRE(b_in != nullptr && xt_in != nullptr, "b and x_true are required");
@@ -782,14 +810,34 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     r0.go();
     const double nb = std::sqrt((double)hs[0]);
     const double nxt = std::sqrt((double)hs[1]);
+    // One pass over the operator per iteration: with At = A' value for value on a
+    // tiled pixel grid, the step v_hat = A'*u - beta*v (:26) and A*v_hat come out of one pass over
+    // At (fused.hip, row epilogue), alpha^2 = ||v_hat||^2 as its side sum, and the next step's
+    // A*v_{k+1} (:22) is (A*v_hat) / alpha: an m-vector operation instead of a second pass.
+    // wm = [A*v_hat | alpha^2] (m + 1: alpha^2 rides the m-vector all-reduce on a communicator).
+    const FusedPlan* fp = (!hybrid && !parity) ? fused_ab_plan(c, A, At) : nullptr;
+    if (fp && !fused_gk_ok(c, At, fp)) fp = nullptr;
+    T* wm = fp ? c->buf<T>("gkb_wm", m + 2) : nullptr;
     // beta = norm(b) (lsqr_solver.m:7; hybrid: norm([b;0]) = norm(b), hybrid_lsqr_solver.m:9)
     double beta = nb;
     div_scalar<T>(c, m, b, u, (T)beta);                                        // :8  u = b / beta
     if (hybrid) fill<T>(c, n, un, T(0));                                       // u_aug = [b;0]/beta
-    if (hybrid) apply_B<T>(c, At, u, v, EPI_ADD, sq, un);                      // A_aug'*u_aug
-    else apply_B<T>(c, At, u, v, EPI_NONE, T(0), nullptr);                     // :10 v_hat = A'*u
-    nsumsq<T>(c, n, v, sl + S_ALPHA);
-    double alpha = std::sqrt((double)read1<T>(c, sl + S_ALPHA));               // :11
+    if (hybrid) {
+        apply_B<T>(c, At, u, v, EPI_ADD, sq, un);                              // A_aug'*u_aug
+    } else if (fp) {
+        FusedArgs<T> fa;                                                       // :10 v_hat = A'*u, A*v_hat
+        fa.q = u;
+        fa.zraw = v;
+        fa.w = wm;
+        fa.side_sq = true;
+        fa.side_out = wm + m;                                                  // ||v_hat||^2
+        fused_pass<T>(c, At, fp, fa);
+        if (dist_n(c)) allreduce(c, wm, m + 1);
+    } else {
+        apply_B<T>(c, At, u, v, EPI_NONE, T(0), nullptr);                      // :10 v_hat = A'*u
+    }
+    if (!fp) nsumsq<T>(c, n, v, sl + S_ALPHA);
+    double alpha = std::sqrt((double)read1<T>(c, fp ? wm + m : sl + S_ALPHA));   // :11
     div_scalar<T>(c, n, v, v, (T)alpha);                                       // :12
     HGM_HIP(hipMemcpyAsync(w, v, sizeof(T) * n, hipMemcpyDeviceToDevice, c->stream));   // :14 w = v
     double phi_bar = beta, rho_bar = alpha;                                    // :15-16
@@ -803,7 +851,49 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     // double arithmetic as the host loop below -- the same bits, with no host round trip per
     // iteration.  The host reads the stop flag once per batch of iterations (none when tol <= 0
     // cannot stop early); an iteration enqueued past the stop leaves x and w untouched.
-    const bool dev_scalars = !hybrid && !parity && !dist_n(c) && c->num.lsqr_dev;
+    const bool dev_scalars = !fp && !hybrid && !parity && !dist_n(c) && c->num.lsqr_dev;
+    if (fp) {
+        // one pass per iteration, device-resident scalars (as below; on a communicator too: alpha^2
+        // rides the m-vector all-reduce, beta^2 is a sum over the replicated m-vector)
+        double* st = c->buf<double>("lsqr_st", 4);
+        double* phib = c->buf<double>("lsqr_phib", maxit);
+        T* coef = c->buf<T>("lsqr_coef", 2);
+        const double st0[4] = {rho_bar, phi_bar, 0.0, 0.0};
+        h2d(c, st, st0, sizeof(st0));
+        FusedArgs<T> fa;
+        fa.q = u;
+        fa.ev = v;                                 // v_k (divided by the previous lsqr_step)
+        fa.easq = sl + S_BETA;
+        fa.zout = v;                               // v_hat_{k+1} in place
+        fa.w = wm;
+        fa.side_sq = true;
+        fa.side_out = wm + m;
+        const int batch = tol > 0 ? 8 : maxit;
+        int stop = 0;
+        for (k = 0; k < maxit && stop == 0;) {
+            const int kend = std::min(maxit, k + batch);
+            for (; k < kend; ++k) {
+                gkb_mstep<T>(c, m, wm, wm + m, u, t, nullptr, sl + S_BETA);          // :22-23 A*v - alpha*u
+                div_sqrt<T>(c, m, t, u, sl + S_BETA);                                // :24
+                fused_pass<T>(c, At, fp, fa);                                        // :26-27 (+ A*v_hat)
+                if (dist_n(c)) allreduce(c, wm, m + 1);
+                lsqr_rot<T>(c, sl + S_BETA, wm + m, st, coef, phib, k, nb, tol);     // :31-38, :44-46
+                lsqr_step<T>(c, n, x, w, v, wm + m, coef, st, k, xt, errh + k);     // :28, :40-41, :43
+                if (dist_n(c)) allreduce(c, errh + k, 1);
+            }
+            double sv = 0;
+            Reader rs(c);
+            rs.add(&sv, st + 2, sizeof(double));
+            rs.go();
+            stop = (int)sv;
+        }
+        k = stop > 0 ? stop - 1 : maxit;
+        std::vector<double> pbh(maxit);
+        Reader rh(c);
+        rh.add(pbh.data(), phib, sizeof(double) * maxit);
+        rh.go();
+        for (int i = 0; i < maxit && i <= k; ++i) res[i] = std::fabs(pbh[i]) / nb;   // :44
+    }
     if (dev_scalars) {
         double* st = c->buf<double>("lsqr_st", 4);
         double* phib = c->buf<double>("lsqr_phib", maxit);
@@ -839,7 +929,7 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         rh.go();
         for (int i = 0; i < maxit && i <= k; ++i) res[i] = std::fabs(pbh[i]) / nb;   // :44
     }
-    for (; !dev_scalars && k < maxit; ++k) {
+    for (; !dev_scalars && !fp && k < maxit; ++k) {
         // :22-24  u_hat = A*v - alpha*u ; beta = norm(u_hat) ; u = u_hat / beta
         apply_A<T>(c, A, v, t, EPI_SUB, (T)alpha, u);
         sumsq<T>(c, m, t, sl + S_BETA);
@@ -929,6 +1019,7 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
            const double* xt_in, double tol, int maxit, double* x_out, double* err_out, double* res_out,
            double* ar_out, int* iters) {
     check_dims(A, At);
+    solver_guard(c);
     HGM_REQUIRE(At != nullptr, "At is NULL");
     const PixOrder po = n_order(c, A, At);
     HGM_REQUIRE(b_in != nullptr, "b is required");
@@ -1000,13 +1091,29 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         fill<double>(c, n, Ixn, 0.0);                                          // A'A*x_0 = 0
         apply_B<T>(c, At, b, Atb, EPI_NONE, T(0), nullptr);                    // A'*b (once per solve)
     }
+    // One pass over the operator per iteration (as lsqr_t): the step :38-39 and
+    // A*v_hat in one pass over At, A*v_{k+1} (:34, the kept A*v) = (A*v_hat) / alpha.
+    const FusedPlan* fp = !parity ? fused_ab_plan(c, A, At) : nullptr;
+    if (fp && !fused_gk_ok(c, At, fp)) fp = nullptr;
+    T* wm = fp ? c->buf<T>("gkb_wm", m + 2) : nullptr;                         // [A*v_hat | alpha^2]
     HGM_HIP(hipMemcpyAsync(u, b, sizeof(T) * m, hipMemcpyDeviceToDevice, c->stream));   // :10
     double beta = nb;                                                          // :11
     if (beta > 0) div_scalar<T>(c, m, u, u, (T)beta);                          // :12
     T* v0 = kept ? Atu0 : v;                                                   // raw A'*u_0 kept
-    apply_B<T>(c, At, u, v0, EPI_NONE, T(0), nullptr);                         // :14
-    nsumsq<T>(c, n, v0, sl + S_ALPHA);
-    double alpha = std::sqrt((double)read1<T>(c, sl + S_ALPHA));              // :15
+    if (fp) {
+        FusedArgs<T> fa;                                                       // :14 (+ A*v_hat, ||v_hat||^2)
+        fa.q = u;
+        fa.zraw = v0;
+        fa.w = wm;
+        fa.side_sq = true;
+        fa.side_out = wm + m;
+        fused_pass<T>(c, At, fp, fa);
+        if (dist_n(c)) allreduce(c, wm, m + 1);
+    } else {
+        apply_B<T>(c, At, u, v0, EPI_NONE, T(0), nullptr);                     // :14
+        nsumsq<T>(c, n, v0, sl + S_ALPHA);
+    }
+    double alpha = std::sqrt((double)read1<T>(c, fp ? wm + m : sl + S_ALPHA));   // :15
     if (alpha > 0) div_scalar<T>(c, n, v0, v, (T)alpha);                       // :16
     else if (kept) HGM_HIP(hipMemcpyAsync(v, v0, sizeof(T) * n, hipMemcpyDeviceToDevice, c->stream));
     double zetabar = alpha * beta, alphabar = alpha, rho = 1, rhobar = 1, cbar = 1, sbar = 0;   // :19-23
@@ -1026,23 +1133,43 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     int k = 0;
     for (k = 0; k < maxit; ++k) {
         const double alpha_k = alpha;
-        if (kept) {
-            apply_A<T>(c, A, v, Av, EPI_NONE, T(0), nullptr);                  // A*v_k (kept)
-            epilogue_to<T>(c, m, Av, u, EPI_SUB, (T)alpha, u);                 // :34 u = A*v - alpha*u
+        if (fp) {
+            // :34 A*v_k = (A*v_hat)/alpha_k (kept), u = A*v - alpha*u, ||u||^2
+            gkb_mstep<T>(c, m, wm, wm + m, u, r, kept ? Av : nullptr, sl + S_BETA);
+            beta = std::sqrt((double)read1<T>(c, sl + S_BETA));               // :35
+            if (beta > 0) div_scalar<T>(c, m, r, u, (T)beta);                  // :36
+            else HGM_HIP(hipMemcpyAsync(u, r, sizeof(T) * m, hipMemcpyDeviceToDevice, c->stream));
+            FusedArgs<T> fa;                                                   // :38 v = A.'*u - beta*v, one pass
+            fa.q = u;
+            fa.zraw = kept ? Atu1 : nullptr;                                   // A'*u_{k+1} (kept)
+            fa.ev = v;
+            fa.easq = sl + S_BETA;
+            fa.zout = v;
+            fa.w = wm;
+            fa.side_sq = true;
+            fa.side_out = wm + m;                                              // ||v||^2 (:39)
+            fused_pass<T>(c, At, fp, fa);
+            if (dist_n(c)) allreduce(c, wm, m + 1);
+            alpha = std::sqrt((double)read1<T>(c, wm + m));                    // :39
         } else {
-            apply_A<T>(c, A, v, u, EPI_SUB, (T)alpha, u);                      // :34 u = A*v - alpha*u
+            if (kept) {
+                apply_A<T>(c, A, v, Av, EPI_NONE, T(0), nullptr);              // A*v_k (kept)
+                epilogue_to<T>(c, m, Av, u, EPI_SUB, (T)alpha, u);             // :34 u = A*v - alpha*u
+            } else {
+                apply_A<T>(c, A, v, u, EPI_SUB, (T)alpha, u);                  // :34 u = A*v - alpha*u
+            }
+            sumsq<T>(c, m, u, sl + S_BETA);
+            beta = std::sqrt((double)read1<T>(c, sl + S_BETA));               // :35
+            if (beta > 0) div_scalar<T>(c, m, u, u, (T)beta);                  // :36
+            if (kept) {
+                apply_B<T>(c, At, u, Atu1, EPI_NONE, T(0), nullptr);           // A'*u_{k+1} (kept)
+                epilogue_to<T>(c, n, Atu1, v, EPI_SUB, (T)beta, v);            // :38 v = A.'*u - beta*v
+            } else {
+                apply_B<T>(c, At, u, v, EPI_SUB, (T)beta, v);                  // :38 v = A.'*u - beta*v
+            }
+            nsumsq<T>(c, n, v, sl + S_ALPHA);
+            alpha = std::sqrt((double)read1<T>(c, sl + S_ALPHA));             // :39
         }
-        sumsq<T>(c, m, u, sl + S_BETA);
-        beta = std::sqrt((double)read1<T>(c, sl + S_BETA));                   // :35
-        if (beta > 0) div_scalar<T>(c, m, u, u, (T)beta);                      // :36
-        if (kept) {
-            apply_B<T>(c, At, u, Atu1, EPI_NONE, T(0), nullptr);               // A'*u_{k+1} (kept)
-            epilogue_to<T>(c, n, Atu1, v, EPI_SUB, (T)beta, v);                // :38 v = A.'*u - beta*v
-        } else {
-            apply_B<T>(c, At, u, v, EPI_SUB, (T)beta, v);                      // :38 v = A.'*u - beta*v
-        }
-        nsumsq<T>(c, n, v, sl + S_ALPHA);
-        alpha = std::sqrt((double)read1<T>(c, sl + S_ALPHA));                 // :39
         if (alpha > 0) div_scalar<T>(c, n, v, v, (T)alpha);                    // :40
         const double alphahat = alphabar;                                      // :42
         const double rhoold = rho;                                             // :43
@@ -1118,6 +1245,7 @@ int hybrid_lsmr(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* 
                 const double* xt_in, double tol, int maxit, double lambda, double* x_out, double* err_out,
                 double* res_out, int* niters) {
     check_dims(A, At);
+    solver_guard(c);
     HGM_REQUIRE(At != nullptr, "At is NULL");
     const PixOrder po = n_order(c, A, At);
     HGM_REQUIRE(A->dtype == HGM_F64, "hybrid LSMR is fp64");
@@ -1221,6 +1349,7 @@ int hybrid_lsmr(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* 
 int arnoldi(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const double* b_in, int kg, int side,
             double btol, int orth, double* H_out, double* beta_out, int* kdone) {
     check_dims(A, B);
+    solver_guard(c);
     HGM_REQUIRE(B != nullptr, "B is NULL");
     (void)n_order(c, A, B);   // H does not depend on the stored pixel order (up to rounding)
     HGM_REQUIRE(A->dtype == HGM_F64, "Arnoldi is fp64");

@@ -1,7 +1,8 @@
 """Micro-benchmark of the m-space operator A*(B*q) (hgm_spmv_ab) at a BASELINE geometry: the
 one-pass kernel (fused.hip) against the two SpMVs, and phase-skip timing variants (fused_dbg:
 results wrong, timing only).  Prints one JSON line per variant.  Run on the GPU box:
-    python scripts/fused_micro.py [N angles reps]"""
+    python scripts/fused_micro.py [N angles reps [variants]]
+HGM_MICRO_F32=1: the fp32 operator (BASELINE configs[4]; the fp32 one-pass kernel)."""
 import ctypes as C
 import json
 import re
@@ -20,15 +21,18 @@ N, na, reps = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (4096, 4
 variants = sys.argv[4].split(",") if len(sys.argv) > 4 else ["two", "f1024", "f512", "d1", "d2", "d4", "d8", "d15"]
 ctx = hgmres.Context(0)
 lib = L.load()
-A = hgmres.SparseOperator.siddon(N, na, ctx=ctx)
+f32 = os.environ.get("HGM_MICRO_F32", "0") == "1"
+A = hgmres.SparseOperator.siddon(N, na, ctx=ctx, dtype=L.HGM_F32 if f32 else L.HGM_F64)
 B = A.T
 m, n = A.shape
 dev = torch.device("cuda", 0)
-q = torch.from_numpy(np.random.default_rng(0).standard_normal(m)).to(dev)
-bq = torch.empty(n, dtype=torch.float64, device=dev)
-abq = torch.empty(m, dtype=torch.float64, device=dev)
+tdt = torch.float32 if f32 else torch.float64
+q = torch.from_numpy(np.random.default_rng(0).standard_normal(m)).to(dev).to(tdt)
+bq = torch.empty(n, dtype=tdt, device=dev)
+abq = torch.empty(m, dtype=tdt, device=dev)
 P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
-two = 2 * 12.0 * A.nnz + 8.0 * (m + 1) + 8.0 * (n + 1) + 16.0 * (m + n)
+s_ = 4.0 if f32 else 8.0
+two = 2 * (s_ + 4) * A.nnz + 8.0 * (m + 1) + 8.0 * (n + 1) + 2 * s_ * (m + n)
 ref = None
 for vname in variants:
     # two | f<threads>[x<depth>][r<region>] (fused, pipeline depth [2], region side [64])
@@ -63,5 +67,5 @@ for vname in variants:
         ref = (bq.cpu().numpy(), out)
     dev_ = None if ref is None else float(np.linalg.norm(out - ref[1]) / np.linalg.norm(ref[1]))
     devz = None if ref is None else float(np.linalg.norm(bq.cpu().numpy() - ref[0]) / np.linalg.norm(ref[0]))
-    print(json.dumps({"variant": vname, "N": N, "angles": na, "ms": round(dt * 1e3, 4),
+    print(json.dumps({"variant": vname, "N": N, "angles": na, "dtype": "f32" if f32 else "f64", "ms": round(dt * 1e3, 4),
                       "effective_GBps_two_pass": round(two / dt / 1e9, 1), "rel_dev_vs_two_pass": dev_, "bq_rel_dev": devz}), flush=True)

@@ -96,6 +96,23 @@ def solve_all(ctx, rank, world):
     res.update(tabn_x=out_[0], tabn_res=out_[2], tabn_err=out_[1], tabn_H=out_[-1])
     x, e, r, k, H = hgmres.hybrid_ba_gmres_rtp(A2, B2, P.b, xs[tlo:thi], 0.0, 15, 1e-2, ctx=ctx, return_H=True)
     res.update(thba_x=x, thba_res=r, thba_err=e, thba_H=H)
+    # configs[2]'s GCV on pixel shards: the n-space Arnoldi (sharded basis) once, fminbnd on the
+    # cached H with the GLOBAL pixel count as the trace term (gcv_function.m:46-50; bench.py c3gcv),
+    # and the one-call gcv_function (the library all-reduces n itself)
+    Hg, beta_g, kd = hgmres.arnoldi(A_g, B_g, P.b, 20, "ba", ctx=ctx)
+    lam, gval = hgmres.gcv_fminbnd(Hg, beta_g, float(P.A.shape[1]), 1e-8, 1.0, 1e-10)
+    gfix = hgmres.gcv_function(1e-3, A_g, B_g, P.b, P.A.shape[0], 20, "ba", ctx=ctx)
+    res.update(gcv_H=Hg, gcv_beta=beta_g, gcv_lam=lam, gcv_val=gval, gcv_fix=gfix)
+    # configs[4] as bench.py build_shard cuts it: fp32 tiled shards of the fp32 operator (one pass
+    # per Golub-Kahan iteration on each shard, A*v_hat all-reduced with alpha^2 riding along)
+    from hgmres import _lib as L
+    Af32 = hgmres.SparseOperator.siddon(64, 90, ctx=ctx, order=(4, 0), dtype=L.HGM_F32)
+    B32s = Af32.T.row_slice(tlo, thi)
+    A32s = B32s.T
+    x, e, r, k = hgmres.lsqr_solver(A32s, P.b, xs[tlo:thi], 0.0, 6, ctx=ctx, At=B32s)
+    res.update(tlsqr32_x=x, tlsqr32_res=r, tlsqr32_err=e)
+    x, e, r, a, k = hgmres.lsmr_solver(A32s, P.b, xs[tlo:thi], 0.0, 6, ctx=ctx, At=B32s)
+    res.update(tlsmr32_x=x, tlsmr32_res=r, tlsmr32_err=e, tlsmr32_ar=a)
     res.update(lo=lo, hi=hi, tlo=tlo, thi=thi)
     return res
 

@@ -44,6 +44,15 @@ def test_gpus_n_spawns_n_ranks(n, workload):
     assert max(sizes) - min(sizes) <= 4 * N
 
 
+@pytest.mark.parametrize("workload,dtype", [("c4", "f64"), ("c5", "f32"), ("c5m", "f32"), ("c3gcv", "f64")])
+def test_plan_carries_dtype(workload, dtype):
+    """configs[4] (c5/c5m) is fp32 on N GPUs: the plan every rank follows names that dtype
+    (bench.py build_shard cuts the fp32 shards; main() refuses operators of another dtype)."""
+    rc, d, p = _run(["--gpus", "2", "--dry-run", "--workload", workload])
+    assert rc == 0, p.stderr[-2000:]
+    assert d["dtype"] == dtype and d["mode"] == "pixel-sharded"
+
+
 def test_replicas_plan():
     rc, d, _ = _run(["--gpus", "2", "--dry-run", "--replicas"])
     assert rc == 0 and d["mode"] == "replicas" and d["world"] == 2

@@ -154,3 +154,135 @@ def test_fused_on_pixel_shards(gpu_ctx, world, kind):
         A_g.close()
         B_g.close()
     assert rel(total, full) <= 1e-13
+
+
+# ---------------------------------------------------------------------------------------------
+# One pass per Golub-Kahan iteration: with At = A' value for value on the tiled
+# grid, lsqr_solver / lsmr_solver form v_hat = A'*u - beta*v and A*v_hat in one pass over At (the
+# row epilogue of the row-wave kernel), alpha^2 as its side sum, and A*v_{k+1} = (A*v_hat)/alpha.
+# That differs from A*(v_hat/alpha) by rounding only; the Golub-Kahan recurrences amplify rounding
+# about tenfold per iteration, so the bars are those of the production GKB tests:
+# 1e-10 against the oracle over the first iterations, bitwise repeats, and fp32 against the fp32
+# oracle within the fp32 envelope.
+# ---------------------------------------------------------------------------------------------
+def _gkb_pair(ctx, N, na, dtype=None):
+    from hgmres import _lib as L
+    A64, _, b, xt = _device_problem(ctx, N, na)
+    if dtype is None:
+        return A64, A64.T, b, xt
+    A = hgmres.SparseOperator.siddon(N, na, ctx=ctx, dtype=L.HGM_F32)
+    return A, A.T, b, xt
+
+
+@pytest.mark.parametrize("N,na", [(256, 47), (200, 60), (128, 90)])
+def test_fused_gkb_fp64_matches_two_pass_and_oracle(gpu_ctx, N, na):
+    A, At, b, xt = _gkb_pair(gpu_ctx, N, na)
+    k = 8
+    with gpu_ctx.options(fused_ab=0):
+        q2 = hgmres.lsqr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+        m2 = hgmres.lsmr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+    with gpu_ctx.options(fused_ab=1):
+        q1 = hgmres.lsqr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+        q1b = hgmres.lsqr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+        m1 = hgmres.lsmr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+        m1b = hgmres.lsmr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+    for a_, b_ in list(zip(q1, q1b)) + list(zip(m1, m1b)):
+        assert np.array_equal(np.asarray(a_), np.asarray(b_))               # bitwise reproducible
+    As = A.to_scipy()
+    xo, eo, ro, ko = R.lsqr_solver(As, b, xt, 0.0, k)
+    mo = R.lsmr_solver(As, b, xt, 0.0, k)
+    def devs(q, mm):
+        return dict(lsqr_x=rel(q[0], xo), lsqr_res=hist_dev(q[2], ro), lsqr_err=hist_dev(q[1], eo),
+                    lsmr_x=rel(mm[0], mo[0]), lsmr_res=hist_dev(mm[2], mo[2]), lsmr_err=hist_dev(mm[1], mo[1]),
+                    lsmr_ar=hist_dev(mm[3], mo[3]))
+    dev, dev2 = devs(q1, m1), devs(q2, m2)
+    print(f"[fused gkb fp64 N={N} angles={na} k={k}] " + " ".join(f"{a}={v:.1e}" for a, v in dev.items()) +
+          " | two-pass: " + " ".join(f"{a}={v:.1e}" for a, v in dev2.items()))
+    assert q1[3] == m1[4] == k
+    # the one-pass solve holds the production bar: 1e-10 against the oracle, or (where the two-pass
+    # production solve itself is past 1e-10 at k = 8: GKB rounding growth) within 3x of its deviation
+    for key in dev:
+        assert dev[key] <= max(TOL, 3 * dev2[key]), key
+
+
+@pytest.mark.parametrize("N,na", [(256, 47), (128, 90)])
+def test_fused_gkb_fp32_matches_oracle(gpu_ctx, N, na):
+    """configs[4]'s path at test size: the fp32 one-pass LSQR / LSMR against the fp32 restatement
+    (oracle/restatement.py lsqr_solver_f32 / lsmr_solver_f32) and the fp32 two-pass solve.  The
+    fp32 rows sum in another order, so the bar is the production fp32 envelope:
+    1e-5 on every history entry through iteration 4."""
+    A, At, b, xt = _gkb_pair(gpu_ctx, N, na, dtype="f32")
+    k = 4
+    with gpu_ctx.options(fused_ab=0):
+        q2 = hgmres.lsqr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+        m2 = hgmres.lsmr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+    with gpu_ctx.options(fused_ab=1):
+        q1 = hgmres.lsqr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+        q1b = hgmres.lsqr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+        m1 = hgmres.lsmr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+    for a_, b_ in zip(q1, q1b):
+        assert np.array_equal(np.asarray(a_), np.asarray(b_))
+    As = A.to_scipy()                              # fp32 values (exact in float64)
+    xo, eo, ro, ko = R.lsqr_solver_f32(As, b, xt, 0.0, k)
+    mo = R.lsmr_solver_f32(As, b, xt, 0.0, k)
+    dev = dict(lsqr_x=rel(q1[0], xo), lsqr_res=hist_dev(q1[2], ro), lsqr_err=hist_dev(q1[1], eo),
+               lsmr_x=rel(m1[0], mo[0]), lsmr_res=hist_dev(m1[2], mo[2]), lsmr_err=hist_dev(m1[1], mo[1]),
+               two_pass_lsqr_x=rel(q2[0], xo), vs_two_pass_lsqr_x=rel(q1[0], q2[0]),
+               vs_two_pass_lsmr_x=rel(m1[0], m2[0]))
+    print(f"[fused gkb fp32 N={N} angles={na} k={k}] " + " ".join(f"{a}={v:.1e}" for a, v in dev.items()))
+    for key in ("lsqr_res", "lsqr_err", "lsmr_res", "lsmr_err"):
+        assert dev[key] <= 1e-5, key
+    for key in ("lsqr_x", "lsmr_x", "vs_two_pass_lsqr_x", "vs_two_pass_lsmr_x"):
+        assert dev[key] <= 1e-4, key
+
+
+def test_fused_spmv_ab_fp32(gpu_ctx):
+    """hgm_spmv_ab on an fp32 pair runs the fp32 one-pass kernel: within fp32 rounding of the
+    two-pass product, bitwise repeatable."""
+    A, At, b, xt = _gkb_pair(gpu_ctx, 256, 47, dtype="f32")
+    B = At
+    q = np.random.default_rng(3).standard_normal(A.shape[0]).astype(np.float32)
+    with gpu_ctx.options(fused_ab=0):
+        bq2, ab2 = hgmres.spmv_ab(A, B, q)
+    with gpu_ctx.options(fused_ab=1):
+        bq1, ab1 = hgmres.spmv_ab(A, B, q)
+        bq1b, ab1b = hgmres.spmv_ab(A, B, q)
+    assert bq1.dtype == np.float32 and ab1.dtype == np.float32
+    assert np.array_equal(ab1, ab1b) and np.array_equal(bq1, bq1b)
+    Bs = B.to_scipy()
+    ref_bq = Bs @ q.astype(np.float64)
+    ref_ab = Bs.T @ ref_bq
+    print(f"[fused spmv_ab fp32] bq {rel(bq1, ref_bq):.1e} (two-pass {rel(bq2, ref_bq):.1e}), "
+          f"ab {rel(ab1, ref_ab):.1e} (two-pass {rel(ab2, ref_ab):.1e})")
+    assert rel(bq1, ref_bq) <= 1e-6 and rel(ab1, ref_ab) <= 1e-6
+
+
+def test_fused_failed_plan_is_retried_with_other_options(gpu_ctx):
+    """a refused plan (a 64 x 64 region holds more rays than four waves' LDS) is
+    remembered for THAT option tuple only; the default options then plan and run the one pass
+    on the same operator (kernel timing sees the fused class)."""
+    A, B, b, xt = _device_problem(gpu_ctx, 256, 47)
+    q = np.random.default_rng(2).standard_normal(A.shape[0])
+    with gpu_ctx.options(fused_ab=0):
+        _, ref = hgmres.spmv_ab(A, B, q)
+    with gpu_ctx.options(**_fused_opts(1, 64)):
+        _, r64 = hgmres.spmv_ab(A, B, q)                  # refused: the two-pass product
+    assert np.array_equal(r64, ref)
+    gpu_ctx.kernel_timing(True)
+    try:
+        _, r32 = hgmres.spmv_ab(A, B, q)                  # defaults: the one pass
+        ms, calls, _ = gpu_ctx.kernel_timing_read(3)
+    finally:
+        gpu_ctx.kernel_timing(False)
+    assert calls == 1 and rel(r32, ref) <= 1e-13
+
+
+def test_fused_dbg_refused_by_solvers(gpu_ctx):
+    """fused_dbg (phase-skipping timing variants, wrong results) is refused by every
+    solver; hgm_spmv_ab keeps it for scripts/fused_micro.py."""
+    A, B, b, xt = _device_problem(gpu_ctx, 64, 17)
+    with gpu_ctx.options(fused_dbg=1):
+        with pytest.raises(hgmres.HgmError, match="fused_dbg"):
+            hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 4, ctx=gpu_ctx)
+        with pytest.raises(hgmres.HgmError, match="fused_dbg"):
+            hgmres.lsqr_solver(A, b, xt, 0.0, 4, ctx=gpu_ctx, At=B)

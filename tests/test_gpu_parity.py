@@ -978,3 +978,38 @@ def test_shard_emulation_two_ranks(tmp_path):
         assert np.array_equal(o[0][f"{tag}_res"], o[1][f"{tag}_res"])
         hist_ok(o[0][f"{tag}_res"], s[f"{ref}_res"], TOL)
         H_ok(o[0][f"{tag}_H"], s[f"{ref}_H"])
+    # --- against the ORACLE, not only the 1-rank library solve (VERDICT r3 "Next" #1) ---
+    import scipy.optimize as so
+    from hgmres import _lib as L
+    P = tomo_problem(64, 90, noise=1e-2, seed=0)
+    # sharded GCV (configs[2]): H of the sharded Arnoldi, the GCV lambda with the global trace n
+    Ho, beta_o = R.arnoldi(P.A, P.B, P.b, 20, "ba")
+    H_ok(o[0]["gcv_H"], Ho)
+    assert np.array_equal(o[0]["gcv_H"], o[1]["gcv_H"])
+    n = P.A.shape[1]
+    lam_o, g_o, _, _ = so.fminbound(lambda l: R.gcv_from_H(Ho, beta_o, l, n), 1e-8, 1.0, xtol=1e-10,
+                                    full_output=True)
+    lam2, lam1 = float(o[0]["gcv_lam"]), float(s["gcv_lam"])
+    print(f"[shard gcv] lambda 2-rank {lam2:.12e} 1-rank {lam1:.12e} oracle {lam_o:.12e}; "
+          f"G {float(o[0]['gcv_val']):.12e} vs oracle {g_o:.12e}")
+    assert abs(lam2 - lam1) <= 1e-8 * lam1          # the same cached-H search on H equal to ~1e-13
+    assert abs(float(o[0]["gcv_val"]) - g_o) <= 1e-9 * g_o
+    assert abs(float(o[0]["gcv_val"]) - float(s["gcv_val"])) <= 1e-10 * float(s["gcv_val"])
+    g_fix = R.gcv_function(1e-3, P.A, P.B, P.b, P.A.shape[0], 20, "ba")
+    assert abs(float(o[0]["gcv_fix"]) - g_fix) <= 1e-9 * g_fix
+    # sharded fp32 Golub-Kahan (configs[4]) on the tiled fp32 shards vs the fp32 restatement on
+    # the same fp32 operator (reference order): the production fp32 envelope through 6 iterations
+    ctx1 = hgmres.default_context()
+    A32 = hgmres.SparseOperator.siddon(64, 90, ctx=ctx1, order=(4, 0), dtype=L.HGM_F32).to_scipy()
+    xs = np.empty(n)
+    xs[perm] = P.x_true
+    xq, eq, rq, _ = R.lsqr_solver_f32(A32, P.b, P.x_true, 0.0, 6)
+    xm, em, rm, am, _ = R.lsmr_solver_f32(A32, P.b, P.x_true, 0.0, 6)
+    for tag, (xo_, eo_, ro_) in (("tlsqr32", (xq, eq, rq)), ("tlsmr32", (xm, em, rm))):
+        x2 = np.concatenate([o[0][f"{tag}_x"], o[1][f"{tag}_x"]])[perm]
+        d = dict(x=rel(x2, xo_), res=float(np.max(np.abs(o[0][f"{tag}_res"] - ro_) / ro_)),
+                 err=float(np.max(np.abs(o[0][f"{tag}_err"] - eo_) / eo_)),
+                 vs_1rank=rel(np.concatenate([o[0][f"{tag}_x"], o[1][f"{tag}_x"]]), s[f"{tag}_x"]))
+        print(f"[shard {tag} vs fp32 oracle] " + " ".join(f"{a}={v:.1e}" for a, v in d.items()))
+        assert np.array_equal(o[0][f"{tag}_res"], o[1][f"{tag}_res"])
+        assert d["res"] <= 1e-4 and d["err"] <= 1e-4 and d["x"] <= 1e-3 and d["vs_1rank"] <= 1e-3, tag
