@@ -527,6 +527,10 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             n.fused_depth = (int)v;
             break;
         case HGM_OPT_FUSED_PAIRS: if (!b01) return bad("fused_pairs is 0 or 1"); n.fused_pairs = v != 0; break;
+        case HGM_OPT_FUSED_ACC32:
+            if (!(v == 0 || v == 1 || v == 2)) return bad("fused_acc32 is 0, 1 or 2");
+            n.fused_acc32 = (int)v;
+            break;
         default: return bad("unknown option");
     }
     return HGM_OK;
@@ -565,6 +569,7 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_FUSED_GROUP: *v = n.fused_group; break;
         case HGM_OPT_FUSED_DEPTH: *v = n.fused_depth; break;
         case HGM_OPT_FUSED_PAIRS: *v = n.fused_pairs; break;
+        case HGM_OPT_FUSED_ACC32: *v = n.fused_acc32; break;
         default: return HGM_E_ARG;
     }
     return HGM_OK;

@@ -334,10 +334,10 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(D <= 2 ? FB
 #endif
 // With zx_out, block 0 first adds the nzx regional shares of the side dot x_true'(B*q) (fixed
 // order) into *zx_out.
-template <int RG, typename T>
+template <int RG, typename T, typename TP = T>
 __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* __restrict__ rs_ptr,
                                                      const int32_t* __restrict__ rs_slot,
-                                                     const T* __restrict__ part, T* __restrict__ w,
+                                                     const TP* __restrict__ part, T* __restrict__ w,
                                                      const T* __restrict__ zx_part, int nzx, T* zx_out) {
     if (zx_out && blockIdx.x == 0) {
         __shared__ T sh[4];
@@ -346,12 +346,12 @@ __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* _
     }
     const int gl = threadIdx.x % RG;
     for (int64_t i = ((int64_t)blockIdx.x * BS + threadIdx.x) / RG; i < m; i += (int64_t)gridDim.x * (BS / RG)) {
-        T s = T(0);
+        TP s = TP(0);
         const int64_t k0 = rs_ptr[i], k1 = rs_ptr[i + 1];
         int64_t k = k0 + gl;
         for (; k + 3 * RG < k1; k += 4 * RG) {   // 4 slot reads, then 4 partial reads in flight
             int32_t sl[4];
-            T p[4];
+            TP p[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) sl[u] = rs_slot[k + u * RG];
 #pragma unroll
@@ -360,8 +360,8 @@ __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* _
             for (int u = 0; u < 4; ++u) s += p[u];
         }
         for (; k < k1; k += RG) s += part[rs_slot[k]];
-        if constexpr (RG > 1) s = group_sum<T, RG>(s);
-        if (gl == 0) w[i] = s;
+        if constexpr (RG > 1) s = group_sum<TP, RG>(s);
+        if (gl == 0) w[i] = (T)s;
     }
 }
 
@@ -475,20 +475,33 @@ __device__ __forceinline__ void lds_add(T* p, T t) {
 // Side sum (one value per region, in zx_part): side_sq == 0: sum_j zs_j * xt[j] (the m-space Gram
 // error monitor's x_true'(B*q)); side_sq == 1: sum_j zs_j^2 (alpha^2 of the Golub-Kahan step).
 // GK: the row epilogue / zout / side_sq code exists (false: the GMRES family's instruction stream).
-template <typename T, bool GK, int W, int MAXR, int G, int NCH, int D, bool PR, int DBG = 0>
+// AM: how the accumulators are updated (AccT: their type; the partials are AccT too):
+//   0  ds_add of T: fp64 ds_add_f64 (the fp64 production form); fp32 ds_add_f32 measured 11.3 ms
+//      at C5 -- the no-return fp32 LDS add runs at a fraction of ds_add_f64's rate on gfx950
+//      (9.5 ms of it; scripts/fused_micro.py, profiles/r4_micro_f32.jsonl) -- so fp32 does not use it;
+//   1  fp32 read-add-write (ds_read_b32, v_add_f32, ds_write_b32; a wave's rows in order): the fp32
+//      production form, 2.00 ms at C5 against 2.44 ms for the two fp32 SpMVs;
+//   2  fp64 accumulators for an fp32 pass: products formed in double and added by ds_add_f64,
+//      partials and their reduction in double, w rounded to float once: 2.16 ms (half the
+//      workgroups per CU: 72 KB of LDS).
+template <typename T, int AM> struct AccT { using t = T; };
+template <> struct AccT<float, 2> { using t = double; };
+template <typename T, bool GK, int AM, int W, int MAXR, int G, int NCH, int D, bool PR, int DBG = 0>
 __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__ reg_base, const int32_t* __restrict__ ray_tab,
                                                      const int32_t* __restrict__ wrun, const int2* __restrict__ runs,
                                                      const int64_t* __restrict__ rp, const T* __restrict__ val,
                                                      const uint16_t* __restrict__ lidx, const T* __restrict__ q,
-                                                     T* __restrict__ zraw, T* __restrict__ part,
+                                                     T* __restrict__ zraw, typename AccT<T, AM>::t* __restrict__ part,
                                                      const T* __restrict__ xt, T* __restrict__ zx_part,
                                                      const T* ev, const T* __restrict__ easq, T* zout, int side_sq) {
     static_assert(D >= 2 && D <= 4, "ring depth");
+    using TA = typename AccT<T, AM>::t;
     constexpr int EPL = PR ? 2 : 1;              // entries per lane per chunk
     constexpr int CH = 64 * EPL;                 // entries per chunk
     constexpr int ES = (int)sizeof(T);
+    constexpr int AS = (int)(sizeof(TA) / sizeof(T));   // accumulator offset = slot offset * AS
     __shared__ T qloc[MAXR];                     // (the last 64: the lanes' dummy slots)
-    __shared__ T acc[W][MAXR];
+    __shared__ TA acc[W][MAXR];
     const int g = blockIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int ln = threadIdx.x & 63;
@@ -497,7 +510,7 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     for (int k = threadIdx.x; k < nr; k += 64 * W) {
         qloc[k] = q[ray_tab[pb + k]];
 #pragma unroll
-        for (int w = 0; w < W; ++w) acc[w][k] = T(0);
+        for (int w = 0; w < W; ++w) acc[w][k] = TA(0);
     }
     if (threadIdx.x < 64) qloc[MAXR - 64 + threadIdx.x] = T(0);
     // the epilogue coefficient: the bits the host takes from the same sum of squares
@@ -505,7 +518,7 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     int ua = wrun[g * W + wv];
     const int ub = wrun[g * W + wv + 1];
     __syncthreads();
-    T* __restrict__ ac = acc[wv];
+    TA* __restrict__ ac = acc[wv];
     // the wave's runs (<= 64, the plan checks) in lanes: readlane in the loop, no loads there
     // (a conditional load makes the compiler wait for every load in flight after it, and scalar
     // loads' lgkmcnt waits would also wait on the LDS)
@@ -666,9 +679,17 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
             for (int c = 0; c < NCH; ++c)
 #pragma unroll
                 for (int e = 0; e < EPL; ++e) {
-                    const T t = b.v[j][c][e] * sj;
-                    if constexpr (DBG & 2) S += t;
-                    else lds_add(reinterpret_cast<T*>(reinterpret_cast<char*>(ac) + k[j][c][e]), t);
+                    TA* pa = reinterpret_cast<TA*>(reinterpret_cast<char*>(ac) + k[j][c][e] * AS);
+                    if constexpr (DBG & 2) {
+                        S += b.v[j][c][e] * sj;
+                    } else if constexpr (AM == 2) {
+                        lds_add(pa, (double)b.v[j][c][e] * (double)sj);
+                    } else if constexpr (AM == 1) {
+                        const T t = b.v[j][c][e] * sj;
+                        *pa = *pa + t;
+                    } else {
+                        lds_add(pa, b.v[j][c][e] * sj);
+                    }
                 }
         }
     };
@@ -708,7 +729,7 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     // array of their own would push the workgroup past half the LDS, one workgroup per CU)
     if (zx_part && ln == 0) qloc[wv] = zx;
     for (int k = threadIdx.x; k < nr; k += 64 * W) {
-        T t = acc[0][k];
+        TA t = acc[0][k];
 #pragma unroll
         for (int w = 1; w < W; ++w) t += acc[w][k];
         part[pb + k] = t;
@@ -1147,7 +1168,7 @@ static int64_t fused_key(const Numerics& nu) {
     const bool rw = nu.fused_kind == 1;
     if (!rw) return ((int64_t)nu.fused_region << 1);
     return 1 | ((int64_t)nu.fused_wregion << 1) | ((int64_t)nu.fused_waves << 10) | ((int64_t)nu.fused_group << 13) |
-           ((int64_t)nu.fused_depth << 17) | ((int64_t)nu.fused_pairs << 20);
+           ((int64_t)nu.fused_depth << 17) | ((int64_t)nu.fused_pairs << 20) | ((int64_t)nu.fused_acc32 << 21);
 }
 
 // The plan of B, built on first use (a failure to plan leaves the two-pass path in place).
@@ -1191,38 +1212,47 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
     const int64_t ml = P->maxlen + (PRm ? 1 : 0);
     const int NC = ml <= (PRm ? 128 : 64) ? 1 : ml <= (PRm ? 256 : 128) ? 2 : 4;
     const int dbg = c->num.fused_dbg;
+    const int am = sizeof(T) == 4 ? c->num.fused_acc32 : 0;   // accumulation mode (k_fused_rw AM)
     const bool side = fa.side_out != nullptr && (fa.xt != nullptr || fa.side_sq);
-#define HGM_RWL(WV, MRV, GV, NCV, DV, PV, DBV)                                                                       \
+#define HGM_RWL(AMV, WV, MRV, GV, NCV, DV, PV, DBV)                                                                  \
     {                                                                                                                 \
         if (!dry)                                                                                                     \
-            launch(c, false, k_fused_rw<T, GK, WV, MRV, GV, NCV, DV, PV, DBV>, dim3((unsigned)P->nreg),             \
+            launch(c, false, k_fused_rw<T, GK, AMV, WV, MRV, GV, NCV, DV, PV, DBV>, dim3((unsigned)P->nreg),        \
                    dim3(64 * WV), (const int64_t*)P->reg_base, (const int32_t*)P->ray_tab, (const int32_t*)P->wrun, \
                    (const int2*)P->runs, (const int64_t*)B->rp, (const T*)B->val, (const uint16_t*)P->lidx, fa.q,  \
-                   fa.zraw, (T*)P->part, side ? fa.xt : nullptr, side ? (T*)P->zx_part : nullptr, fa.ev, fa.easq,  \
-                   fa.zout, fa.side_sq ? 1 : 0);                                                                    \
+                   fa.zraw, (typename AccT<T, AMV>::t*)P->part, side ? fa.xt : nullptr,                            \
+                   side ? (T*)P->zx_part : nullptr, fa.ev, fa.easq, fa.zout, fa.side_sq ? 1 : 0);                  \
         return true;                                                                                                  \
     }
     if constexpr (GK) {
+        constexpr int AMP = sizeof(T) == 4 ? 1 : 0;    // the production accumulation of this T
+        const bool dshape = W == 4 && MR == 2048 && G == 8 && NC == 1 && PRm && D == 2;
         if (dbg) {   // timing experiments (hgm_spmv_ab only): the default shape
-            if (W == 4 && MR == 2048 && G == 8 && NC == 1 && PRm && D == 2) {
-#define HGM_RWD(DV) if (dbg == DV) HGM_RWL(4, 2048, 8, 1, 2, true, DV)
+            if (dshape && am == AMP) {
+#define HGM_RWD(DV) if (dbg == DV) HGM_RWL(AMP, 4, 2048, 8, 1, 2, true, DV)
                 HGM_RWD(1) HGM_RWD(2) HGM_RWD(4) HGM_RWD(7)
 #undef HGM_RWD
             }
             if (dry) return false;
             throw Error{HGM_E_ARG, "fused_dbg (Golub-Kahan / fp32 pass): waves 4, 2048 slots, 8 rows, pairs, depth 2, one chunk; 1, 2, 4 or 7"};
         }
+        if constexpr (sizeof(T) == 4) {   // the other fp32 accumulations: the default shape (measurements)
+            if (dshape && am == 0) HGM_RWL(0, 4, 2048, 8, 1, 2, true, 0)
+            if (dshape && am == 2) HGM_RWL(2, 4, 2048, 8, 1, 2, true, 0)
+        }
+        if (am == AMP) {
 #define HGM_RW(WV, MRV)                                                                                              \
     if (W == WV && MR == MRV && G == 8 && PRm && D == 2) {                                                           \
-        if (NC == 1) HGM_RWL(WV, MRV, 8, 1, 2, true, 0)                                                             \
-        if (NC == 2) HGM_RWL(WV, MRV, 8, 2, 2, true, 0)                                                             \
+        if (NC == 1) HGM_RWL(AMP, WV, MRV, 8, 1, 2, true, 0)                                                        \
+        if (NC == 2) HGM_RWL(AMP, WV, MRV, 8, 2, 2, true, 0)                                                        \
     }
-        HGM_RW_SHAPES_GK(HGM_RW)
+            HGM_RW_SHAPES_GK(HGM_RW)
 #undef HGM_RW
+        }
     } else {
         if (dbg) {   // timing experiments: the default shape only
             if (W == 4 && MR == 2048 && G == 8 && NC == 1 && PRm && D == 2) {
-#define HGM_RWD(DV) if (dbg == DV) HGM_RWL(4, 2048, 8, 1, 2, true, DV)
+#define HGM_RWD(DV) if (dbg == DV) HGM_RWL(0, 4, 2048, 8, 1, 2, true, DV)
                 HGM_RWD(1) HGM_RWD(2) HGM_RWD(3) HGM_RWD(4) HGM_RWD(5) HGM_RWD(6) HGM_RWD(7)
 #undef HGM_RWD
             }
@@ -1233,19 +1263,19 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
         // variants for the default shape only (measurements)
 #define HGM_RW(WV, MRV)                                                                                              \
     if (W == WV && MR == MRV && G == 8 && PRm && D == 2) {                                                           \
-        if (NC == 1) HGM_RWL(WV, MRV, 8, 1, 2, true, 0)                                                             \
-        if (NC == 2) HGM_RWL(WV, MRV, 8, 2, 2, true, 0)                                                             \
+        if (NC == 1) HGM_RWL(0, WV, MRV, 8, 1, 2, true, 0)                                                          \
+        if (NC == 2) HGM_RWL(0, WV, MRV, 8, 2, 2, true, 0)                                                          \
     }
         HGM_RW_SHAPES(HGM_RW)
 #undef HGM_RW
         if (W == 4 && MR == 2048 && NC == 1 && PRm) {
-            if (G == 8 && D == 3) HGM_RWL(4, 2048, 8, 1, 3, true, 0)
-            if (G == 4 && D == 2) HGM_RWL(4, 2048, 4, 1, 2, true, 0)
-            if (G == 4 && D == 3) HGM_RWL(4, 2048, 4, 1, 3, true, 0)
+            if (G == 8 && D == 3) HGM_RWL(0, 4, 2048, 8, 1, 3, true, 0)
+            if (G == 4 && D == 2) HGM_RWL(0, 4, 2048, 4, 1, 2, true, 0)
+            if (G == 4 && D == 3) HGM_RWL(0, 4, 2048, 4, 1, 3, true, 0)
         }
         if (W == 4 && MR == 2048 && NC == 2 && !PRm && D == 2) {
-            if (G == 8) HGM_RWL(4, 2048, 8, 2, 2, false, 0)
-            if (G == 4) HGM_RWL(4, 2048, 4, 2, 2, false, 0)
+            if (G == 8) HGM_RWL(0, 4, 2048, 8, 2, 2, false, 0)
+            if (G == 4) HGM_RWL(0, 4, 2048, 4, 2, 2, false, 0)
         }
     }
 #undef HGM_RWL
@@ -1306,9 +1336,14 @@ bool fused_pass(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArg
     }
     // one lane group per ray, no grid-stride cap (C4: 8,508 blocks; the 4,096 cap measured 5 us slower)
     const unsigned rgrid = (unsigned)std::max<int64_t>(1, (P->m * HGM_FUSED_RG + BS - 1) / BS);
-    launch(c, true, k_fused_reduce<HGM_FUSED_RG, T>, dim3(rgrid), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
-           (const int32_t*)P->rs_slot, (const T*)P->part, fa.w, (const T*)P->zx_part, (int)P->nreg,
-           side ? fa.side_out : nullptr);
+    if (sizeof(T) == 4 && P->kind == 1 && c->num.fused_acc32 == 2)   // fp64 partials of the fp32 pass
+        launch(c, true, k_fused_reduce<HGM_FUSED_RG, T, double>, dim3(rgrid), dim3(BS), P->m,
+               (const int64_t*)P->rs_ptr, (const int32_t*)P->rs_slot, (const double*)P->part, fa.w,
+               (const T*)P->zx_part, (int)P->nreg, side ? fa.side_out : nullptr);
+    else
+        launch(c, true, k_fused_reduce<HGM_FUSED_RG, T>, dim3(rgrid), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
+               (const int32_t*)P->rs_slot, (const T*)P->part, fa.w, (const T*)P->zx_part, (int)P->nreg,
+               side ? fa.side_out : nullptr);
     HGM_HIP(hipGetLastError());
     // algorithmic bytes of the fused pass: B's CSR once (values, 32-bit indices, row pointers),
     // q read, z and w written (SURVEY.md §8(d)'s SpMV count for one pass over the operator), and

@@ -87,6 +87,7 @@ struct Numerics {
     int fused_group = 8;            // ... row-wave pass: rows per load batch (4, 8)
     int fused_depth = 2;            // ... row-wave pass: batches in the load ring (2..4)
     bool fused_pairs = true;        // ... row-wave pass: two entries per lane
+    int fused_acc32 = 1;            // ... fp32 row-wave pass: 0 ds_add_f32, 1 read-add-write, 2 fp64 accumulators
     int krylov_pad = -1;            // Krylov basis column padding (elements; -1 auto, kernels.hip krylov_ld)
     int fused_dbg = 0;              // ... timing experiments: skip phases (wrong results)
 };

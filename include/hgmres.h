@@ -139,7 +139,10 @@ enum hgm_ctx_option {
     HGM_OPT_FUSED_WAVES = 26,      /* ... row-wave pass: waves per workgroup, 1, 2 or 4 [4] */
     HGM_OPT_FUSED_GROUP = 27,      /* ... row-wave pass: pixel rows per load batch, 4 or 8 [8] */
     HGM_OPT_FUSED_DEPTH = 28,      /* ... row-wave pass: batches in its load ring, 2..4 [2] */
-    HGM_OPT_FUSED_PAIRS = 29       /* ... row-wave pass: two entries per lane (16-byte value pairs) [1] */
+    HGM_OPT_FUSED_PAIRS = 29,      /* ... row-wave pass: two entries per lane (16-byte value pairs) [1] */
+    HGM_OPT_FUSED_ACC32 = 30       /* ... fp32 operators (lsqr_solver / lsmr_solver of BASELINE configs[4]): how
+                                      the pass accumulates a region's rays: 0 ds_add_f32, 1 fp32
+                                      read-add-write, 2 fp64 accumulators and partials (ds_add_f64) [1] */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for

@@ -19,6 +19,16 @@
  *   hgmres_mex('gmres_bounds', side,hybrid, A,B,b,x_true,tol,maxit,lambda, DeltaM[, DeltaR[, ritz_steps]])
  *        -> [x,err,res,niters,phi_final,dphi_final,phi_iter,dphi_iter]   {AB,BA}gmres_{hybrid,nonhybrid}_bounds.m:1-2
  *   hgmres_mex('device', d)                      select the HIP device (default 0)
+ *   hgmres_mex('parity', 'auto'|'on'|'off')      summation orders (below; default 'auto')
+ *
+ * Summation orders.  MATLAB's own orders (MKL-blocked dot products, its sparse mtimes) cannot be
+ * reproduced; libhgmres' fixed-order parity mode (HGM_OPT_PARITY) runs the
+ * reference's sequence of operations in one documented order, in which it is bit-identical to the
+ * oracle restatement.  'auto' (the default) selects it for every problem the reference itself runs
+ * -- operators of at most HGM_PARITY_AUTO_DIM rows and columns (the n = 32 shaw/heat/deriv2
+ * drivers, the 32 x 32 phantom of run_2D_phantom.m) -- so gcv_function.m / analyze_regularization.m
+ * see oracle-identical outputs there without opting in, and the production kernels (fused,
+ * reordered sums) above it.  'on' / 'off' force one or the other.
  *
  * Operands: MATLAB sparse (CSC, 64-bit mwIndex) is handed over as is (hgm_mat_create_csc); a
  * dense double matrix (the n = 32 drivers' shaw/deriv2 operators) is handed over as a CSC that
@@ -41,6 +51,9 @@
 
 static hgm_ctx* g_ctx = NULL;
 static int g_device = 0;
+
+#define HGM_PARITY_AUTO_DIM 4096
+static int g_parity = -1;   /* -1 auto, 0 off, 1 on */
 
 /* operators created during one call, destroyed before returning or raising */
 #define MAX_OPS 8
@@ -142,6 +155,15 @@ static hgm_mat* op(const mxArray* a, const char* what) {
     return M;
 }
 
+/* the summation orders for a solve on operator A (see the header: 'auto' = parity mode for
+ * reference-size operators) */
+static void parity_for(const hgm_mat* A) {
+    int64_t m = 0, n = 0;
+    hgm_mat_info(A, &m, &n, NULL, NULL);
+    const int on = g_parity >= 0 ? g_parity : (m <= HGM_PARITY_AUTO_DIM && n <= HGM_PARITY_AUTO_DIM);
+    check(hgm_ctx_set_option(ctx(), HGM_OPT_PARITY, on ? 1.0 : 0.0));
+}
+
 static hgm_mat* transpose_op(hgm_mat* A) {
     hgm_mat* T = NULL;
     check(hgm_mat_transpose(ctx(), A, &T));
@@ -181,6 +203,7 @@ static void nargs(int nrhs, int lo, int hi, const char* fn) {
 /* [x, error_norm, residual_norm, niters] of the GMRES-family solvers */
 static void gmres_rtp(int nlhs, mxArray* plhs[], const mxArray* prhs[], int ba) {
     hgm_mat* A = op(prhs[1], "A");
+    parity_for(A);
     hgm_mat* B = op(prhs[2], "B");
     int64_t m = 0, n = 0;
     hgm_mat_info(A, &m, &n, NULL, NULL);
@@ -207,6 +230,7 @@ static void gmres_rtp(int nlhs, mxArray* plhs[], const mxArray* prhs[], int ba) 
 /* lsqr_solver / hybrid_lsqr_solver / hybrid_lsmr_solver: [x, error_norm, residual_norm, niters] */
 static void gkb(int nlhs, mxArray* plhs[], const mxArray* prhs[], int which /* 0 lsqr, 1 hlsqr, 2 hlsmr */) {
     hgm_mat* A = op(prhs[1], "A");
+    parity_for(A);
     hgm_mat* At = transpose_op(A);
     int64_t m = 0, n = 0;
     hgm_mat_info(A, &m, &n, NULL, NULL);
@@ -239,6 +263,7 @@ static void gkb(int nlhs, mxArray* plhs[], const mxArray* prhs[], int which /* 0
  * lsmr_solver.m:3,5 (tol = 1e-6, maxit = min(m,n)) */
 static void lsmr(int nlhs, mxArray* plhs[], const mxArray* prhs[]) {
     hgm_mat* A = op(prhs[1], "A");
+    parity_for(A);
     hgm_mat* At = transpose_op(A);
     int64_t m = 0, n = 0;
     hgm_mat_info(A, &m, &n, NULL, NULL);
@@ -267,6 +292,7 @@ static void lsmr(int nlhs, mxArray* plhs[], const mxArray* prhs[]) {
 static void gcv(mxArray* plhs[], const mxArray* prhs[]) {
     const double lambda = scalar(prhs[1], "lambda");
     hgm_mat* A = op(prhs[2], "A");
+    parity_for(A);
     hgm_mat* B = op(prhs[3], "B");
     int64_t m = 0, n = 0;
     hgm_mat_info(A, &m, &n, NULL, NULL);
@@ -283,6 +309,7 @@ static void gcv(mxArray* plhs[], const mxArray* prhs[]) {
 /* [H, beta, kdone] = hgmres_mex('arnoldi', A, B, b, k, gcv_type) */
 static void arnoldi(int nlhs, mxArray* plhs[], const mxArray* prhs[]) {
     hgm_mat* A = op(prhs[1], "A");
+    parity_for(A);
     hgm_mat* B = op(prhs[2], "B");
     int64_t m = 0, n = 0;
     hgm_mat_info(A, &m, &n, NULL, NULL);
@@ -318,6 +345,7 @@ static void bounds(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     const int side = side_of(prhs[1]);
     const int hybrid = scalar(prhs[2], "hybrid") != 0.0;
     hgm_mat* A = op(prhs[3], "A");
+    parity_for(A);
     hgm_mat* B = op(prhs[4], "B");
     int64_t m = 0, n = 0;
     hgm_mat_info(A, &m, &n, NULL, NULL);
@@ -416,6 +444,15 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     } else if (!strcmp(fn, "gmres_bounds")) {
         nargs(nrhs, 9, 12, fn);
         bounds(nlhs, plhs, nrhs, prhs);
+    } else if (!strcmp(fn, "parity")) {
+        nargs(nrhs, 1, 1, fn);
+        char mode[8];
+        if (!mxIsChar(prhs[1]) || mxGetString(prhs[1], mode, sizeof mode) != 0)
+            fail("hgmres:arg", "hgmres: parity mode is 'auto', 'on' or 'off'");
+        if (!strcmp(mode, "auto")) g_parity = -1;
+        else if (!strcmp(mode, "on")) g_parity = 1;
+        else if (!strcmp(mode, "off")) g_parity = 0;
+        else fail("hgmres:arg", "hgmres: parity mode is 'auto', 'on' or 'off'");
     } else if (!strcmp(fn, "device")) {
         nargs(nrhs, 1, 1, fn);
         const double d = scalar(prhs[1], "device");

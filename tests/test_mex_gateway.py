@@ -126,6 +126,17 @@ def mex():
     return Mex()
 
 
+@pytest.fixture(autouse=True)
+def _production_orders(mex):
+    """The bit-identical dispatch tests compare the gateway with the Python binding's production
+    kernels, so they run with the gateway's summation orders 'off'.  The default, 'auto' (fixed-order
+    parity mode for reference-size operators, VERDICT r3 "Next" #8), has tests of its own below
+    (test_gateway_auto_parity, test_analyze_regularization_through_wrappers)."""
+    mex(0, "parity", "off")
+    yield
+    mex(0, "parity", "auto")
+
+
 def test_gateway_builds_and_exports_mexfunction(mex):
     assert hasattr(mex.L, "mexFunction")
 
@@ -425,3 +436,92 @@ def test_wrapper_logic_cpu():
     assert calls[-1][-2:] == ("L", "R")
     g(8, A.T, A, np.ones(7), np.ones(5), 0.0, 3.0, 1e-2, "M")
     assert calls[-1][-2] == "M" and np.size(calls[-1][-1]) == 0
+
+
+# ------------------------------------------------------------------ the default summation orders
+@pytest.mark.gpu
+def test_gateway_auto_parity(mex, gpu_ctx, tomo):
+    """'auto', the gateway's default: operators of at most 4,096 rows and columns (every problem the
+    reference runs; here tomo24) take the fixed-order parity mode, bit-identical to the oracle's
+    fixed_order(); above it (a 72 x 72 phantom, n = 5,184) the production kernels, bit for bit the
+    Python binding's."""
+    A, B, b, xt = tomo
+    mex(0, "parity", "auto")
+    x, e, r, k = mex(4, "lsqr_solver", A, b, xt, 0.0, 6.0)
+    with R.fixed_order():
+        xo, eo, ro, ko = R.lsqr_solver(A.tocsr(), b, xt, 0.0, 6)
+    for a, r_ in ((x, xo), (e, eo), (r, ro)):
+        np.testing.assert_array_equal(a, r_)
+    x, e, r, k = mex(4, "hybrid_ba_gmres_rtp", A, B, b, xt, 0.0, 10.0, 1e-2)
+    with R.fixed_order():
+        ref = R.hybrid_ba_gmres_rtp(A.tocsr(), B.tocsr(), b, xt, 0.0, 10, 1e-2)
+    for a, r_ in zip((x, e, r), ref[:3]):
+        np.testing.assert_array_equal(a, r_)
+    from hgmres.problems import tomo_problem
+    P = tomo_problem(72, 30, noise=1e-2, seed=0)
+    Ac = sp.csc_matrix(P.A)
+    out = mex(4, "lsqr_solver", Ac, P.b, P.x_true, 0.0, 6.0)
+    Ao, = _ops(gpu_ctx, Ac)
+    ref = hgmres.lsqr_solver(Ao, P.b, P.x_true, 0.0, 6, ctx=gpu_ctx, At=Ao.T)
+    for a, r_ in zip(out[:3], ref[:3]):
+        np.testing.assert_array_equal(a, r_)
+    with pytest.raises(MexError) as err:
+        mex(0, "parity", "sometimes")
+    assert err.value.ident == "hgmres:arg"
+
+
+@pytest.mark.gpu
+def test_analyze_regularization_through_wrappers(mex, gpu_ctx):
+    """analyze_regularization.m's numeric part (:19-49, :106-107, :122-123) driven through the .m
+    wrappers with the gateway's DEFAULT summation orders (no opt-in), against oracle/pipeline.py in
+    the oracle's fixed order: the 100-lambda sweep (200 solves) and the non-hybrid solutions bit for
+    bit; the GCV lambdas (fminbnd over the gcv_function wrapper, as :39-46) to fminbnd's TolX -- the
+    SVD inside each GCV value is LAPACK's on the oracle's side and one-sided Jacobi here -- and the
+    final hybrid solves bit for bit against the oracle at the same lambda.  (Round 3: through the
+    production kernels solution_nonhybrid_ab differed from the oracle by 3.18 normwise.)"""
+    import scipy.optimize as so
+    import warnings
+    from mwrap import Function
+    from oracle import pipeline
+    mex(0, "parity", "auto")                # the gateway's default (the autouse fixture sets 'off')
+    g = load_golden("shaw32_pipeline.npz")
+    A, E, b, xt = g["A"], g["E"], g["b"], g["x_true"]
+    Bp = A.T + E
+    W = {nm: Function(os.path.join(ROOT, "matlab", nm + ".m"), mex) for nm in
+         ("ABgmres_hybrid_bounds", "BAgmres_hybrid_bounds", "ABgmres_nonhybrid_bounds", "BAgmres_nonhybrid_bounds",
+          "gcv_function")}
+    lam_range = np.logspace(-10, 0, 100)                                          # :19
+    nb = np.linalg.norm(b)
+    As, Bs = sp.csr_matrix(A), sp.csr_matrix(Bp)      # (b - A*x on the host as the pipeline forms it)
+    o = {k: np.zeros(100) for k in ("res_norms_ab", "sol_norms_ab", "err_norms_ab", "res_norms_ba",
+                                     "sol_norms_ba", "err_norms_ba")}
+    for i, lam in enumerate(lam_range):                                           # :22-33
+        for side in ("ab", "ba"):
+            x, err = W[f"{side.upper()}gmres_hybrid_bounds"](2, A, Bp, b, xt, 1e-6, 32.0, lam)
+            o[f"res_norms_{side}"][i] = np.linalg.norm(b - As @ x) / nb
+            o[f"sol_norms_{side}"][i] = np.linalg.norm(x)
+            o[f"err_norms_{side}"][i] = err[-1]
+    m = A.shape[0]
+    for side in ("ab", "ba"):                                                    # :35-49
+        gcv = lambda l: float(np.ravel(W["gcv_function"](1, l, A, Bp, b, float(m), 20.0, side)[0])[0])   # noqa: E731
+        o[f"lambda_gcv_{side}"] = so.fminbound(gcv, 1e-9, 1e-1, xtol=1e-8)
+    o["x_optimal_ab"] = W["ABgmres_hybrid_bounds"](1, A, Bp, b, xt, 1e-6, 32.0, o["lambda_gcv_ab"])[0]   # :106
+    o["x_optimal_ba"] = W["BAgmres_hybrid_bounds"](1, A, Bp, b, xt, 1e-6, 32.0, o["lambda_gcv_ba"])[0]   # :107
+    o["solution_nonhybrid_ab"] = W["ABgmres_nonhybrid_bounds"](1, A, Bp, b, xt, 1e-6, 32.0)[0]           # :122
+    o["solution_nonhybrid_ba"] = W["BAgmres_nonhybrid_bounds"](1, A, Bp, b, xt, 1e-6, 32.0)[0]           # :123
+    with warnings.catch_warnings(), R.fixed_order():
+        warnings.simplefilter("ignore")
+        f = pipeline.analyze_regularization(As, b, xt, Bs, None, None, bounds_outputs=False, explicit_BA=False)
+        xab = R.ABgmres_hybrid_bounds(As, Bs, b, xt, 1e-6, 32, o["lambda_gcv_ab"])[0]
+        xba = R.BAgmres_hybrid_bounds(As, Bs, b, xt, 1e-6, 32, o["lambda_gcv_ba"])[0]
+    for key in ("err_norms_ab", "sol_norms_ab", "err_norms_ba", "sol_norms_ba", "res_norms_ab", "res_norms_ba"):
+        np.testing.assert_array_equal(o[key], f[key], err_msg=key)
+    for side in ("ab", "ba"):
+        assert abs(o[f"lambda_gcv_{side}"] - f[f"lambda_gcv_{side}"]) <= 3e-8, side   # TolX = 1e-8
+    np.testing.assert_array_equal(o["x_optimal_ab"], xab)
+    np.testing.assert_array_equal(o["x_optimal_ba"], xba)
+    np.testing.assert_array_equal(o["solution_nonhybrid_ab"], f["solution_nonhybrid_ab"])
+    np.testing.assert_array_equal(o["solution_nonhybrid_ba"], f["solution_nonhybrid_ba"])
+    print(f"[analyze_regularization via wrappers, default orders] lambda_gcv ab {o['lambda_gcv_ab']:.6e} "
+          f"(oracle {f['lambda_gcv_ab']:.6e}), ba {o['lambda_gcv_ba']:.6e} (oracle {f['lambda_gcv_ba']:.6e}); "
+          f"sweep and solves bit-identical")
