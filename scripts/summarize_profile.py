@@ -39,7 +39,7 @@ def groups(dispatches):
     i = 0
     while i < len(dispatches):
         _, nm, val = dispatches[i]
-        if "k_fused_ab" in nm:                      # one pass A*(B*q): main kernel + partial reduction
+        if "k_fused_ab" in nm or "k_fused_rw" in nm:   # one pass A*(B*q): main kernel + partial reduction
             vals = [val]
             if i + 1 < len(dispatches) and "k_fused_reduce" in dispatches[i + 1][1]:
                 vals.append(dispatches[i + 1][2])
@@ -70,7 +70,35 @@ def groups(dispatches):
     return out
 
 
+def traffic_of(dirs):
+    """{class: HBM bytes per launch} from FETCH_SIZE / WRITE_SIZE counter passes (dirs: key -> dir)."""
+    traffic = defaultdict(float)
+    for key, d in dirs.items():
+        f = find(os.path.join(d, "**", "*counter_collection.csv"))
+        if not f:
+            continue
+        per_dispatch = {}
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != key:
+                continue
+            did = int(r["Dispatch_Id"])
+            v = float(r["Counter_Value"]) * 1024.0 * (2.0 if key == "FETCH_SIZE" else 1.0)
+            nm, acc = per_dispatch.get(did, (r["Kernel_Name"], 0.0))
+            per_dispatch[did] = (nm, acc + v)
+        seqc = [(d_, nm, v) for d_, (nm, v) in sorted(per_dispatch.items())]
+        per = defaultdict(list)
+        for cls, vals in groups(seqc):
+            per[cls].append(sum(vals))
+        for cls, vals in per.items():
+            traffic[cls] += sum(vals) / len(vals)
+    return {c: round(v) for c, v in traffic.items()}
+
+
 def main():
+    if sys.argv[1] == "--traffic":      # scripts/gpu.sh traffic: <dir with FETCH_SIZE/ WRITE_SIZE/> <wl>
+        d = sys.argv[2]
+        print(json.dumps(traffic_of({k: os.path.join(d, k) for k in ("FETCH_SIZE", "WRITE_SIZE")}), indent=1))
+        return
     out, wl, tag = sys.argv[1], sys.argv[2], sys.argv[3]
     prof = os.environ.get("PROFILES_DIR", os.path.join(ROOT, "profiles"))
     os.makedirs(prof, exist_ok=True)
@@ -94,26 +122,7 @@ def main():
     per_class = {c: {"calls": len(v), "avg_us": sum(v) / len(v)} for c, v in cls_dur.items()}
     json.dump({"per_kernel": summ, "per_class": per_class},
               open(os.path.join(prof, f"{tag}_{wl}_kernel_trace_summary.json"), "w"), indent=1)
-    traffic = defaultdict(float)
-    for pas, key in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
-        f = find(os.path.join(out, pas, "**", "*counter_collection.csv"))
-        if not f:
-            continue
-        per_dispatch = {}
-        for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != key:
-                continue
-            did = int(r["Dispatch_Id"])
-            v = float(r["Counter_Value"]) * 1024.0 * (2.0 if key == "FETCH_SIZE" else 1.0)
-            nm, acc = per_dispatch.get(did, (r["Kernel_Name"], 0.0))
-            per_dispatch[did] = (nm, acc + v)
-        seqc = [(d, nm, v) for d, (nm, v) in sorted(per_dispatch.items())]
-        per = defaultdict(list)
-        for cls, vals in groups(seqc):
-            per[cls].append(sum(vals))
-        for cls, vals in per.items():
-            traffic[cls] += sum(vals) / len(vals)
-    res = {c: round(v) for c, v in traffic.items()}
+    res = traffic_of({"FETCH_SIZE": os.path.join(out, "fetch"), "WRITE_SIZE": os.path.join(out, "write")})
     json.dump(res, open(os.path.join(prof, f"traffic_{wl}.json"), "w"), indent=1)
     print(json.dumps({"traffic_bytes_per_launch": res,
                       "per_class_avg_us": {c: v["avg_us"] for c, v in per_class.items()}}, indent=1))

@@ -37,11 +37,13 @@ def test_one_rank_rccl_matches_single_context():
     finally:
         ctx0.close()
     tols = {"hba": TOL, "abp": TOL, "abn": TOL, "hab": TOL, "tabn": TOL, "thba": TOL,
-            "lsqr": 1e-7, "lsqr32": 1e-4}          # the Golub-Kahan envelope of the shard test
+            "lsqr": 1e-7, "lsqr32": 1e-4,          # the Golub-Kahan envelope of the shard test
+            "tlsqr32": 1e-4, "tlsmr32": 1e-4}      # (fp32 one-pass shards; the same code path at one rank)
     for tag, tol in tols.items():
         assert rel(r[f"{tag}_x"], s[f"{tag}_x"]) < tol, tag
         assert rel(r[f"{tag}_res"], s[f"{tag}_res"]) < tol, tag
         assert rel(r[f"{tag}_err"], s[f"{tag}_err"]) < tol, tag
+    assert rel(r["gcv_H"], s["gcv_H"]) < TOL and abs(r["gcv_lam"] - s["gcv_lam"]) <= 1e-8 * s["gcv_lam"]
     for tag in ("hba", "abn", "hab", "tabn", "thba"):
         assert r[f"{tag}_H"].shape == s[f"{tag}_H"].shape
         assert rel(r[f"{tag}_H"], s[f"{tag}_H"]) < TOL, tag
