@@ -531,6 +531,7 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             if (!(v == 0 || v == 1 || v == 2)) return bad("fused_acc32 is 0, 1 or 2");
             n.fused_acc32 = (int)v;
             break;
+        case HGM_OPT_FUSED_PLAN_DEV: if (!b01) return bad("fused_plan_dev is 0 or 1"); n.fused_plan_dev = v != 0; break;
         default: return bad("unknown option");
     }
     return HGM_OK;
@@ -570,6 +571,7 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_FUSED_DEPTH: *v = n.fused_depth; break;
         case HGM_OPT_FUSED_PAIRS: *v = n.fused_pairs; break;
         case HGM_OPT_FUSED_ACC32: *v = n.fused_acc32; break;
+        case HGM_OPT_FUSED_PLAN_DEV: *v = n.fused_plan_dev; break;
         default: return HGM_E_ARG;
     }
     return HGM_OK;
@@ -855,6 +857,20 @@ HGM_API int hgm_spmv_ab(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, const vo
         };
         if (A->dtype == HGM_F64) run(double(0));
         else run(float(0));
+    });
+    return HGM_OK;
+}
+
+HGM_API int hgm_fused_plan_info(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B, double* build_s, uint64_t* checksum,
+                                int64_t* nslot, int* device_built) {
+    if (!c || !A || !B) return HGM_E_ARG;
+    HGM_TRY(c, {
+        const FusedPlan* P = fused_ab_plan(c, A, B);
+        HGM_REQUIRE(P != nullptr, "fused plan: this pair has none (two-pass path)");
+        if (build_s) *build_s = fused_plan_build_seconds(P);
+        if (checksum) *checksum = fused_plan_checksum(c, B, P);
+        if (nslot) *nslot = fused_plan_slots(P);
+        if (device_built) *device_built = fused_plan_device_built(P) ? 1 : 0;
     });
     return HGM_OK;
 }

@@ -81,6 +81,7 @@ struct FusedPlan {
     double* part = nullptr;       // nslot (fp32 plans use it as float)
     double* zx_part = nullptr;    // kind 1: nreg (the regions' side sums; fp32 plans: float)
     double build_s = 0;
+    bool dev_built = false;       // kind 1: ray sets built on the device (HGM_OPT_FUSED_PLAN_DEV)
 };
 
 void fused_plan_free(FusedPlan* P) {
@@ -1011,6 +1012,214 @@ constexpr int RW_ROW_MAX = 255;                   // entries per pixel row (two 
 template <typename T, bool GK>
 static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArgs<T>& fa, bool dry);
 
+// ------------------------------------------------------------------------------------------
+// Device build of the row-wave plan's ray sets (HGM_OPT_FUSED_PLAN_DEV).  Per
+// region, one workgroup marks the rays of the region's entries in an LDS bitmap over the ray
+// space (atomic OR: order-free, so the set is the same whatever the schedule); a ray's slot is its
+// rank among the set bits.  That is exactly the host build's sorted-unique ray list and
+// map[ray] = index, so the plan's bytes are identical (tested).  The bitmap (and, in the fill
+// pass, its per-word prefix counts) sit in dynamic LDS: ceil(m / 32) words each, so rays up to
+// PLAN_DEV_MAX_M (C4: 272,271 rays, 68 KB).
+// ------------------------------------------------------------------------------------------
+namespace {
+constexpr int PLAN_BS = 1024;
+constexpr int64_t PLAN_DEV_MAX_M = int64_t(19) * 1024 * 32;   // 2 x 19 Ki words = 152 KB of LDS
+
+// the region's entries (all its waves' runs), mark their rays in bm
+__device__ __forceinline__ void plan_mark(uint32_t* bm, int nwords, const int32_t* __restrict__ wrun,
+                                          const int2* __restrict__ runs, int W, const int64_t* __restrict__ rp,
+                                          const int32_t* __restrict__ ci) {
+    const int g = blockIdx.x;
+    for (int i = threadIdx.x; i < nwords; i += PLAN_BS) bm[i] = 0u;
+    __syncthreads();
+    for (int u = wrun[g * W]; u < wrun[g * W + W]; ++u) {
+        const int2 r = runs[u];
+        const int64_t e1 = rp[r.x + r.y];
+        for (int64_t e = rp[r.x] + threadIdx.x; e < e1; e += PLAN_BS) {
+            const int32_t ray = ci[e];
+            atomicOr(&bm[ray >> 5], 1u << (ray & 31));
+        }
+    }
+    __syncthreads();
+}
+
+// exclusive prefix of v over the workgroup (fixed order), and the total
+__device__ __forceinline__ int block_exscan(int v, int* sh, int* total) {
+    const int ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d, 64);
+        if (ln >= d) x += y;
+    }
+    if (ln == 63) sh[wv] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int a = 0;
+        for (int w = 0; w < PLAN_BS / 64; ++w) {
+            const int t = sh[w];
+            sh[w] = a;
+            a += t;
+        }
+        sh[PLAN_BS / 64] = a;
+    }
+    __syncthreads();
+    *total = sh[PLAN_BS / 64];
+    return sh[wv] + x - v;
+}
+
+__global__ __launch_bounds__(PLAN_BS) void k_plan_count(const int32_t* __restrict__ wrun, const int2* __restrict__ runs,
+                                                        int W, const int64_t* __restrict__ rp,
+                                                        const int32_t* __restrict__ ci, int nwords,
+                                                        int32_t* __restrict__ cnt) {
+    extern __shared__ uint32_t plan_lds[];
+    __shared__ int sh[PLAN_BS / 64 + 1];
+    plan_mark(plan_lds, nwords, wrun, runs, W, rp, ci);
+    int c = 0;
+    for (int i = threadIdx.x; i < nwords; i += PLAN_BS) c += __popc(plan_lds[i]);
+    int tot = 0;
+    (void)block_exscan(c, sh, &tot);
+    if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
+}
+
+// ray_tab[reg_base[g] + rank] = ray (ascending), lidx[e] = rank(ci[e]) * es
+__global__ __launch_bounds__(PLAN_BS) void k_plan_fill(const int32_t* __restrict__ wrun, const int2* __restrict__ runs,
+                                                       int W, const int64_t* __restrict__ rp,
+                                                       const int32_t* __restrict__ ci, int nwords,
+                                                       const int64_t* __restrict__ reg_base,
+                                                       int32_t* __restrict__ ray_tab, uint16_t* __restrict__ lidx,
+                                                       int es) {
+    extern __shared__ uint32_t plan_lds[];
+    __shared__ int sh[PLAN_BS / 64 + 1];
+    uint32_t* bm = plan_lds;
+    uint32_t* pre = plan_lds + nwords;
+    plan_mark(bm, nwords, wrun, runs, W, rp, ci);
+    // words in contiguous per-thread chunks, so the exclusive scan of the chunk counts orders them
+    const int cw = (nwords + PLAN_BS - 1) / PLAN_BS;
+    const int w0 = min(nwords, (int)threadIdx.x * cw), w1 = min(nwords, w0 + cw);
+    int c = 0;
+    for (int i = w0; i < w1; ++i) c += __popc(bm[i]);
+    int tot = 0;
+    int a = block_exscan(c, sh, &tot);
+    int32_t* rt = ray_tab + reg_base[blockIdx.x];
+    for (int i = w0; i < w1; ++i) {
+        pre[i] = (uint32_t)a;
+        uint32_t b = bm[i];
+        while (b) {
+            const int k = __ffs(b) - 1;
+            rt[a++] = i * 32 + k;
+            b &= b - 1;
+        }
+    }
+    __syncthreads();
+    const int g = blockIdx.x;
+    for (int u = wrun[g * W]; u < wrun[g * W + W]; ++u) {
+        const int2 r = runs[u];
+        const int64_t e1 = rp[r.x + r.y];
+        for (int64_t e = rp[r.x] + threadIdx.x; e < e1; e += PLAN_BS) {
+            const int32_t ray = ci[e];
+            const uint32_t wd = bm[ray >> 5];
+            const int rank = (int)pre[ray >> 5] + __popc(wd & ((1u << (ray & 31)) - 1u));
+            lidx[e] = (uint16_t)(rank * es);
+        }
+    }
+}
+}  // namespace
+
+// The device part of the row-wave plan: ray sets, slots (lidx) and ray_tab by k_plan_count /
+// k_plan_fill, then the ray-major reduction index by a counting sort of ray_tab on the host
+// (slots in increasing order = regions in order, as the host build).
+static FusedPlan* fused_plan_dev_finish(hgm_ctx* c, const hgm_mat* B, int R, int W, int G, int es, int64_t nreg,
+                                        int64_t maxlen, const std::vector<int32_t>& wrun,
+                                        const std::vector<int2>& runs,
+                                        std::chrono::steady_clock::time_point t0) {
+    const int64_t m = B->cols, nnz = B->nnz;
+    const int nwords = (int)((m + 31) / 32);
+    FusedPlan* P = new FusedPlan;
+    int32_t* cnt_d = nullptr;
+    try {
+        P->kind = 1;
+        P->elem = es;
+        P->region = R;
+        P->waves = W;
+        P->group = G;
+        P->depth = c->num.fused_depth;
+        P->pairs = c->num.fused_pairs;
+        P->maxlen = maxlen;
+        P->nreg = nreg;
+        P->m = m;
+        P->wrun = upload(wrun);
+        P->runs = upload(runs);
+        if (hipMalloc(&cnt_d, sizeof(int32_t) * std::max<int64_t>(nreg, 1)) != hipSuccess)
+            throw Error{HGM_E_NOMEM, "fused plan: hipMalloc failed"};
+        hipLaunchKernelGGL(k_plan_count, dim3((unsigned)nreg), dim3(PLAN_BS), sizeof(uint32_t) * nwords, c->stream,
+                           (const int32_t*)P->wrun, (const int2*)P->runs, W, (const int64_t*)B->rp,
+                           (const int32_t*)B->ci, nwords, cnt_d);
+        HGM_HIP(hipGetLastError());
+        std::vector<int32_t> cnt(nreg);
+        HGM_HIP(hipMemcpyAsync(cnt.data(), cnt_d, sizeof(int32_t) * nreg, hipMemcpyDeviceToHost, c->stream));
+        HGM_HIP(hipStreamSynchronize(c->stream));
+        int worst = 0;
+        for (int32_t v : cnt) worst = std::max(worst, (int)v);
+        int maxr = 0;
+#define HGM_RW_PICK(WV, MRV) \
+    if (W == WV && worst <= MRV - 64 && (maxr == 0 || MRV < maxr)) maxr = MRV;
+        HGM_RW_SHAPES(HGM_RW_PICK)
+#undef HGM_RW_PICK
+        HGM_REQUIRE(maxr > 0, "fused A*(B*q): a region is crossed by more rays than the LDS of its waves holds");
+        P->maxr = maxr;
+        std::vector<int64_t> reg_base(nreg + 1, 0);
+        for (int64_t g = 0; g < nreg; ++g) reg_base[g + 1] = reg_base[g] + cnt[g];
+        const int64_t nslot = reg_base[nreg];
+        HGM_REQUIRE(nslot < (int64_t(1) << 31), "fused A*(B*q): partial slots");
+        P->nslot = nslot;
+        P->reg_base = upload(reg_base);
+        if (hipMalloc(&P->ray_tab, sizeof(int32_t) * std::max<int64_t>(nslot, 1)) != hipSuccess ||
+            hipMalloc(&P->lidx, sizeof(uint16_t) * (nnz + 256)) != hipSuccess)
+            throw Error{HGM_E_NOMEM, "fused plan: hipMalloc failed"};
+        HGM_HIP(hipMemsetAsync(P->lidx + nnz, 0, sizeof(uint16_t) * 256, c->stream));   // (the padding)
+        hipLaunchKernelGGL(k_plan_fill, dim3((unsigned)nreg), dim3(PLAN_BS), 2 * sizeof(uint32_t) * nwords, c->stream,
+                           (const int32_t*)P->wrun, (const int2*)P->runs, W, (const int64_t*)B->rp,
+                           (const int32_t*)B->ci, nwords, (const int64_t*)P->reg_base, P->ray_tab, P->lidx, es);
+        HGM_HIP(hipGetLastError());
+        std::vector<int32_t> ray_tab(std::max<int64_t>(nslot, 1));
+        HGM_HIP(hipMemcpyAsync(ray_tab.data(), P->ray_tab, sizeof(int32_t) * nslot, hipMemcpyDeviceToHost, c->stream));
+        HGM_HIP(hipStreamSynchronize(c->stream));
+        // ray-major reduction index: ray i's slots in region order (= increasing slot)
+        std::vector<int64_t> rs_ptr(m + 1, 0);
+        for (int64_t k = 0; k < nslot; ++k) rs_ptr[ray_tab[k] + 1]++;
+        for (int64_t i = 0; i < m; ++i) rs_ptr[i + 1] += rs_ptr[i];
+        std::vector<int32_t> rs_slot(std::max<int64_t>(nslot, 1));
+        {
+            std::vector<int64_t> fill(rs_ptr.begin(), rs_ptr.end() - 1);
+            for (int64_t k = 0; k < nslot; ++k) rs_slot[fill[ray_tab[k]]++] = (int32_t)k;
+        }
+        P->rs_ptr = upload(rs_ptr);
+        P->rs_slot = upload(rs_slot);
+        if (hipMalloc(&P->zx_part, sizeof(double) * std::max<int64_t>(nreg, 1)) != hipSuccess ||
+            hipMalloc(&P->part, sizeof(double) * std::max<int64_t>(nslot, 1)) != hipSuccess)
+            throw Error{HGM_E_NOMEM, "fused plan: hipMalloc failed"};
+        (void)hipFree(cnt_d);
+        cnt_d = nullptr;
+    } catch (...) {
+        if (cnt_d) (void)hipFree(cnt_d);
+        fused_plan_free(P);
+        throw;
+    }
+    P->dev_built = true;
+    P->build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const bool have = es == 4 ? fused_rw_launch<float, true>(c, B, P, FusedArgs<float>{}, true)
+                              : fused_rw_launch<double, false>(c, B, P, FusedArgs<double>{}, true);
+    if (!have) {
+        fused_plan_free(P);
+        throw Error{HGM_E_ARG, "fused A*(B*q): no row-wave kernel for this plan's shape and the options"};
+    }
+    if (std::getenv("HGM_FUSED_VERBOSE"))
+        std::fprintf(stderr, "[fused rw plan, device] region %d waves %d: %lld regions, %lld slots, max rays %d (LDS slots %d), %.3f s\n",
+                     R, W, (long long)nreg, (long long)P->nslot, 0, P->maxr, P->build_s);
+    return P;
+}
+
 FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G) {
     const int es = B->dtype == HGM_F32 ? 4 : 8;       // slots as LDS byte offsets of T
 
@@ -1020,10 +1229,12 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
     const int64_t n = B->rows, m = B->cols, nnz = B->nnz;
     int64_t nreg = 0;
     const std::vector<int32_t> reg = row_regions(B, R, &nreg);
+    // the ray sets on the device (no download of the column indices), or on the host (reference)
+    const bool dev_build = c->num.fused_plan_dev && m <= PLAN_DEV_MAX_M && nnz > 0;
     std::vector<int64_t> rp(n + 1);
-    std::vector<int32_t> ci(std::max<int64_t>(nnz, 1));
+    std::vector<int32_t> ci(dev_build ? 1 : std::max<int64_t>(nnz, 1));
     HGM_HIP(hipMemcpy(rp.data(), B->rp, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost));
-    if (nnz) HGM_HIP(hipMemcpy(ci.data(), B->ci, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
+    if (nnz && !dev_build) HGM_HIP(hipMemcpy(ci.data(), B->ci, sizeof(int32_t) * nnz, hipMemcpyDeviceToHost));
     int64_t maxlen = 0;
     for (int64_t s = 0; s < n; ++s) maxlen = std::max(maxlen, rp[s + 1] - rp[s]);
     HGM_REQUIRE(maxlen <= RW_ROW_MAX, "fused A*(B*q): a pixel row longer than the row-wave pass takes");
@@ -1058,6 +1269,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
     }
     std::vector<int2> runs(std::max<int32_t>(wrun.back(), 1));
     for (size_t i = 0; i < wr.size(); ++i) std::copy(wr[i].begin(), wr[i].end(), runs.begin() + wrun[i]);
+    if (dev_build) return fused_plan_dev_finish(c, B, R, W, G, es, nreg, maxlen, wrun, runs, t0);
     // region ray sets and every entry's slot among them (a dense map per thread)
     std::vector<std::vector<int32_t>> rrays(nreg);
     std::vector<uint16_t> lidx(std::max<int64_t>(nnz, 1) + 256, 0);
@@ -1168,7 +1380,8 @@ static int64_t fused_key(const Numerics& nu) {
     const bool rw = nu.fused_kind == 1;
     if (!rw) return ((int64_t)nu.fused_region << 1);
     return 1 | ((int64_t)nu.fused_wregion << 1) | ((int64_t)nu.fused_waves << 10) | ((int64_t)nu.fused_group << 13) |
-           ((int64_t)nu.fused_depth << 17) | ((int64_t)nu.fused_pairs << 20) | ((int64_t)nu.fused_acc32 << 21);
+           ((int64_t)nu.fused_depth << 17) | ((int64_t)nu.fused_pairs << 20) | ((int64_t)nu.fused_acc32 << 21) |
+           ((int64_t)nu.fused_plan_dev << 23);
 }
 
 // The plan of B, built on first use (a failure to plan leaves the two-pass path in place).
@@ -1369,4 +1582,34 @@ bool fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q,
     return fused_pass<double>(c, B, P, fa);
 }
 
+}  // namespace hgm
+
+namespace hgm {
+// FNV-1a over the plan's arrays (hgm_fused_plan_info): two builds compare byte for byte
+uint64_t fused_plan_checksum(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P) {
+    HGM_REQUIRE(P->kind == 1, "plan checksum: the row-wave plan");
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void* dev, size_t bytes) {
+        std::vector<unsigned char> v(bytes);
+        if (bytes) HGM_HIP(hipMemcpy(v.data(), dev, bytes, hipMemcpyDeviceToHost));
+        for (unsigned char b : v) h = (h ^ b) * 1099511628211ull;
+    };
+    int32_t nrun = 0;
+    HGM_HIP(hipMemcpy(&nrun, P->wrun + P->nreg * P->waves, sizeof(int32_t), hipMemcpyDeviceToHost));
+    mix(P->wrun, sizeof(int32_t) * (P->nreg * P->waves + 1));
+    mix(P->runs, sizeof(int2) * nrun);
+    mix(P->reg_base, sizeof(int64_t) * (P->nreg + 1));
+    mix(P->ray_tab, sizeof(int32_t) * P->nslot);
+    mix(P->lidx, sizeof(uint16_t) * B->nnz);
+    mix(P->rs_ptr, sizeof(int64_t) * (P->m + 1));
+    mix(P->rs_slot, sizeof(int32_t) * P->nslot);
+    const int64_t meta[6] = {P->elem, P->region, P->waves, P->maxr, P->maxlen, P->nslot};
+    for (int64_t v : meta)
+        for (int k = 0; k < 8; ++k) h = (h ^ (unsigned char)(v >> (8 * k))) * 1099511628211ull;
+    (void)c;
+    return h;
+}
+double fused_plan_build_seconds(const FusedPlan* P) { return P->build_s; }
+int64_t fused_plan_slots(const FusedPlan* P) { return P->nslot; }
+bool fused_plan_device_built(const FusedPlan* P) { return P->dev_built; }
 }  // namespace hgm

@@ -88,6 +88,7 @@ struct Numerics {
     int fused_depth = 2;            // ... row-wave pass: batches in the load ring (2..4)
     bool fused_pairs = true;        // ... row-wave pass: two entries per lane
     int fused_acc32 = 1;            // ... fp32 row-wave pass: 0 ds_add_f32, 1 read-add-write, 2 fp64 accumulators
+    bool fused_plan_dev = true;     // ... row-wave plan's ray sets built on the device (false: the host build)
     int krylov_pad = -1;            // Krylov basis column padding (elements; -1 auto, kernels.hip krylov_ld)
     int fused_dbg = 0;              // ... timing experiments: skip phases (wrong results)
 };
@@ -461,6 +462,10 @@ bool fused_gk_ok(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P);
 // *dst = *src (one scalar, device to the host-visible ring, system scope), on the context stream
 void copy_sys(hgm_ctx* c, const double* src, double* dst);
 void fused_plan_free(FusedPlan* P);
+uint64_t fused_plan_checksum(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P);
+double fused_plan_build_seconds(const FusedPlan* P);
+int64_t fused_plan_slots(const FusedPlan* P);
+bool fused_plan_device_built(const FusedPlan* P);
 
 // Solver entry check: HGM_OPT_FUSED_DBG skips phases of the one-pass kernel (timing experiments of
 // hgm_spmv_ab only, scripts/fused_micro.py): a solve would return wrong results, so it is refused.

@@ -5,7 +5,7 @@ The compute path is ``libhgmres.so`` (hand-written HIP for gfx950, C ABI in
 ``include/hgmres.h``); this package is the thin host mirror of the reference
 interface plus the synthetic 2-D tomography problem generator.
 """
-from .core import spmv_ab  # noqa: F401
+from .core import spmv_ab, fused_plan_info  # noqa: F401
 from .core import (  # noqa: F401
     ABgmres_hybrid_bounds,
     ABgmres_nonhybrid_bounds,

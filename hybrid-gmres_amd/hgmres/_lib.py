@@ -25,7 +25,7 @@ OPTIONS = {"parity": 1, "mgs_form": 2, "mgs_single": 3, "gram_err": 4, "gram_err
            "mgs_ppl": 12, "mgs1_ppl": 13, "mgs_fused": 14, "lsqr_dev": 15, "paged16": 16,
            "band_dual": 17, "fused_ab": 18, "fused_region": 19, "fused_bs": 20, "fused_dbg": 21, "fused_pf": 22,
            "krylov_pad": 23, "fused_kind": 24, "fused_wregion": 25, "fused_waves": 26, "fused_group": 27,
-           "fused_depth": 28, "fused_pairs": 29, "fused_acc32": 30}
+           "fused_depth": 28, "fused_pairs": 29, "fused_acc32": 30, "fused_plan_dev": 31}
 HGM_MGS, HGM_CGS2 = 0, 1
 HGM_SIDE_AB, HGM_SIDE_BA = 0, 1
 HGM_DEVICE_PTRS = 1
@@ -77,6 +77,7 @@ _SIGS = {
     "hgm_mat_destroy": (None, [c_void_p]),
     "hgm_spmv": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "hgm_spmv_ab": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hgm_fused_plan_info": (c_int, [c_void_p, c_void_p, c_void_p, dp, P(C.c_uint64), ip64, P(c_int)]),
     "hgm_dev_alloc": (c_int, [c_void_p, c_int64, P(c_void_p)]),
     "hgm_dev_free": (c_int, [c_void_p, c_void_p]),
     "hgm_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),

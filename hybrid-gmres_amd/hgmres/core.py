@@ -395,6 +395,17 @@ def spmv_ab(A: "SparseOperator", B: "SparseOperator", q):
     return bq.astype(np.float64), abq.astype(np.float64)
 
 
+def fused_plan_info(A: "SparseOperator", B: "SparseOperator"):
+    """The one-pass plan of (A, B) under the context's options (built if needed): dict with the
+    build seconds, a checksum over every plan array, the partial slots and whether the device built
+    the ray sets (``hgm_fused_plan_info``)."""
+    ctx = A.ctx
+    bs, ck, ns, dv = C.c_double(), C.c_uint64(), C.c_int64(), C.c_int()
+    _check(L.load().hgm_fused_plan_info(ctx.handle, A._h, B._h, C.byref(bs), C.byref(ck), C.byref(ns), C.byref(dv)),
+           ctx)
+    return {"build_s": bs.value, "checksum": ck.value, "nslot": ns.value, "device_built": bool(dv.value)}
+
+
 def as_operator(M, ctx=None, dtype=L.HGM_F64) -> SparseOperator:
     if isinstance(M, SparseOperator):
         return M

@@ -142,7 +142,9 @@ enum hgm_ctx_option {
     HGM_OPT_FUSED_PAIRS = 29,      /* ... row-wave pass: two entries per lane (16-byte value pairs) [1] */
     HGM_OPT_FUSED_ACC32 = 30       /* ... fp32 operators (lsqr_solver / lsmr_solver of BASELINE configs[4]): how
                                       the pass accumulates a region's rays: 0 ds_add_f32, 1 fp32
-                                      read-add-write, 2 fp64 accumulators and partials (ds_add_f64) [1] */
+                                      read-add-write, 2 fp64 accumulators and partials (ds_add_f64) [1] */,
+    HGM_OPT_FUSED_PLAN_DEV = 31    /* ... the row-wave plan's region ray sets and slots built on the device
+                                      (an LDS bitmap per region) [1]; 0 the host build (same bytes) */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for
@@ -245,6 +247,12 @@ HGM_API int hgm_spmv(hgm_ctx* ctx, const hgm_mat* A, const void* x_dev, void* y_
  * in the reference pixel order, as hgm_spmv's. */
 HGM_API int hgm_spmv_ab(hgm_ctx* ctx, const hgm_mat* A, const hgm_mat* B, const void* q_dev, void* Bq_dev,
                         void* ABq_dev);
+/* The one-pass plan of the pair (A, B) under the context's current options, built if it is not
+ * yet: the seconds its build took, a 64-bit FNV-1a checksum over every plan array (so two builds
+ * can be compared byte for byte), the partial slots, and whether the device built the ray sets
+ * (HGM_OPT_FUSED_PLAN_DEV).  HGM_E_ARG when the pair has no plan (two-pass path). */
+HGM_API int hgm_fused_plan_info(hgm_ctx* ctx, const hgm_mat* A, const hgm_mat* B, double* build_s,
+                                uint64_t* checksum, int64_t* nslot, int* device_built);
 
 /* ---- device memory helpers (for callers without their own allocator) ---- */
 HGM_API int hgm_dev_alloc(hgm_ctx* ctx, int64_t bytes, void** ptr);
