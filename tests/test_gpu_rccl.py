@@ -43,7 +43,8 @@ def test_one_rank_rccl_matches_single_context():
         assert rel(r[f"{tag}_x"], s[f"{tag}_x"]) < tol, tag
         assert rel(r[f"{tag}_res"], s[f"{tag}_res"]) < tol, tag
         assert rel(r[f"{tag}_err"], s[f"{tag}_err"]) < tol, tag
-    assert rel(r["gcv_H"], s["gcv_H"]) < TOL and abs(r["gcv_lam"] - s["gcv_lam"]) <= 1e-8 * s["gcv_lam"]
+    # (the GCV minimum is flat: lambda itself is ill-determined at 1e-4, the minimum value is not)
+    assert rel(r["gcv_H"], s["gcv_H"]) < TOL and abs(r["gcv_val"] - s["gcv_val"]) <= 1e-10 * s["gcv_val"]
     for tag in ("hba", "abn", "hab", "tabn", "thba"):
         assert r[f"{tag}_H"].shape == s[f"{tag}_H"].shape
         assert rel(r[f"{tag}_H"], s[f"{tag}_H"]) < TOL, tag
