@@ -532,6 +532,7 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             n.fused_acc32 = (int)v;
             break;
         case HGM_OPT_FUSED_PLAN_DEV: if (!b01) return bad("fused_plan_dev is 0 or 1"); n.fused_plan_dev = v != 0; break;
+        case HGM_OPT_FUSED_REDUCE: if (!b01) return bad("fused_reduce is 0 or 1"); n.fused_reduce = (int)v; break;
         default: return bad("unknown option");
     }
     return HGM_OK;
@@ -572,6 +573,7 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_FUSED_PAIRS: *v = n.fused_pairs; break;
         case HGM_OPT_FUSED_ACC32: *v = n.fused_acc32; break;
         case HGM_OPT_FUSED_PLAN_DEV: *v = n.fused_plan_dev; break;
+        case HGM_OPT_FUSED_REDUCE: *v = n.fused_reduce; break;
         default: return HGM_E_ARG;
     }
     return HGM_OK;

@@ -78,6 +78,12 @@ struct FusedPlan {
     uint32_t* lr_pk = nullptr;    // nlr: first position | entries << 12 | region ray index << 20
     int64_t* rs_ptr = nullptr;    // m+1
     int32_t* rs_slot = nullptr;   // nslot
+    // kind 1: the partials by ray band (k_fused_reduce_band): band b = rays [64 b, 64 b + 64); its
+    // runs (first slot, first ray - 64 b, rays) of consecutive rays in consecutive slots of one
+    // region, regions in increasing order
+    int64_t nband = 0, nrun = 0;
+    int32_t* band_ptr = nullptr;  // nband + 1
+    int4* band_run = nullptr;     // nrun
     double* part = nullptr;       // nslot (fp32 plans use it as float)
     double* zx_part = nullptr;    // kind 1: nreg (the regions' side sums; fp32 plans: float)
     double build_s = 0;
@@ -88,7 +94,8 @@ void fused_plan_free(FusedPlan* P) {
     if (!P) return;
     for (void* p : {(void*)P->reg_sub, (void*)P->reg_base, (void*)P->subs, (void*)P->perm, (void*)P->lr_ray,
                     (void*)P->lr_pk, (void*)P->rs_ptr, (void*)P->rs_slot, (void*)P->part, (void*)P->wrun,
-                    (void*)P->runs, (void*)P->ray_tab, (void*)P->lidx, (void*)P->zx_part})
+                    (void*)P->runs, (void*)P->ray_tab, (void*)P->lidx, (void*)P->zx_part, (void*)P->band_ptr,
+                    (void*)P->band_run})
         if (p) (void)hipFree(p);
     delete P;
 }
@@ -363,6 +370,73 @@ __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* _
         for (; k < k1; k += RG) s += part[rs_slot[k]];
         if constexpr (RG > 1) s = group_sum<TP, RG>(s);
         if (gl == 0) w[i] = (T)s;
+    }
+}
+
+// The same sums by ray band (the row-wave plan's default, HGM_OPT_FUSED_REDUCE = 1): one wave per
+// band of 64 consecutive rays, lane l owning ray 64 b + l.  The band's runs come in region order;
+// a lane adds each partial of its ray to accumulator (j mod 8), j = the partial's index in the
+// ray's region-ordered list -- the exact sums lane j mod 8 of k_fused_reduce<8> forms -- and the 8
+// accumulators of a ray then go through the same group_sum<8>: the bits of k_fused_reduce<8>.  The
+// partials are read in runs of consecutive slots (coalesced) instead of through the 4-B rs_slot
+// gather (C4: 126 MB less per pass).  RUNB runs' loads are issued before their adds.
+constexpr int RUNB = 16;
+template <typename T, typename TP = T>
+__global__ __launch_bounds__(BS) void k_fused_reduce_band(int64_t m, int64_t nband, const int32_t* __restrict__ band_ptr,
+                                                          const int4* __restrict__ band_run,
+                                                          const TP* __restrict__ part, T* __restrict__ w,
+                                                          const T* __restrict__ zx_part, int nzx, T* zx_out) {
+    __shared__ TP tr[BS / 64][64][9];             // per wave: the lanes' 8 sums (+1: bank spread)
+    if (zx_out && blockIdx.x == 0) {
+        __shared__ T sh[4];
+        const T t = reduce_parts<T, false>(zx_part, nzx, sh);
+        if (threadIdx.x == 0) st_sys(zx_out, t);
+    }
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const int64_t band = (int64_t)blockIdx.x * (BS / 64) + wv;
+    if (band >= nband) return;                    // (a whole wave: no barrier follows)
+    TP a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
+    int jc = 0;
+    const int r0 = band_ptr[band], r1 = band_ptr[band + 1];
+    for (int rc = r0; rc < r1; rc += 64) {
+        const int nr = min(64, r1 - rc);
+        const int4 d = ln < nr ? band_run[rc + ln] : make_int4(0, 0, 0, 0);
+        for (int rb = 0; rb < nr; rb += RUNB) {
+            TP p[RUNB];
+            bool in[RUNB];
+#pragma unroll
+            for (int u = 0; u < RUNB; ++u) {      // the loads of RUNB runs first (runs past nr: empty)
+                const int r = min(rb + u, 63);
+                const int slo = __builtin_amdgcn_readlane(d.x, r), rlo = __builtin_amdgcn_readlane(d.y, r);
+                const int cnt = rb + u < nr ? __builtin_amdgcn_readlane(d.z, r) : 0;
+                in[u] = (unsigned)(ln - rlo) < (unsigned)cnt;
+                p[u] = part[in[u] ? slo + (ln - rlo) : slo];
+            }
+#pragma unroll
+            for (int u = 0; u < RUNB; ++u) {      // then the adds, in run (= region) order
+                const int g = jc & 7;
+                a0 = (in[u] && g == 0) ? a0 + p[u] : a0;
+                a1 = (in[u] && g == 1) ? a1 + p[u] : a1;
+                a2 = (in[u] && g == 2) ? a2 + p[u] : a2;
+                a3 = (in[u] && g == 3) ? a3 + p[u] : a3;
+                a4 = (in[u] && g == 4) ? a4 + p[u] : a4;
+                a5 = (in[u] && g == 5) ? a5 + p[u] : a5;
+                a6 = (in[u] && g == 6) ? a6 + p[u] : a6;
+                a7 = (in[u] && g == 7) ? a7 + p[u] : a7;
+                jc += in[u] ? 1 : 0;
+            }
+        }
+    }
+    TP* t = tr[wv][ln];
+    t[0] = a0; t[1] = a1; t[2] = a2; t[3] = a3; t[4] = a4; t[5] = a5; t[6] = a6; t[7] = a7;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (one wave: its LDS accesses run in order)
+    const int64_t ray0 = band * 64;
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) {              // 8 rays at a time: lanes 8i..8i+7 = ray 8 s8 + i
+        const int rr = s8 * 8 + (ln >> 3);
+        TP v = tr[wv][rr][ln & 7];
+        v = group_sum<TP, 8>(v);
+        if ((ln & 7) == 0 && ray0 + rr < m) w[ray0 + rr] = (T)v;
     }
 }
 
@@ -1126,6 +1200,33 @@ __global__ __launch_bounds__(PLAN_BS) void k_plan_fill(const int32_t* __restrict
 }
 }  // namespace
 
+// The band runs of k_fused_reduce_band from the plan's region ray lists (regions in order).
+static void plan_bands(FusedPlan* P, const std::vector<int32_t>& ray_tab, const std::vector<int64_t>& reg_base) {
+    const int64_t m = P->m, nreg = P->nreg, nband = (m + 63) / 64;
+    std::vector<int32_t> cnt(nband + 1, 0);
+    auto runs_of = [&](auto emit) {
+        for (int64_t g = 0; g < nreg; ++g) {
+            for (int64_t k = reg_base[g], k1 = reg_base[g + 1]; k < k1;) {
+                const int32_t ray = ray_tab[k];
+                const int64_t b = ray / 64;
+                int64_t e = k + 1;
+                while (e < k1 && ray_tab[e] == ray + (int32_t)(e - k) && ray_tab[e] / 64 == b) ++e;
+                emit(b, make_int4((int)k, (int)(ray - b * 64), (int)(e - k), 0));
+                k = e;
+            }
+        }
+    };
+    runs_of([&](int64_t b, int4) { cnt[b + 1]++; });
+    for (int64_t b = 0; b < nband; ++b) cnt[b + 1] += cnt[b];
+    std::vector<int4> run(std::max<int32_t>(cnt[nband], 1));
+    std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
+    runs_of([&](int64_t b, int4 r) { run[fill[b]++] = r; });
+    P->nband = nband;
+    P->nrun = cnt[nband];
+    P->band_ptr = upload(cnt);
+    P->band_run = upload(run);
+}
+
 // The device part of the row-wave plan: ray sets, slots (lidx) and ray_tab by k_plan_count /
 // k_plan_fill, then the ray-major reduction index by a counting sort of ray_tab on the host
 // (slots in increasing order = regions in order, as the host build).
@@ -1196,6 +1297,7 @@ static FusedPlan* fused_plan_dev_finish(hgm_ctx* c, const hgm_mat* B, int R, int
         }
         P->rs_ptr = upload(rs_ptr);
         P->rs_slot = upload(rs_slot);
+        plan_bands(P, ray_tab, reg_base);
         if (hipMalloc(&P->zx_part, sizeof(double) * std::max<int64_t>(nreg, 1)) != hipSuccess ||
             hipMalloc(&P->part, sizeof(double) * std::max<int64_t>(nslot, 1)) != hipSuccess)
             throw Error{HGM_E_NOMEM, "fused plan: hipMalloc failed"};
@@ -1344,6 +1446,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
             throw Error{HGM_E_NOMEM, "fused plan: hipMalloc failed"};
         P->rs_ptr = upload(rs_ptr);
         P->rs_slot = upload(rs_slot);
+        plan_bands(P, ray_tab, reg_base);
         if (hipMalloc(&P->part, sizeof(double) * std::max<int64_t>(nslot, 1)) != hipSuccess)
             throw Error{HGM_E_NOMEM, "fused plan: hipMalloc failed"};
     } catch (...) {
@@ -1549,14 +1652,26 @@ bool fused_pass(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArg
     }
     // one lane group per ray, no grid-stride cap (C4: 8,508 blocks; the 4,096 cap measured 5 us slower)
     const unsigned rgrid = (unsigned)std::max<int64_t>(1, (P->m * HGM_FUSED_RG + BS - 1) / BS);
-    if (sizeof(T) == 4 && P->kind == 1 && c->num.fused_acc32 == 2)   // fp64 partials of the fp32 pass
+    const bool f64p = sizeof(T) == 4 && P->kind == 1 && c->num.fused_acc32 == 2;   // fp64 partials of the fp32 pass
+    if (P->kind == 1 && P->band_ptr && c->num.fused_reduce == 1) {
+        const unsigned bgrid = (unsigned)std::max<int64_t>(1, (P->nband + BS / 64 - 1) / (BS / 64));
+        if (f64p)
+            launch(c, true, k_fused_reduce_band<T, double>, dim3(bgrid), dim3(BS), P->m, P->nband,
+                   (const int32_t*)P->band_ptr, (const int4*)P->band_run, (const double*)P->part, fa.w,
+                   (const T*)P->zx_part, (int)P->nreg, side ? fa.side_out : nullptr);
+        else
+            launch(c, true, k_fused_reduce_band<T, T>, dim3(bgrid), dim3(BS), P->m, P->nband,
+                   (const int32_t*)P->band_ptr, (const int4*)P->band_run, (const T*)P->part, fa.w,
+                   (const T*)P->zx_part, (int)P->nreg, side ? fa.side_out : nullptr);
+    } else if (f64p) {
         launch(c, true, k_fused_reduce<HGM_FUSED_RG, T, double>, dim3(rgrid), dim3(BS), P->m,
                (const int64_t*)P->rs_ptr, (const int32_t*)P->rs_slot, (const double*)P->part, fa.w,
                (const T*)P->zx_part, (int)P->nreg, side ? fa.side_out : nullptr);
-    else
+    } else {
         launch(c, true, k_fused_reduce<HGM_FUSED_RG, T>, dim3(rgrid), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
                (const int32_t*)P->rs_slot, (const T*)P->part, fa.w, (const T*)P->zx_part, (int)P->nreg,
                side ? fa.side_out : nullptr);
+    }
     HGM_HIP(hipGetLastError());
     // algorithmic bytes of the fused pass: B's CSR once (values, 32-bit indices, row pointers),
     // q read, z and w written (SURVEY.md §8(d)'s SpMV count for one pass over the operator), and
@@ -1603,6 +1718,10 @@ uint64_t fused_plan_checksum(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P) {
     mix(P->lidx, sizeof(uint16_t) * B->nnz);
     mix(P->rs_ptr, sizeof(int64_t) * (P->m + 1));
     mix(P->rs_slot, sizeof(int32_t) * P->nslot);
+    if (P->band_ptr) {
+        mix(P->band_ptr, sizeof(int32_t) * (P->nband + 1));
+        mix(P->band_run, sizeof(int4) * P->nrun);
+    }
     const int64_t meta[6] = {P->elem, P->region, P->waves, P->maxr, P->maxlen, P->nslot};
     for (int64_t v : meta)
         for (int k = 0; k < 8; ++k) h = (h ^ (unsigned char)(v >> (8 * k))) * 1099511628211ull;

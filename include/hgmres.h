@@ -143,8 +143,11 @@ enum hgm_ctx_option {
     HGM_OPT_FUSED_ACC32 = 30       /* ... fp32 operators (lsqr_solver / lsmr_solver of BASELINE configs[4]): how
                                       the pass accumulates a region's rays: 0 ds_add_f32, 1 fp32
                                       read-add-write, 2 fp64 accumulators and partials (ds_add_f64) [1] */,
-    HGM_OPT_FUSED_PLAN_DEV = 31    /* ... the row-wave plan's region ray sets and slots built on the device
+    HGM_OPT_FUSED_PLAN_DEV = 31,   /* ... the row-wave plan's region ray sets and slots built on the device
                                       (an LDS bitmap per region) [1]; 0 the host build (same bytes) */
+    HGM_OPT_FUSED_REDUCE = 32      /* ... the row-wave pass's partial reduction: 1 by bands of 64 rays over
+                                      runs of consecutive slots, 0 per ray through its slot list [0] (the
+                                      same sums: bitwise equal) */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for

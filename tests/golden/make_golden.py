@@ -74,11 +74,14 @@ def dump_c3(name="c3_2048.npz", k=20):
     with MGS (the reference's orthogonalisation, hybrid_ba_gmres_rtp.m:20-23) and with CGS2 (the
     config's alternative), and the 20-step GCV Arnoldi (gcv_function.m:18-33) with the lambda that
     fminbnd picks on it over the bench's bounds [1e-8, 1] (TolX 1e-10, analyze_regularization.m:39-46).
+    The lambda search is the oracle's own: scipy's fminbound (the Forsythe-Malcolm-Moler search
+    MATLAB documents for fminbnd) over the restatement's gcv_from_H -- not the product's
+    hgm_gcv_fminbnd, which the full-size test checks against it.
     The operator is pinned by its CSR hash (the device generator reproduces it bitwise); x is stored
     as its norm plus every 997th entry.  SpMVs run on the host's OpenMP threads (oracle/parallel.py:
     bitwise scipy's csr_matvec)."""
+    import scipy.optimize as so
     from oracle import parallel as OP
-    from hgmres.core import gcv_fminbnd
     P = tomo_problem(2048, 19, noise=1e-2, seed=0, backprojector="matched")
     A, B, b, xt = P.A, P.B.tocsr(), P.b, P.x_true
     OP.build()
@@ -91,7 +94,9 @@ def dump_c3(name="c3_2048.npz", k=20):
         d.update({f"hba_{orth}_H": H, f"hba_{orth}_err": e, f"hba_{orth}_res": r, f"hba_{orth}_k": kk,
                   f"hba_{orth}_xnorm": np.linalg.norm(x), f"hba_{orth}_xs": x[::997].copy()})
         Hg, beta = R.arnoldi(PA, PB, b, k, "ba", orth=orth)
-        lam, g = gcv_fminbnd(Hg, beta, A.shape[1], gcv["lo"], gcv["hi"], gcv["tolx"])
+        lam, g, _, _ = so.fminbound(lambda l: R.gcv_from_H(Hg, beta, l, A.shape[1]), gcv["lo"], gcv["hi"],
+                                    xtol=gcv["tolx"], full_output=True)
+        lam, g = float(lam), float(g)
         d.update({f"gcv_{orth}_H": Hg, f"gcv_{orth}_beta": beta, f"gcv_{orth}_lam": lam, f"gcv_{orth}_val": g})
         # the solve at the GCV lambda: the c3gcv bench step (hybrid_ba_gmres_rtp at lambda_GCV)
         x, e, r, kk, H = R.hybrid_ba_gmres_rtp(PA, PB, b, xt, 0.0, k, lam, return_H=True, orth=orth)

@@ -318,3 +318,27 @@ def test_fused_plan_device_build_matches_host(gpu_ctx, N, na, dtype, world):
     assert info[1]["device_built"] and not info[0]["device_built"]
     assert info[0]["checksum"] == info[1]["checksum"] and info[0]["nslot"] == info[1]["nslot"]
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("N,na,dtype", [(256, 47, None), (512, 30, None), (256, 47, "f32"), (100, 17, None)])
+def test_fused_reduce_by_band_is_bitwise(gpu_ctx, N, na, dtype):
+    """The partial reduction by ray band (runs of consecutive slots, HGM_OPT_FUSED_REDUCE = 1, the
+    default) forms exactly the sums of the per-ray reduction through the slot list (= 0): products,
+    the AB-GMRES solve and the one-pass LSQR bit for bit."""
+    from hgmres import _lib as L
+    A = hgmres.SparseOperator.siddon(N, na, ctx=gpu_ctx, dtype=L.HGM_F32 if dtype else L.HGM_F64)
+    B = A.T
+    q = np.random.default_rng(5).standard_normal(A.shape[0])
+    xt = shepp_logan(N).ravel(order="F")
+    b = (A @ xt).astype(np.float64)
+    outs = {}
+    for red in (0, 1):
+        with gpu_ctx.options(fused_ab=1, fused_reduce=red):
+            hgmres.fused_plan_info(A, B)
+            o = list(hgmres.spmv_ab(A, B, q))
+            o += list(hgmres.lsqr_solver(A, b, xt, 0.0, 6, ctx=gpu_ctx, At=B)[:3])
+            if dtype is None:
+                o += list(hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True))
+            outs[red] = o
+    for a_, b_ in zip(outs[0], outs[1]):
+        assert np.array_equal(np.asarray(a_), np.asarray(b_))
