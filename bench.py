@@ -371,7 +371,7 @@ def main():
         dom_name = max(spmv, key=lambda k: spmv[k]["total_ms"])
         d = spmv[dom_name]
         traffic = None
-        tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
+        tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}{'_unmatched' if args.unmatched else ''}.json")
         # the committed PMC traffic is the single-GPU operator's: not a shard's
         if os.path.exists(tf) and not shard:
             try:

@@ -11,8 +11,9 @@
 #   tests [PYTEST_ARGS]      pytest -m gpu (e.g. tests/test_gpu_fused.py -k gkb) -> $TAG_gpu_tests_<n>.log
 #   bench WL [BENCH_ARGS]    one bench line of workload WL (c2 c3 c3gcv c4 c5 c5m) -> $TAG_bench_<wl>.json
 #   trace WL [BENCH_ARGS]    rocprofv3 --kernel-trace --stats of that bench -> $TAG_<wl>_kernel_stats.csv
-#   traffic WL               FETCH_SIZE / WRITE_SIZE passes (one counter per run) + the per-kernel
-#                            HBM-bytes summary (gfx950 x2 FETCH correction) -> traffic_<wl>.json
+#   traffic WL [BENCH_ARGS]  FETCH_SIZE / WRITE_SIZE passes (one counter per run) + the per-kernel
+#                            HBM-bytes summary (gfx950 x2 FETCH correction) -> traffic_<NAME or wl>.json
+#                            (NAME=c4_unmatched with --unmatched: bench.py reads that file then)
 #   pmc WL                   SQ / LDS counter groups of the fused pass, one run each
 #                            -> $TAG_pmc_<wl>/summary.json
 #   micro N ANGLES VARIANTS  hgm_spmv_ab micro-benchmark (scripts/fused_micro.py; F32=1 for fp32)
@@ -70,13 +71,14 @@ case "$recipe" in
     ;;
   traffic)
     wl=$1; shift
-    B="bench.py --workload $wl --steps 2 --warmup 1 --no-cpu-baseline --no-timing"
+    nm=${NAME:-$wl}
+    B="bench.py --workload $wl --steps 2 --warmup 1 --no-cpu-baseline --no-timing $*"
     for c in FETCH_SIZE WRITE_SIZE; do
-      timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$O/pmc_$wl/$c" -o p \
-          -- python3 $B > "$O/pmc_${wl}_$c.log" 2>&1 || { tail -5 "$O/pmc_${wl}_$c.log"; exit 1; }
+      timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$O/pmc_$nm/$c" -o p \
+          -- python3 $B > "$O/pmc_${nm}_$c.log" 2>&1 || { tail -5 "$O/pmc_${nm}_$c.log"; exit 1; }
     done
-    python3 scripts/summarize_profile.py --traffic "$O/pmc_$wl" "$wl" > "$O/traffic_$wl.json" || exit 1
-    cat "$O/traffic_$wl.json"
+    python3 scripts/summarize_profile.py --traffic "$O/pmc_$nm" "$nm" > "$O/traffic_$nm.json" || exit 1
+    cat "$O/traffic_$nm.json"
     ;;
   pmc)
     wl=$1; shift
