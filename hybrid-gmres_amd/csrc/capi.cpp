@@ -487,7 +487,7 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             n.mgs_ppl = (int)v;
             break;
         case HGM_OPT_MGS1_PPL:
-            if (!(v >= 1.0 && v <= 8.0) || v != (double)(int)v) return bad("mgs1 ppl is 1..8");
+            if (!(v == 0.0 || v == 1.0 || v == 2.0 || v == 4.0)) return bad("mgs1 ppl is 0, 1, 2 or 4");
             n.mgs1_ppl = (int)v;
             break;
         case HGM_OPT_MGS_FUSED: n.mgs_fused = v != 0.0; break;

@@ -72,7 +72,7 @@ struct Numerics {
     int pipe_depth = 2;
     bool sync_event_fence = false;
     int mgs_ppl = 1;
-    int mgs1_ppl = 2;
+    int mgs1_ppl = 0;               // one-reduction sweep: element pairs per lane of a tile (0: by length)
     bool mgs_fused = true;          // one-reduction MGS: solve folded into the update kernel
     bool lsqr_dev = true;           // LSQR: device-resident beta/alpha/rotation (no host round trip)
     bool paged16 = true;            // streaming SpMV: paged gathers also for 16-bit-index operators

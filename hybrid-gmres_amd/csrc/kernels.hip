@@ -688,8 +688,20 @@ static int mgs1_mode(const hgm_ctx* c) { return c->num.mgs_form; }
 bool mgs_gram_ok(const hgm_ctx* c, int64_t ldq, int maxit, bool dist) {
     return !dist && !c->num.parity && maxit <= MGS1_MAXC && mgs1_mode(c) == 1 && !krylov_padded(c, ldq);
 }
-// element pairs per lane of the dots pass (HGM_OPT_MGS1_PPL; fewer partials to sum)
-static int mgs1_ppl(const hgm_ctx* c) { return c->num.mgs1_ppl > 0 ? c->num.mgs1_ppl : 2; }
+// Element pairs per lane of the sweep's tiles (HGM_OPT_MGS1_PPL; 0: by length).  A workgroup sweeps
+// one tile of BS * P pairs at a time, and the grid has one workgroup per tile (up to MAX_PARTS, then
+// grid-stride).  4 pairs per lane from n = 2^20 on (>= 512 tiles); shorter vectors take 2 (C2,
+// n = 2^18: the sweep 19.2 us per step against 20.6 with 4 and 21.7 with 1, whose 512 partial rows
+// every update workgroup sums again; profiles/r4_c2_mgs_tile_ab.jsonl).
+static int mgs1_tile(const hgm_ctx* c, int64_t n) {
+    if (c->num.mgs1_ppl > 0) return c->num.mgs1_ppl;
+    const int64_t n2 = n >> 1;
+    return n2 >= (int64_t)BS * 4 * 512 ? 4 : n2 >= (int64_t)BS * 2 * 128 ? 2 : 1;
+}
+static int mgs1_blocks(int64_t n, int P) {
+    const int64_t tp = (int64_t)BS * P, nt = ((n >> 1) + tp - 1) / tp;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(nt, MAX_PARTS));
+}
 
 // Forward substitution (I + L) h = r in wave 0 (rows j = lane, lane + 64):
 // s_j = ((r_j - h_0 G_j0) - h_1 G_j1) - ...;  h_i = s_i once rows < i are applied.
@@ -737,12 +749,12 @@ __device__ __forceinline__ void mgs1_substitute(int kk, const T* sr, const T* sG
 // step (the column-group form read them once per 8 columns) and a block streams two columns at a
 // time.  Per column the tile's partial dot products are wave-summed (DPP, fixed order) and added
 // into the block's LDS accumulators in tile order: fixed order, bitwise reproducible.
-template <typename T>
+template <typename T, int P>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_mgs1_dots(
     int64_t n, const T* Q, int64_t ldq, int kk, const T* __restrict__ w, int npr, T* __restrict__ pr,
     T* __restrict__ pg, MdotStage<T> side, const T* hpend, const T* __restrict__ xe) {
     using T2 = typename V2<T>::t;
-    constexpr int P = 4, NW = BS / 64;
+    constexpr int NW = BS / 64;
     // acc[row][wave]: rows 0..kk = q_c'w, kk+1.. = q_c'q_k (c < kk; with xe also c = kk, then
     // q_k'x_true)
     __shared__ T acc[2 * MGS1_MAXC + 2][NW];
@@ -806,16 +818,19 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
             for (int p = 0; p < P; ++p) q[p] = buf_load2<T2>(rc, (ok[p] ? ix[p] : lim) * (int)sizeof(T2));
         };
+        // CU columns' loads in flight together (P * CU = 8 pairs a lane for short tiles)
+        constexpr int CU = P >= 4 ? 2 : 8 / P;
         int c = 0;
 #pragma unroll 1
-        for (; c + 2 <= kk + 1; c += 2) {
-            T2 qa[P], qb[P];
-            load(c, qa);
-            load(c + 1, qb);
-            col(qa, c);
-            col(qb, c + 1);
+        for (; c + CU <= kk + 1; c += CU) {
+            T2 qa[CU][P];
+#pragma unroll
+            for (int u = 0; u < CU; ++u) load(c + u, qa[u]);
+#pragma unroll
+            for (int u = 0; u < CU; ++u) col(qa[u], c + u);
         }
-        if (c <= kk) {
+#pragma unroll 1
+        for (; c <= kk; ++c) {
             T2 qa[P];
             load(c, qa);
             col(qa, c);
@@ -932,7 +947,7 @@ __global__ __launch_bounds__(MGS1_SBS) void k_mgs1_solve(int kk, const T* __rest
     if ((t >> 6) == 0) mgs1_substitute(kk, sr, sG, hdev);
 }
 
-template <typename T, bool FUSED>
+template <typename T, bool FUSED, int P>
 // hpend: Q(:,k) still holds v_k (pending normalisation): q_k = v_k / *hpend is used for the
 // last term and written back (each element by the one thread that updates it).
 // (4 waves per SIMD: the 1024-block cap is resident at once)
@@ -1003,7 +1018,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // at a time): a block streams a few columns at a time instead of touching all k+3 vectors
     // per element (C3 at k = 19: 4.6 TB/s that way, against 6 TB/s at k = 5).  Every element's
     // subtraction order is MGS's, j = 0..k.
-    constexpr int P = 4, CW = 4;
+    constexpr int CW = 16 / P;                         // (16 pairs a lane in flight)
     const int64_t tp = (int64_t)BS * P, ntile = (n2 + tp - 1) / tp;
     (void)stride;
     for (int64_t tl = blockIdx.x; tl < ntile; tl += nb) {
@@ -1173,15 +1188,22 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
             s2.stage = 2;
         }
         hipStream_t st = c->stream;
-        const int npr = gemv_blocks(n, mgs1_ppl(c));
+        const int P = mgs1_tile(c, n);
+        const int npr = mgs1_blocks(n, P);
         T* pr = c->buf<T>("mgs1_pr", (size_t)MGS1_MAXC * MAX_PARTS);
         T* pg = c->buf<T>("mgs1_pg", (size_t)(MGS1_MAXC + 2) * MAX_PARTS);
         T* gx = xe ? c->buf<T>("mgs1_gx", 2) : nullptr;
         T* Gt = c->buf<T>("mgs1_G", (size_t)MGS1_MAXC * MGS1_MAXC / 2 + MGS1_MAXC);
         T* hdev = c->buf<T>("mgs1_h", MGS1_MAXC + 2);
         const size_t lds = sizeof(T) * ((size_t)kk * (kk + 1) / 2 + 1);
-        k_mgs1_dots<T><<<npr + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1, pend_h, xe);
-        const int nb = gemv_blocks(n, mgs_ppl(c));
+#define HGM_MGS1_P(PV, STMT) \
+    if (P == PV) {          \
+        constexpr int PT = PV; \
+        STMT;               \
+    }
+#define HGM_MGS1_PS(STMT) HGM_MGS1_P(1, STMT) else HGM_MGS1_P(2, STMT) else HGM_MGS1_P(4, STMT) else HGM_REQUIRE(false, "mgs1: tile width")
+        HGM_MGS1_PS((k_mgs1_dots<T, PT><<<npr + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1, pend_h, xe)));
+        const int nb = npr;
         T* pout = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
         const bool fused = !dist && c->num.mgs_fused;
         Mgs1Fused<T> fz;
@@ -1191,9 +1213,8 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
             fz.npr = npr;
             fz.Gt = Gt;
             fz.ngx = xe ? 2 : 0;
-            k_mgs1_update<T, true><<<nb + s2.blocks(), BS, lds, st>>>(n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout,
-                                                                      s2, pend_h, nullptr, nullptr, xe ? qg : nullptr,
-                                                                      fz);
+            HGM_MGS1_PS((k_mgs1_update<T, true, PT><<<nb + s2.blocks(), BS, lds, st>>>(
+                n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout, s2, pend_h, nullptr, nullptr, xe ? qg : nullptr, fz)));
         } else if (dist) {
             T* redd = c->buf<T>("mgs1_red", 2 * MGS1_MAXC + 2);
             k_mgs1_solve<T, 1><<<1, MGS1_SBS, 0, st>>>(kk, pr, pg, npr, redd, Gt, hdev, nullptr);
@@ -1203,9 +1224,11 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
             k_mgs1_solve<T, 0><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, nullptr, Gt, hdev, gx);
         }
         if (!fused)
-            k_mgs1_update<T, false><<<nb + s2.blocks(), BS, 0, st>>>(n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout, s2,
-                                                                     pend_h, Gt + (size_t)kk * (kk - 1) / 2, gx,
-                                                                     xe ? qg : nullptr, fz);
+            HGM_MGS1_PS((k_mgs1_update<T, false, PT><<<nb + s2.blocks(), BS, 0, st>>>(
+                n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout, s2, pend_h, Gt + (size_t)kk * (kk - 1) / 2, gx,
+                xe ? qg : nullptr, fz)));
+#undef HGM_MGS1_PS
+#undef HGM_MGS1_P
         if (defer && !dist && kk + 2 <= MGS1_MAXC) {   // the next step must be one-reduction too
             // the next step's SpMVs divide by H(kk+1,kk) in their epilogues
             HGM_HIP(hipGetLastError());

@@ -109,7 +109,8 @@ enum hgm_ctx_option {
     HGM_OPT_PIPE_DEPTH = 10,       /* speculative Arnoldi steps in flight, 1..6 [2] */
     HGM_OPT_SYNC_EVENT_FENCE = 11, /* system-scope release on the pipeline events [0] */
     HGM_OPT_MGS_PPL = 12,          /* row pairs per lane of the MGS update / pass kernels [1] */
-    HGM_OPT_MGS1_PPL = 13,         /* row pairs per lane of the one-reduction dots kernel [2] */
+    HGM_OPT_MGS1_PPL = 13,         /* element pairs per lane of the one-reduction MGS sweep's tiles (one
+                                      workgroup per tile): 1, 2, 4, or 0 by vector length [0] */
     HGM_OPT_MGS_FUSED = 14,        /* one-reduction MGS (single rank): the partial-row reduction and the
                                       triangular solve run in the update kernel's prologue, redundantly per
                                       block (2 launches per sweep), instead of a one-block solve kernel [1] */

@@ -18,7 +18,7 @@
 #                            -> $TAG_pmc_<wl>/summary.json
 #   micro N ANGLES VARIANTS  hgm_spmv_ab micro-benchmark (scripts/fused_micro.py; F32=1 for fp32)
 #                            -> $TAG_micro_<f32|f64>.jsonl
-#   ab ROUNDS "ARGS_A" "ARGS_B"   alternating bench lines with two argument sets (same box)
+#   ab ROUNDS "ARGS_1" "ARGS_2" ...  alternating bench lines, one per argument set and round
 #                            -> $TAG_ab.jsonl
 #   libab OLD.so WL...       alternating library builds (HGM_LIB) on scripts/time_ops.py -> $TAG_lib_ab.jsonl
 set -o pipefail
@@ -99,16 +99,17 @@ case "$recipe" in
     grep variant "$O/${TAG}_micro_$f.jsonl"
     ;;
   ab)
-    rounds=$1; A=$2; B=$3
+    rounds=$1; shift
     : > "$O/${TAG}_ab.jsonl"
     for r in $(seq "$rounds"); do
-      for side in A B; do
-        args=$A; [ $side = B ] && args=$B
+      side=0
+      for args in "$@"; do
+        side=$((side + 1))
         timeout -k 10 600 python -u bench.py $args > "$O/ab.log" 2>&1 || { tail -20 "$O/ab.log"; exit 1; }
         python3 -c "
 import json, sys
 d = json.loads([l for l in open('$O/ab.log') if l.startswith('{')][-1])
-print(json.dumps({'round': $r, 'side': '$side', 'args': '''$args''', 'value': d['value'],
+print(json.dumps({'round': $r, 'side': $side, 'args': '''$args''', 'value': d['value'],
                   'kernels': {k: round(v['avg_us'], 2) for k, v in d['kernels'].items()}}))" | tee -a "$O/${TAG}_ab.jsonl"
       done
     done
