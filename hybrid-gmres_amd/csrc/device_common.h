@@ -22,6 +22,11 @@ typedef unsigned short nus4 __attribute__((ext_vector_type(4)));
 template <typename T> struct NV2;
 template <> struct NV2<double> { using t = nd2; };
 template <> struct NV2<float> { using t = nf2; };
+// 16-byte vectors of the elementwise kernels: W elements of T per access
+template <typename T> struct V16;
+template <> struct V16<double> { using t = nd2; static constexpr int W = 2; };
+template <> struct V16<float> { using t = nf4; static constexpr int W = 4; };
+static inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 template <bool NT, typename V>
 __device__ __forceinline__ V ld(const V* p) {

@@ -74,7 +74,7 @@ struct Numerics {
     int mgs_ppl = 1;
     int mgs1_ppl = 0;               // one-reduction sweep: element pairs per lane of a tile (0: by length)
     bool mgs_fused = true;          // one-reduction MGS: solve folded into the update kernel
-    bool lsqr_dev = true;           // LSQR: device-resident beta/alpha/rotation (no host round trip)
+    bool lsqr_dev = true;           // LSQR / LSMR: device-resident beta/alpha/rotations (no host round trip)
     bool paged16 = true;            // streaming SpMV: paged gathers also for 16-bit-index operators
     bool band_dual = true;          // banded tiled ray-major operators: steep rows in row strips
     bool fused_ab = true;           // m-space operator A*(B*q) in one pass over B (fused.hip)
@@ -377,9 +377,23 @@ void lsmr_update(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, const T* v, T c_hba
                  bool first);
 // LSMR kept-product monitor step (kernels.hip: k_lsmr_mon): image of v_k = c1*p1 + c0*p0 (or
 // p1 if p0 == nullptr), then the h / hbar / x image recurrences; *out = ||rhs - image(x)||^2
+// (cf != NULL: [c1, c0, f, e, cx] read on the device, from lsmr_rot)
 template <typename T>
 void lsmr_monitor(hgm_ctx* c, int64_t n, const T* p1, const T* p0, double c1, double c0, double* Ih, double* Ihb,
-                  double* Ix, const T* rhs, double f, double e, double cx, bool first, double* out);
+                  double* Ix, const T* rhs, double f, double e, double cx, bool first, double* out,
+                  const double* cf = nullptr);
+// Device-resident LSMR scalars (kernels.hip): the rotations :42-67 in one thread from *ssb = beta^2 and
+// *ssa = alpha^2 (st = [alpha, alphabar, rho, rhobar, cbar, sbar, zetabar, theta/rho, stop]); the
+// n-space step v /= alpha, hbar / x / h updates (skipped after the stop) with ||x - x_true||^2 fused
+// into err_out when xt != NULL; the stop test :76 on the m-space monitor; out = in / sqrt(*ss)
+// unless the sum is zero.
+template <typename T>
+void lsmr_rot(hgm_ctx* c, const T* ssb, const T* ssa, double* st, T* coef, double* cfm, double* cfn);
+template <typename T>
+void lsmr_step(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, T* v, const T* ssa, const T* coef, const double* st,
+               int k, const T* xt, T* err_out);
+void lsmr_stop(hgm_ctx* c, const double* rr, double nb, double tol, double* st, int k);
+template <typename T> void div_sqrt_nz(hgm_ctx* c, int64_t n, const T* in, T* out, const T* ss);
 // out[i] = epi(in[i], a, z[i]) (out may alias z): the epilogue of an SpMV applied to its raw product
 template <typename T> void epilogue_to(hgm_ctx* c, int64_t n, const T* in, T* out, int epi, T a, const T* z);
 template <typename T> void fill(hgm_ctx* c, int64_t n, T* x, T v);

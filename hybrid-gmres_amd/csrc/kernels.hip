@@ -104,17 +104,70 @@ void fixed_reduce(hgm_ctx* c, int op, int64_t n1, const T* a1, const T* b1, int6
 // ------------------------------------------------------------------------------
 // Reductions
 // ------------------------------------------------------------------------------
-template <typename T, int OP>   // 0: a.b   1: a.a   2: (a-b).(a-b)
+// Grid-stride order of the elementwise kernels with a fused partial sum (VEC: 16-byte vectors of W
+// elements -- thread g of the grid takes vectors g, g + G, ... and their elements in order, and the
+// last block's thread 0 then the n mod W tail; else single elements g, g + G, ...).  Every kernel
+// whose partials must give the same bits as another's (k_lsqr_step's error sum and
+// k_reduce_partial<T, 2>) walks its elements through this.
+template <typename T, bool VEC, typename F>
+__device__ __forceinline__ void grid_elems(int64_t n, F&& f) {
+    if constexpr (VEC) {
+        using V = typename V16<T>::t;
+        constexpr int W = V16<T>::W;
+        (void)sizeof(V);
+        const int64_t nv = n / W;
+#pragma unroll 2
+        for (int64_t g = (int64_t)blockIdx.x * BS + threadIdx.x; g < nv; g += (int64_t)gridDim.x * BS)
+            f(g * W, std::integral_constant<int, W>{});
+        if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+            for (int64_t i = nv * W; i < n; ++i) f(i, std::integral_constant<int, 1>{});
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS)
+            f(i, std::integral_constant<int, 1>{});
+    }
+}
+
+// W consecutive elements from p + i (one 16-byte access for W > 1; i a multiple of W)
+template <int W, typename T>
+__device__ __forceinline__ void vload(const T* p, int64_t i, T (&o)[W]) {
+    if constexpr (W == 1) {
+        o[0] = p[i];
+    } else {
+        const typename V16<T>::t v = *reinterpret_cast<const typename V16<T>::t*>(p + i);
+#pragma unroll
+        for (int e = 0; e < W; ++e) o[e] = v[e];
+    }
+}
+template <int W, typename T>
+__device__ __forceinline__ void vstore(T* p, int64_t i, const T (&o)[W]) {
+    if constexpr (W == 1) {
+        p[i] = o[0];
+    } else {
+        typename V16<T>::t v;
+#pragma unroll
+        for (int e = 0; e < W; ++e) v[e] = o[e];
+        *reinterpret_cast<typename V16<T>::t*>(p + i) = v;
+    }
+}
+
+template <typename T, int OP, bool VEC>   // 0: a.b   1: a.a   2: (a-b).(a-b)
 __global__ __launch_bounds__(BS) void k_reduce_partial(int64_t n, const T* __restrict__ a,
                                                        const T* __restrict__ b,
                                                        T* __restrict__ parts) {
     __shared__ T sh[4];
     T acc = 0;
-    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
-        if (OP == 0) acc += a[i] * b[i];
-        else if (OP == 1) acc += a[i] * a[i];
-        else { T d = a[i] - b[i]; acc += d * d; }
-    }
+    grid_elems<T, VEC>(n, [&](int64_t i, auto wc) {
+        constexpr int W = decltype(wc)::value;
+        T av[W], bv[W];
+        vload<W>(a, i, av);
+        if (OP != 1) vload<W>(b, i, bv);
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+            if (OP == 0) acc += av[e] * bv[e];
+            else if (OP == 1) acc += av[e] * av[e];
+            else { T d = av[e] - bv[e]; acc += d * d; }
+        }
+    });
     T tot = block_sum_all(acc, sh);
     if (threadIdx.x == 0) parts[blockIdx.x] = tot;
 }
@@ -174,7 +227,8 @@ static void reduce_to(hgm_ctx* c, int64_t n, const T* a, const T* b, T* out) {
     }
     const int np = parts_for(n);
     T* parts = c->buf<T>("red_parts", MAX_PARTS);
-    k_reduce_partial<T, OP><<<np, BS, 0, c->stream>>>(n, a, b, parts);
+    if (al16(a) && al16(b)) k_reduce_partial<T, OP, true><<<np, BS, 0, c->stream>>>(n, a, b, parts);
+    else k_reduce_partial<T, OP, false><<<np, BS, 0, c->stream>>>(n, a, b, parts);
     k_finalize<T><<<1, BS, 0, c->stream>>>(parts, np, out);
     HGM_HIP(hipGetLastError());
 }
@@ -1223,10 +1277,11 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
         } else {
             k_mgs1_solve<T, 0><<<1, MGS1_SBS, lds, st>>>(kk, pr, pg, npr, nullptr, Gt, hdev, gx);
         }
-        if (!fused)
+        if (!fused) {
             HGM_MGS1_PS((k_mgs1_update<T, false, PT><<<nb + s2.blocks(), BS, 0, st>>>(
                 n, nb, Q, ldq, kk, src, v, hdev, Hcol, pout, s2, pend_h, Gt + (size_t)kk * (kk - 1) / 2, gx,
                 xe ? qg : nullptr, fz)));
+        }
 #undef HGM_MGS1_PS
 #undef HGM_MGS1_P
         if (defer && !dist && kk + 2 <= MGS1_MAXC) {   // the next step must be one-reduction too
@@ -1394,7 +1449,8 @@ template <typename T> void normalize_to(hgm_ctx* c, int64_t n, T* v, T* nrm_out)
     }
     const int np = parts_for(n);
     T* parts = c->buf<T>("red_parts", MAX_PARTS);
-    k_reduce_partial<T, 1><<<np, BS, 0, c->stream>>>(n, v, v, parts);
+    if (al16(v)) k_reduce_partial<T, 1, true><<<np, BS, 0, c->stream>>>(n, v, v, parts);
+    else k_reduce_partial<T, 1, false><<<np, BS, 0, c->stream>>>(n, v, v, parts);
     k_vnorm<T><<<grid_for(n), BS, 0, c->stream>>>(n, v, parts, np, nrm_out);
     HGM_HIP(hipGetLastError());
 }
@@ -1446,7 +1502,7 @@ __global__ void k_lsqr_rot(const T* ssb, const T* ssa, double* st, T* coef, doub
 // v = v_hat / alpha (alpha = sqrt(*ssa)), then x += (phi/rho) w ; w = v - (theta/rho) w
 // (lsqr_solver.m:28,40-41), skipped once an earlier iteration met the stop test; with parts,
 // also the partials of ||x - x_true||^2 (:43) in k_reduce_partial<T, 2>'s order (same bits).
-template <typename T>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(BS) void k_lsqr_step(int64_t n, T* __restrict__ x, T* __restrict__ w, T* __restrict__ v,
                                                   const T* ssa, const T* coef, const double* st, int k,
                                                   const T* __restrict__ xt, T* __restrict__ parts) {
@@ -1455,23 +1511,33 @@ __global__ __launch_bounds__(BS) void k_lsqr_step(int64_t n, T* __restrict__ x, 
     const bool live = !(st[2] != 0.0 && st[2] < (double)(k + 1));
     const T a = coef[0], b = coef[1];
     T acc = 0;
-    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
-        const T vi = v[i] / alpha;
-        v[i] = vi;
-        T xi = x[i];
+    grid_elems<T, VEC>(n, [&](int64_t i, auto wc) {
+        constexpr int W = decltype(wc)::value;
+        T vv[W], xx[W], ww[W], tt[W];
+        vload<W>(v, i, vv);
+        vload<W>(x, i, xx);
+        if (live) vload<W>(w, i, ww);
+        if (parts) vload<W>(xt, i, tt);
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+            vv[e] = vv[e] / alpha;
+            if (live) {
+                const T p = a * ww[e];
+                xx[e] = xx[e] + p;
+                const T q = b * ww[e];
+                ww[e] = vv[e] - q;
+            }
+            if (parts) {
+                const T d = xx[e] - tt[e];
+                acc += d * d;
+            }
+        }
+        vstore<W>(v, i, vv);
         if (live) {
-            const T wi = w[i];
-            const T p = a * wi;
-            xi = xi + p;
-            x[i] = xi;
-            const T q = b * wi;
-            w[i] = vi - q;
+            vstore<W>(x, i, xx);
+            vstore<W>(w, i, ww);
         }
-        if (parts) {
-            const T d = xi - xt[i];
-            acc += d * d;
-        }
-    }
+    });
     if (parts) {
         const T tot = block_sum_all(acc, sh);
         if (threadIdx.x == 0) parts[blockIdx.x] = tot;
@@ -1499,7 +1565,11 @@ void lsqr_step(hgm_ctx* c, int64_t n, T* x, T* w, T* v, const T* ssa, const T* c
     const bool fuse = xt && n > SINGLE_MAX && !c->num.parity;
     const int np = fuse ? parts_for(n) : grid_for(n);
     T* parts = fuse ? c->buf<T>("red_parts", MAX_PARTS) : nullptr;
-    k_lsqr_step<T><<<np, BS, 0, c->stream>>>(n, x, w, v, ssa, coef, st, k, xt, parts);
+    // (vectors as k_reduce_partial takes them for the same x and x_true: the same error bits)
+    if (al16(x) && al16(w) && al16(v) && (!xt || al16(xt)))
+        k_lsqr_step<T, true><<<np, BS, 0, c->stream>>>(n, x, w, v, ssa, coef, st, k, xt, parts);
+    else
+        k_lsqr_step<T, false><<<np, BS, 0, c->stream>>>(n, x, w, v, ssa, coef, st, k, xt, parts);
     if (fuse) k_finalize<T><<<1, BS, 0, c->stream>>>(parts, np, err_out);
     HGM_HIP(hipGetLastError());
     if (xt && !fuse) sumsq_diff<T>(c, n, x, xt, err_out);
@@ -1516,22 +1586,28 @@ void div_sqrt(hgm_ctx* c, int64_t n, const T* in, T* out, const T* ss) {
 // leave v undivided), kept in av when given, then t = A*v_k - alpha*u (lsqr_solver.m:22,
 // lsmr_solver.m:34; two roundings, as the two-pass EPI_SUB epilogue), with the partials of ||t||^2
 // in k_reduce_partial<T, 1>'s layout (parts == nullptr: none).
-template <typename T>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(BS) void k_gkb_mstep(int64_t n, const T* __restrict__ w, const T* ssa,
                                                   const T* __restrict__ u, T* __restrict__ t, T* __restrict__ av,
                                                   T* __restrict__ parts) {
     __shared__ T sh[4];
     const T a = (T)sqrt((double)*ssa);
     T acc = 0;
-    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
-        const T wi = w[i];
-        const T avi = a != T(0) ? wi / a : wi;
-        if (av) av[i] = avi;
-        const T s = a * u[i];
-        const T ti = avi - s;
-        t[i] = ti;
-        acc += ti * ti;
-    }
+    grid_elems<T, VEC>(n, [&](int64_t i, auto wc) {
+        constexpr int W = decltype(wc)::value;
+        T ww[W], uu[W], tt[W];
+        vload<W>(w, i, ww);
+        vload<W>(u, i, uu);
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+            ww[e] = a != T(0) ? ww[e] / a : ww[e];
+            const T s = a * uu[e];
+            tt[e] = ww[e] - s;
+            acc += tt[e] * tt[e];
+        }
+        if (av) vstore<W>(av, i, ww);
+        vstore<W>(t, i, tt);
+    });
     if (parts) {
         const T tot = block_sum_all(acc, sh);
         if (threadIdx.x == 0) parts[blockIdx.x] = tot;
@@ -1543,7 +1619,10 @@ void gkb_mstep(hgm_ctx* c, int64_t n, const T* w, const T* ssa, const T* u, T* t
     const bool fuse = n > SINGLE_MAX && !c->num.parity;
     const int np = fuse ? parts_for(n) : grid_for(n);
     T* parts = fuse ? c->buf<T>("red_parts", MAX_PARTS) : nullptr;
-    k_gkb_mstep<T><<<np, BS, 0, c->stream>>>(n, w, ssa, u, t, av, parts);
+    if (al16(w) && al16(u) && al16(t) && (!av || al16(av)))
+        k_gkb_mstep<T, true><<<np, BS, 0, c->stream>>>(n, w, ssa, u, t, av, parts);
+    else
+        k_gkb_mstep<T, false><<<np, BS, 0, c->stream>>>(n, w, ssa, u, t, av, parts);
     if (fuse) k_finalize<T><<<1, BS, 0, c->stream>>>(parts, np, ss_out);
     HGM_HIP(hipGetLastError());
     if (!fuse) sumsq<T>(c, n, t, ss_out);
@@ -1576,6 +1655,150 @@ void lsmr_update(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, const T* v, T c_hba
     HGM_HIP(hipGetLastError());
 }
 
+// Device-resident LSMR scalars (lsmr_solver.m:42-67), the host loop's double arithmetic in one
+// thread.  st = [alpha, alphabar, rho, rhobar, cbar, sbar, zetabar, prev (theta/rho), stop];
+// *ssb = beta^2, *ssa = alpha^2 of this step.  coef = (T)[c_hbar, c_x, c_h] of :64/:66/:67 for the
+// n-space update; cfm / cfn = the monitors' coefficients [c1, c0, f, e, cx] (m-space: image of
+// v = A*v_k; n-space: beta A'u_{k+1} + alpha_k A'u_k).
+template <typename T>
+__global__ void k_lsmr_rot(const T* ssb, const T* ssa, double* st, T* coef, double* cfm, double* cfn) {
+    if (threadIdx.x != 0) return;
+    const double alpha_k = st[0];
+    const double beta = sqrt((double)*ssb), alpha = sqrt((double)*ssa);   // :35, :39
+    const double alphahat = st[1];                                        // :42
+    const double rhoold = st[2];                                          // :43
+    const double rho = hypot(alphahat, beta);                             // :44
+    const double cc = alphahat / rho, ss = beta / rho;                    // :45-46
+    const double thetanew = ss * alpha;                                   // :48
+    st[1] = cc * alpha;                                                   // :49 alphabar
+    const double rhobarold = st[3];                                       // :51
+    const double thetabar = st[5] * rho;                                  // :52
+    const double cr = st[4] * rho;
+    const double rhobar = hypot(cr, thetanew);                            // :53
+    st[4] = cr / rhobar;                                                  // :54 cbar
+    st[5] = thetanew / rhobar;                                            // :55 sbar
+    const double zeta = st[4] * st[6];                                    // :58
+    st[6] = -st[5] * st[6];                                               // :59 zetabar
+    const double c_hbar = (thetabar * rho) / (rhoold * rhobarold);        // :64
+    const double c_x = zeta / (rho * rhobar);                             // :66
+    const double c_h = thetanew / rho;                                    // :67
+    coef[0] = (T)c_hbar;
+    coef[1] = (T)c_x;
+    coef[2] = (T)c_h;
+    const double f = st[7];
+    const double m5[5] = {1.0, 0.0, f, c_hbar, c_x}, n5[5] = {beta, alpha_k, f, c_hbar, c_x};
+    for (int i = 0; i < 5; ++i) {
+        cfm[i] = m5[i];
+        cfn[i] = n5[i];
+    }
+    st[0] = alpha;
+    st[2] = rho;
+    st[3] = rhobar;
+    st[7] = c_h;
+}
+
+// The n-space LSMR step (lsmr_solver.m:40, :61-67) with device coefficients: v = v / alpha
+// (alpha = (T)sqrt(*ssa); a zero alpha leaves v, :40), hbar = h - c_hbar hbar (k = 0: h), x += c_x hbar,
+// h = v - c_h h -- x, h, hbar untouched once an earlier iteration met the stop test -- and, with
+// parts, the partials of ||x - x_true||^2 (:72) in k_lsqr_step's layout.
+template <typename T, bool FIRST, bool VEC>
+__global__ __launch_bounds__(BS) void k_lsmr_step(int64_t n, T* __restrict__ x, T* __restrict__ h,
+                                                  T* __restrict__ hbar, T* __restrict__ v, const T* ssa,
+                                                  const T* coef, const double* st, int k, const T* __restrict__ xt,
+                                                  T* __restrict__ parts) {
+    __shared__ T sh[4];
+    const T alpha = (T)sqrt((double)*ssa);
+    const bool live = !(st[8] != 0.0 && st[8] < (double)(k + 1));
+    const T c_hbar = coef[0], c_x = coef[1], c_h = coef[2];
+    T acc = 0;
+    grid_elems<T, VEC>(n, [&](int64_t i, auto wc) {
+        constexpr int W = decltype(wc)::value;
+        T vv[W], xx[W], hh[W], hb[W], tt[W];
+        vload<W>(v, i, vv);
+        vload<W>(x, i, xx);
+        if (live) {
+            vload<W>(h, i, hh);
+            if (!FIRST) vload<W>(hbar, i, hb);
+        }
+        if (parts) vload<W>(xt, i, tt);
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+            if (alpha > T(0)) vv[e] = vv[e] / alpha;                 // :40
+            if (live) {
+                if (FIRST) hb[e] = hh[e];                            // :62
+                else { const T p = c_hbar * hb[e]; hb[e] = hh[e] - p; }   // :64
+                const T q = c_x * hb[e];
+                xx[e] = xx[e] + q;                                   // :66
+                const T r = c_h * hh[e];
+                hh[e] = vv[e] - r;                                   // :67
+            }
+            if (parts) {
+                const T d = xx[e] - tt[e];
+                acc += d * d;
+            }
+        }
+        if (alpha > T(0)) vstore<W>(v, i, vv);
+        if (live) {
+            vstore<W>(hbar, i, hb);
+            vstore<W>(x, i, xx);
+            vstore<W>(h, i, hh);
+        }
+    });
+    if (parts) {
+        const T tot = block_sum_all(acc, sh);
+        if (threadIdx.x == 0) parts[blockIdx.x] = tot;
+    }
+}
+
+// :76 on the device: st[8] = k + 1 at the first iteration with sqrt(||r||^2) / (||b|| + eps) < tol
+__global__ void k_lsmr_stop(const double* rr, double nb, double tol, double* st, int k) {
+    if (threadIdx.x != 0) return;
+    const double res = sqrt(rr[0]) / (nb + 0x1p-52);   // eps
+    if (st[8] == 0.0 && res < tol) st[8] = (double)(k + 1);
+}
+
+// out = in / sqrt(*ss), or in when the sum is zero (lsmr_solver.m:36: if beta > 0, u = u / beta)
+template <typename T>
+__global__ __launch_bounds__(BS) void k_div_sqrt_nz(int64_t n, const T* __restrict__ in, T* __restrict__ out,
+                                                    const T* ss) {
+    const T s = (T)sqrt((double)*ss);
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS)
+        out[i] = s > T(0) ? in[i] / s : in[i];
+}
+
+template <typename T>
+void lsmr_rot(hgm_ctx* c, const T* ssb, const T* ssa, double* st, T* coef, double* cfm, double* cfn) {
+    k_lsmr_rot<T><<<1, 64, 0, c->stream>>>(ssb, ssa, st, coef, cfm, cfn);
+    HGM_HIP(hipGetLastError());
+}
+
+template <typename T>
+void lsmr_step(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, T* v, const T* ssa, const T* coef, const double* st,
+               int k, const T* xt, T* err_out) {
+    const bool fuse = xt && n > SINGLE_MAX;
+    const int np = fuse ? parts_for(n) : grid_for(n);
+    T* parts = fuse ? c->buf<T>("red_parts", MAX_PARTS) : nullptr;
+    const bool vec = al16(x) && al16(h) && al16(hbar) && al16(v) && (!xt || al16(xt));
+    if (k == 0 && vec) k_lsmr_step<T, true, true><<<np, BS, 0, c->stream>>>(n, x, h, hbar, v, ssa, coef, st, k, xt, parts);
+    else if (k == 0) k_lsmr_step<T, true, false><<<np, BS, 0, c->stream>>>(n, x, h, hbar, v, ssa, coef, st, k, xt, parts);
+    else if (vec) k_lsmr_step<T, false, true><<<np, BS, 0, c->stream>>>(n, x, h, hbar, v, ssa, coef, st, k, xt, parts);
+    else k_lsmr_step<T, false, false><<<np, BS, 0, c->stream>>>(n, x, h, hbar, v, ssa, coef, st, k, xt, parts);
+    if (fuse) k_finalize<T><<<1, BS, 0, c->stream>>>(parts, np, err_out);
+    HGM_HIP(hipGetLastError());
+    if (xt && !fuse) sumsq_diff<T>(c, n, x, xt, err_out);
+}
+
+void lsmr_stop(hgm_ctx* c, const double* rr, double nb, double tol, double* st, int k) {
+    k_lsmr_stop<<<1, 64, 0, c->stream>>>(rr, nb, tol, st, k);
+    HGM_HIP(hipGetLastError());
+}
+
+template <typename T>
+void div_sqrt_nz(hgm_ctx* c, int64_t n, const T* in, T* out, const T* ss) {
+    k_div_sqrt_nz<T><<<grid_for(n), BS, 0, c->stream>>>(n, in, out, ss);
+    HGM_HIP(hipGetLastError());
+}
+
 // LSMR monitors from kept products.  The images of the LSMR vectors under A
 // and A'A follow the same recurrences as the vectors (lsmr_solver.m:61-67), fed by the raw
 // products the bidiagonalisation already forms:
@@ -1585,13 +1808,21 @@ void lsmr_update(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, const T* v, T c_hba
 // r = b - A*x (:69) and A'r = A'b - A'A*x (:71) are then norms of kept vectors.  The images are
 // accumulated in fp64 for both value types.  parts[blk] = this block's sum of the squared
 // monitor vector.
+// cf != NULL: the coefficients [c1, c0, f, e, cx] from the device (k_lsmr_rot) instead of the arguments.
 template <typename T, bool FIRST>
 __global__ __launch_bounds__(BS) void k_lsmr_mon(int64_t n, const T* __restrict__ p1, const T* __restrict__ p0,
                                                  double c1, double c0, double* __restrict__ Ih,
                                                  double* __restrict__ Ihb, double* __restrict__ Ix,
                                                  const T* __restrict__ rhs, double f, double e, double cx,
-                                                 double* __restrict__ parts) {
+                                                 double* __restrict__ parts, const double* __restrict__ cf) {
     __shared__ double sh[4];
+    if (cf) {
+        c1 = cf[0];
+        c0 = cf[1];
+        f = cf[2];
+        e = cf[3];
+        cx = cf[4];
+    }
     double acc = 0;
     for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) {
         double iv;                                          // image of v_k
@@ -1619,13 +1850,13 @@ __global__ __launch_bounds__(BS) void k_lsmr_mon(int64_t n, const T* __restrict_
 
 template <typename T>
 void lsmr_monitor(hgm_ctx* c, int64_t n, const T* p1, const T* p0, double c1, double c0, double* Ih, double* Ihb,
-                  double* Ix, const T* rhs, double f, double e, double cx, bool first, double* out) {
+                  double* Ix, const T* rhs, double f, double e, double cx, bool first, double* out, const double* cf) {
     const int np = parts_for(n);
     double* parts = c->buf<double>("lsmr_mon_parts", MAX_PARTS);
     if (first)
-        k_lsmr_mon<T, true><<<np, BS, 0, c->stream>>>(n, p1, p0, c1, c0, Ih, Ihb, Ix, rhs, f, e, cx, parts);
+        k_lsmr_mon<T, true><<<np, BS, 0, c->stream>>>(n, p1, p0, c1, c0, Ih, Ihb, Ix, rhs, f, e, cx, parts, cf);
     else
-        k_lsmr_mon<T, false><<<np, BS, 0, c->stream>>>(n, p1, p0, c1, c0, Ih, Ihb, Ix, rhs, f, e, cx, parts);
+        k_lsmr_mon<T, false><<<np, BS, 0, c->stream>>>(n, p1, p0, c1, c0, Ih, Ihb, Ix, rhs, f, e, cx, parts, cf);
     k_finalize<double><<<1, BS, 0, c->stream>>>(parts, np, out);
     HGM_HIP(hipGetLastError());
 }
@@ -1696,7 +1927,11 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
     template void div_sqrt<T>(hgm_ctx*, int64_t, const T*, T*, const T*);                     \
     template void lsmr_update<T>(hgm_ctx*, int64_t, T*, T*, T*, const T*, T, T, T, bool);      \
     template void lsmr_monitor<T>(hgm_ctx*, int64_t, const T*, const T*, double, double, double*, double*, \
-                                  double*, const T*, double, double, double, bool, double*);   \
+                                  double*, const T*, double, double, double, bool, double*, const double*); \
+    template void lsmr_rot<T>(hgm_ctx*, const T*, const T*, double*, T*, double*, double*);   \
+    template void lsmr_step<T>(hgm_ctx*, int64_t, T*, T*, T*, T*, const T*, const T*, const double*, int, \
+                               const T*, T*);                                                  \
+    template void div_sqrt_nz<T>(hgm_ctx*, int64_t, const T*, T*, const T*);                  \
     template void fill<T>(hgm_ctx*, int64_t, T*, T);                                           \
     template void fill_hash<T>(hgm_ctx*, int64_t, T*, uint64_t);                               \
     template void convert<T>(hgm_ctx*, int64_t, const double*, T*);                            \

@@ -707,7 +707,8 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         }
         std::memcpy(c->hring + offY + (size_t)k * maxit, y.data(), sizeof(double) * kk);
         bool want_x = true;
-        if (gem) {
+        // (the last iteration's reconstruction forms x anyway: there the GEMV carries the error)
+        if (gem && k + 1 < maxit) {
             // ||Q y - x_true||^2 = x_true'x_true - 2 y'(Q'x_true) + y'(Q'Q) y (hybrid_*_rtp.m:33/:36
             // with x = Q y), used when it is at least gem_min ||x_true||^2 (the cancellation then
             // costs at most a factor 1/gem_min of the terms' rounding)
@@ -1121,7 +1122,8 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     double prev_ch = 0.0;                                                      // (theta/rho) of the previous :67
     // tol <= 0: `res < tol` (:76) can never hold, so the monitors stay on the device and are
     // read once after the loop instead of once per iteration
-    const bool defer_mon = kept && !(tol > 0);
+    // (and with the device-resident scalars below at any tol)
+    const bool defer_mon = kept && (!(tol > 0) || (fp && c->num.lsqr_dev));
     double* dmonh = defer_mon ? c->buf<double>("lsmr_monh", 2 * (size_t)maxit) : nullptr;
     T* errh = defer_mon ? c->buf<T>("lsmr_errh", maxit) : nullptr;
     auto monitors = [&](int kk, double m0, double m1, double e2) {
@@ -1131,7 +1133,59 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         if (xt) err[kk] = std::sqrt(e2) / nxt;                                 // :72-73
     };
     int k = 0;
-    for (k = 0; k < maxit; ++k) {
+    // Device-resident scalars (the one-pass path with kept monitors): beta and alpha
+    // stay on the device as sums of squares, the rotations :42-67 run in one thread (lsmr_rot, the
+    // loop's double arithmetic below), the n-space step divides v by alpha and carries the error sum,
+    // and the stop test :76 runs on the device after the monitors -- no host round trip per
+    // iteration.  The host reads the stop flag once per batch of 8 iterations (none with tol <= 0);
+    // an iteration enqueued past the stop leaves x untouched, and its histories are dropped.
+    const bool dev_scalars = fp && kept && c->num.lsqr_dev;
+    if (dev_scalars) {
+        double* st = c->buf<double>("lsmr_st", 9);
+        double* cfm = c->buf<double>("lsmr_cf", 10);
+        double* cfn = cfm + 5;
+        T* coef = c->buf<T>("lsmr_coef", 3);
+        const double st0[9] = {alpha, alphabar, rho, rhobar, cbar, sbar, zetabar, 0.0, 0.0};
+        h2d(c, st, st0, sizeof(st0));
+        FusedArgs<T> fa;
+        fa.q = u;
+        fa.ev = v;
+        fa.easq = sl + S_BETA;
+        fa.zout = v;
+        fa.w = wm;
+        fa.side_sq = true;
+        fa.side_out = wm + m;
+        const int batch = tol > 0 ? 8 : maxit;
+        int stop = 0;
+        for (k = 0; k < maxit && stop == 0;) {
+            const int kend = std::min(maxit, k + batch);
+            for (; k < kend; ++k) {
+                gkb_mstep<T>(c, m, wm, wm + m, u, r, Av, sl + S_BETA);           // :34-35 (+ kept A*v_k)
+                div_sqrt_nz<T>(c, m, r, u, sl + S_BETA);                          // :36
+                fa.zraw = Atu1;                                                   // A'*u_{k+1} (kept)
+                fused_pass<T>(c, At, fp, fa);                                     // :38-39 (+ A*v_hat)
+                if (dist_n(c)) allreduce(c, wm, m + 1);
+                lsmr_rot<T>(c, sl + S_BETA, wm + m, st, coef, cfm, cfn);          // :42-67 scalars
+                lsmr_step<T>(c, n, x, h, hbar, v, wm + m, coef, st, k, xt, xt ? errh + k : nullptr);   // :40, :61-67, :72
+                if (xt && dist_n(c)) allreduce(c, errh + k, 1);
+                double* dm = dmonh + 2 * (size_t)k;
+                lsmr_monitor<T>(c, m, Av, nullptr, 0, 0, Ihm, Ihbm, Ixm, b, 0, 0, 0, k == 0, dm, cfm);
+                lsmr_monitor<T>(c, n, Atu1, Atu0, 0, 0, Ihn, Ihbn, Ixn, Atb, 0, 0, 0, k == 0, dm + 1, cfn);
+                if (dist_n(c)) allreduce(c, dm + 1, 1);
+                std::swap(Atu0, Atu1);
+                if (tol > 0) lsmr_stop(c, dm, nb, tol, st, k);                   // :76
+            }
+            if (tol > 0) {
+                double sv = 0;
+                Reader rs(c);
+                rs.add(&sv, st + 8, sizeof(double));
+                rs.go();
+                stop = (int)sv;
+            }
+        }
+        k = stop > 0 ? stop - 1 : maxit;
+    }
+    for (k = dev_scalars ? k : 0; !dev_scalars && k < maxit; ++k) {
         const double alpha_k = alpha;
         if (fp) {
             // :34 A*v_k = (A*v_hat)/alpha_k (kept), u = A*v - alpha*u, ||u||^2

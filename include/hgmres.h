@@ -114,8 +114,8 @@ enum hgm_ctx_option {
     HGM_OPT_MGS_FUSED = 14,        /* one-reduction MGS (single rank): the partial-row reduction and the
                                       triangular solve run in the update kernel's prologue, redundantly per
                                       block (2 launches per sweep), instead of a one-block solve kernel [1] */
-    HGM_OPT_LSQR_DEV = 15,         /* lsqr_solver (single rank): beta, alpha, the Givens rotation and the stop
-                                      test stay on the device (same bits, no host round trip per iteration) [1] */
+    HGM_OPT_LSQR_DEV = 15,         /* lsqr_solver / lsmr_solver: beta, alpha, the rotations and the stop test
+                                      stay on the device (no host round trip per iteration) [1] */
     HGM_OPT_PAGED16 = 16,          /* streaming SpMV: LDS-paged x gathers also for operators with <= 65,536
                                       columns (instead of their 16-bit column indices) [1] */
     HGM_OPT_BAND_DUAL = 17,        /* banded ray-major operators over a whole tiled N x N grid: rows steeper

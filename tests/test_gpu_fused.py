@@ -240,6 +240,40 @@ def test_fused_gkb_fp32_matches_oracle(gpu_ctx, N, na):
         assert dev[key] <= 1e-4, key
 
 
+@pytest.mark.parametrize("dtype", [None, "f32"])
+def test_lsmr_device_scalars_match_host_loop(gpu_ctx, dtype):
+    """lsmr_solver's device-resident scalars (HGM_OPT_LSQR_DEV): the rotations
+    lsmr_solver.m:42-67 in one device thread and the stop test :76 on the device against the host
+    loop (lsqr_dev = 0) -- the same iterations, histories and x up to the last bits of hypot (device
+    against host libm); with tol between two residuals the solve stops at the same iteration
+    (inside the first batch of 8), and the iterations enqueued past the stop leave x as it was."""
+    A, At, b, xt = _gkb_pair(gpu_ctx, 256, 47, dtype=dtype)
+    bar = 1e-12 if dtype is None else 1e-5
+    with gpu_ctx.options(fused_ab=1):
+        hgmres.fused_plan_info(A, At)
+        full = {}
+        for dev_ in (1, 0):
+            with gpu_ctx.options(lsqr_dev=dev_):
+                full[dev_] = hgmres.lsmr_solver(A, b, xt, 0.0, 12, ctx=gpu_ctx, At=At)
+        d, h = full[1], full[0]
+        assert d[4] == h[4] == 12
+        for i in range(1, 4):
+            assert hist_dev(d[i], h[i]) <= bar, i
+        assert rel(d[0], h[0]) <= bar
+        res = np.asarray(h[2])
+        tol = 0.5 * (res[4] + res[5])                  # stops at iteration 6 (1-based): res[5] < tol
+        assert res[5] < tol <= res[4]
+        stopped = {}
+        for dev_ in (1, 0):
+            with gpu_ctx.options(lsqr_dev=dev_):
+                stopped[dev_] = hgmres.lsmr_solver(A, b, xt, tol, 12, ctx=gpu_ctx, At=At)
+        sd, sh = stopped[1], stopped[0]
+        assert sd[4] == sh[4] == 6
+        for i in range(1, 4):
+            assert len(sd[i]) == 6 and hist_dev(sd[i], sh[i]) <= bar, i
+        assert rel(sd[0], sh[0]) <= bar
+
+
 def test_fused_spmv_ab_fp32(gpu_ctx):
     """hgm_spmv_ab on an fp32 pair runs the fp32 one-pass kernel: within fp32 rounding of the
     two-pass product, bitwise repeatable."""
