@@ -357,15 +357,19 @@ __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* _
         TP s = TP(0);
         const int64_t k0 = rs_ptr[i], k1 = rs_ptr[i + 1];
         int64_t k = k0 + gl;
-        for (; k + 3 * RG < k1; k += 4 * RG) {   // 4 slot reads, then 4 partial reads in flight
-            int32_t sl[4];
-            TP p[4];
+#ifndef HGM_FUSED_RB
+#define HGM_FUSED_RB 4
+#endif
+        constexpr int RB = HGM_FUSED_RB;
+        for (; k + (RB - 1) * RG < k1; k += RB * RG) {   // RB slot reads, then RB partial reads in flight
+            int32_t sl[RB];
+            TP p[RB];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) sl[u] = rs_slot[k + u * RG];
+            for (int u = 0; u < RB; ++u) sl[u] = rs_slot[k + u * RG];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) p[u] = part[sl[u]];
+            for (int u = 0; u < RB; ++u) p[u] = part[sl[u]];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) s += p[u];
+            for (int u = 0; u < RB; ++u) s += p[u];
         }
         for (; k < k1; k += RG) s += part[rs_slot[k]];
         if constexpr (RG > 1) s = group_sum<TP, RG>(s);

@@ -96,6 +96,30 @@ def test_fused_ab_matches_two_pass_and_oracle(gpu_ctx, N, na, kind, region, wave
     assert rel(out[0], xo) <= TOL and hist_dev(out[1], eo) <= TOL and hist_dev(out[2], ro) <= TOL
 
 
+@pytest.mark.parametrize("N,na,dtype", [(2048, 19, None), (1024, 47, "f32")])
+def test_fused_pass_stress_repeat_bitwise(gpu_ctx, N, na, dtype):
+    """The row-wave pass adds into LDS accumulators without atomicity (ds_add_f64 into a wave-private
+    array, fp32 read-add-write); its determinism rests on the in-order execution of one wave's DS
+    instructions and distinct slots per instruction (fused.hip lds_add).  Stress it:
+    60 back-to-back passes over an operator with thousands of regions in flight must all return the
+    same bits as the first, for both outputs."""
+    from hgmres import _lib as L
+    dt = L.HGM_F32 if dtype else L.HGM_F64
+    A = hgmres.SparseOperator.siddon(N, na, ctx=gpu_ctx, dtype=dt)
+    B = A.T
+    q = np.random.default_rng(11).standard_normal(A.shape[0])
+    if dtype:
+        q = q.astype(np.float32)
+    with gpu_ctx.options(fused_ab=1):
+        hgmres.fused_plan_info(A, B)                     # the one pass is taken
+        bq0, ab0 = hgmres.spmv_ab(A, B, q)
+        for i in range(60):
+            bq, ab = hgmres.spmv_ab(A, B, q)
+            assert np.array_equal(ab, ab0) and np.array_equal(bq, bq0), i
+    A.close()
+    B.close()
+
+
 @pytest.mark.parametrize("kind", [0, 1])
 def test_fused_region_overflow_falls_back(gpu_ctx, kind):
     """A 128 x 128 region at 47 angles is crossed by ~7,700 rays (> the 3,968 LDS accumulators of
