@@ -377,7 +377,7 @@ __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* _
     }
 }
 
-// The same sums by ray band (the row-wave plan's default, HGM_OPT_FUSED_REDUCE = 1): one wave per
+// The same sums by ray band (HGM_OPT_FUSED_REDUCE = 1; measured 2-4 % slower, off by default): one wave per
 // band of 64 consecutive rays, lane l owning ray 64 b + l.  The band's runs come in region order;
 // a lane adds each partial of its ray to accumulator (j mod 8), j = the partial's index in the
 // ray's region-ordered list -- the exact sums lane j mod 8 of k_fused_reduce<8> forms -- and the 8
