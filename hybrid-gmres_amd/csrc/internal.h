@@ -382,6 +382,11 @@ template <typename T>
 void lsmr_monitor(hgm_ctx* c, int64_t n, const T* p1, const T* p0, double c1, double c0, double* Ih, double* Ihb,
                   double* Ix, const T* rhs, double f, double e, double cx, bool first, double* out,
                   const double* cf = nullptr);
+// The n-space monitor in carried-residual form with T images (the fp32 solves; kernels.hip
+// k_lsmr_mon_r): Ir starts as A'b; *out = ||Ir_k||^2; coefficients from lsmr_rot's cf.
+template <typename T>
+void lsmr_monitor_r(hgm_ctx* c, int64_t n, const T* p1, const T* p0, T* Ih, T* Ihb, T* Ir, bool first, double* out,
+                    const double* cf);
 // Device-resident LSMR scalars (kernels.hip): the rotations :42-67 in one thread from *ssb = beta^2 and
 // *ssa = alpha^2 (st = [alpha, alphabar, rho, rhobar, cbar, sbar, zetabar, theta/rho, stop]); the
 // n-space step v /= alpha, hbar / x / h updates (skipped after the stop) with ||x - x_true||^2 fused

@@ -1848,6 +1848,73 @@ __global__ __launch_bounds__(BS) void k_lsmr_mon(int64_t n, const T* __restrict_
     if (threadIdx.x == 0) parts[blockIdx.x] = tot;
 }
 
+// The n-space monitor of the fp32 solves in carried-residual form: the images of h and hbar and
+// the normal-equations residual Ir = A'b - A'A*x itself (Ir_0 = A'b) are stored in T and updated in
+// double, Ir_k = Ir_{k-1} - cx * image(hbar_k); parts = sum Ir_k^2 (the rounded values carried on).
+// Carrying Ir instead of image(x) keeps the small residual from a cancellation against A'b, so T
+// storage holds its relative accuracy; it moves 3 T arrays twice plus p1, p0 per iteration instead
+// of 3 double arrays twice plus p1, p0 and A'b (C5: 0.54 against 1.0 GB).
+template <typename T, bool FIRST, bool VEC>
+__global__ __launch_bounds__(BS) void k_lsmr_mon_r(int64_t n, const T* __restrict__ p1, const T* __restrict__ p0,
+                                                   T* __restrict__ Ih, T* __restrict__ Ihb, T* __restrict__ Ir,
+                                                   double* __restrict__ parts, const double* __restrict__ cf) {
+    __shared__ double sh[4];
+    const double c1 = cf[0], c0 = cf[1], f = cf[2], e = cf[3], cx = cf[4];
+    double acc = 0;
+    grid_elems<T, VEC>(n, [&](int64_t i, auto wc) {
+        constexpr int W = decltype(wc)::value;
+        T a[W], b[W], h[W], hb[W], r[W];
+        vload<W>(p1, i, a);
+        vload<W>(p0, i, b);
+        if (!FIRST) {
+            vload<W>(Ih, i, h);
+            vload<W>(Ihb, i, hb);
+        }
+        vload<W>(Ir, i, r);
+#pragma unroll
+        for (int u = 0; u < W; ++u) {
+            const double x1 = c1 * (double)a[u], x0 = c0 * (double)b[u];
+            const double iv = x1 + x0;
+            double ih, ihb;
+            if (FIRST) { ih = iv; ihb = ih; }
+            else {
+                const double q = f * (double)h[u];
+                ih = iv - q;
+                const double w = e * (double)hb[u];
+                ihb = ih - w;
+            }
+            const double s = cx * ihb;
+            const double ir = (double)r[u] - s;
+            h[u] = (T)ih;
+            hb[u] = (T)ihb;
+            r[u] = (T)ir;
+            const double rr = (double)r[u];
+            acc += rr * rr;
+        }
+        vstore<W>(Ih, i, h);
+        vstore<W>(Ihb, i, hb);
+        vstore<W>(Ir, i, r);
+    });
+    const double tot = block_sum_all(acc, sh);
+    if (threadIdx.x == 0) parts[blockIdx.x] = tot;
+}
+
+template <typename T>
+void lsmr_monitor_r(hgm_ctx* c, int64_t n, const T* p1, const T* p0, T* Ih, T* Ihb, T* Ir, bool first, double* out,
+                    const double* cf) {
+    const int np = parts_for(n);
+    double* parts = c->buf<double>("lsmr_mon_parts", MAX_PARTS);
+    const bool vec = al16(p1) && al16(p0) && al16(Ih) && al16(Ihb) && al16(Ir);
+#define HGM_MONR(F, V) k_lsmr_mon_r<T, F, V><<<np, BS, 0, c->stream>>>(n, p1, p0, Ih, Ihb, Ir, parts, cf)
+    if (first && vec) HGM_MONR(true, true);
+    else if (first) HGM_MONR(true, false);
+    else if (vec) HGM_MONR(false, true);
+    else HGM_MONR(false, false);
+#undef HGM_MONR
+    k_finalize<double><<<1, BS, 0, c->stream>>>(parts, np, out);
+    HGM_HIP(hipGetLastError());
+}
+
 template <typename T>
 void lsmr_monitor(hgm_ctx* c, int64_t n, const T* p1, const T* p0, double c1, double c0, double* Ih, double* Ihb,
                   double* Ix, const T* rhs, double f, double e, double cx, bool first, double* out, const double* cf) {
@@ -1929,6 +1996,8 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
     template void lsmr_monitor<T>(hgm_ctx*, int64_t, const T*, const T*, double, double, double*, double*, \
                                   double*, const T*, double, double, double, bool, double*, const double*); \
     template void lsmr_rot<T>(hgm_ctx*, const T*, const T*, double*, T*, double*, double*);   \
+    template void lsmr_monitor_r<T>(hgm_ctx*, int64_t, const T*, const T*, T*, T*, T*, bool, double*, \
+                                    const double*);                                            \
     template void lsmr_step<T>(hgm_ctx*, int64_t, T*, T*, T*, T*, const T*, const T*, const double*, int, \
                                const T*, T*);                                                  \
     template void div_sqrt_nz<T>(hgm_ctx*, int64_t, const T*, T*, const T*);                  \

@@ -1141,6 +1141,15 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     // an iteration enqueued past the stop leaves x untouched, and its histories are dropped.
     const bool dev_scalars = fp && kept && c->num.lsqr_dev;
     if (dev_scalars) {
+        // fp32 solves: the n-space monitor carries A'r in T (lsmr_monitor_r; Ir_0 = A'b)
+        constexpr bool img_t = std::is_same_v<T, float>;
+        T *Ihn_t = nullptr, *Ihbn_t = nullptr, *Irn_t = nullptr;
+        if constexpr (img_t) {
+            Ihn_t = c->buf<T>("lsmr_Ihn_t", n + 4);
+            Ihbn_t = c->buf<T>("lsmr_Ihbn_t", n + 4);
+            Irn_t = c->buf<T>("lsmr_Irn_t", n + 4);
+            HGM_HIP(hipMemcpyAsync(Irn_t, Atb, sizeof(T) * n, hipMemcpyDeviceToDevice, c->stream));
+        }
         double* st = c->buf<double>("lsmr_st", 9);
         double* cfm = c->buf<double>("lsmr_cf", 10);
         double* cfn = cfm + 5;
@@ -1170,7 +1179,8 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
                 if (xt && dist_n(c)) allreduce(c, errh + k, 1);
                 double* dm = dmonh + 2 * (size_t)k;
                 lsmr_monitor<T>(c, m, Av, nullptr, 0, 0, Ihm, Ihbm, Ixm, b, 0, 0, 0, k == 0, dm, cfm);
-                lsmr_monitor<T>(c, n, Atu1, Atu0, 0, 0, Ihn, Ihbn, Ixn, Atb, 0, 0, 0, k == 0, dm + 1, cfn);
+                if (img_t) lsmr_monitor_r<T>(c, n, Atu1, Atu0, Ihn_t, Ihbn_t, Irn_t, k == 0, dm + 1, cfn);
+                else lsmr_monitor<T>(c, n, Atu1, Atu0, 0, 0, Ihn, Ihbn, Ixn, Atb, 0, 0, 0, k == 0, dm + 1, cfn);
                 if (dist_n(c)) allreduce(c, dm + 1, 1);
                 std::swap(Atu0, Atu1);
                 if (tol > 0) lsmr_stop(c, dm, nb, tol, st, k);                   // :76
