@@ -125,6 +125,24 @@ static void ensure_stage(hgm_ctx* c, size_t bytes) {
     c->hstage_bytes = nb;
 }
 
+// Host waits of the solvers spin on the stream / event instead of a blocking synchronise, which may
+// sleep and then adds its wake-up to every host round trip (the GPU idles meanwhile); the spin holds
+// one host core while the GPU works.
+void stream_sync(hipStream_t s) {
+    for (;;) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) HGM_HIP(q);
+    }
+}
+static void event_sync(hipEvent_t e) {
+    for (;;) {
+        const hipError_t q = hipEventQuery(e);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) HGM_HIP(q);
+    }
+}
+
 void Reader::go() {
     size_t tot = 0;
     for (auto& it : items) tot += (it.bytes + 15) / 16 * 16;
@@ -135,7 +153,7 @@ void Reader::go() {
         if (it.bytes) HGM_HIP(hipMemcpyAsync(h + off, it.dev, it.bytes, hipMemcpyDeviceToHost, c->stream));
         off += (it.bytes + 15) / 16 * 16;
     }
-    HGM_HIP(hipStreamSynchronize(c->stream));
+    stream_sync(c->stream);
     off = 0;
     for (auto& it : items) {
         if (it.bytes) std::memcpy(it.host, h + off, it.bytes);
@@ -166,16 +184,16 @@ void h2d_pinned(hgm_ctx* c, void* dev, const void* host, size_t bytes) {
 void read_scalars(hgm_ctx* c, int first, int count) {
     HGM_HIP(hipMemcpyAsync(c->hscal + first, c->dscal + first, sizeof(double) * count, hipMemcpyDeviceToHost,
                            c->stream));
-    HGM_HIP(hipStreamSynchronize(c->stream));
+    stream_sync(c->stream);
 }
 
 void sync(hgm_ctx* c) {
-    HGM_HIP(hipStreamSynchronize(c->stream));
-    if (c->aux && c->aux != c->stream) HGM_HIP(hipStreamSynchronize(c->aux));
+    stream_sync(c->stream);
+    if (c->aux && c->aux != c->stream) stream_sync(c->aux);
 }
 
 void pinned_ring(hgm_ctx* c, size_t bytes) {
-    HGM_HIP(hipStreamSynchronize(c->stream));
+    stream_sync(c->stream);
     if (bytes > c->hring_bytes) {
         if (c->hring) (void)hipHostFree(c->hring);
         c->hring = nullptr;
@@ -228,21 +246,21 @@ void step_record(hgm_ctx* c, int k) {
 
 void step_wait(hgm_ctx* c, int k) {
     if (!c->host_stats) {
-        HGM_HIP(hipEventSynchronize(c->ev_step[k & 7]));
+        event_sync(c->ev_step[k & 7]);
         return;
     }
     const auto t0 = std::chrono::steady_clock::now();
-    HGM_HIP(hipEventSynchronize(c->ev_step[k & 7]));
+    event_sync(c->ev_step[k & 7]);
     c->wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
 void pipe_wait(hgm_ctx* c) {
     if (!c->host_stats) {
-        HGM_HIP(hipEventSynchronize(c->ev_pipe));
+        event_sync(c->ev_pipe);
         return;
     }
     const auto t0 = std::chrono::steady_clock::now();
-    HGM_HIP(hipEventSynchronize(c->ev_pipe));
+    event_sync(c->ev_pipe);
     c->wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     c->waits += 1;
 }

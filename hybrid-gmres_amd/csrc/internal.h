@@ -402,6 +402,7 @@ template <typename T> void div_sqrt_nz(hgm_ctx* c, int64_t n, const T* in, T* ou
 // out[i] = epi(in[i], a, z[i]) (out may alias z): the epilogue of an SpMV applied to its raw product
 template <typename T> void epilogue_to(hgm_ctx* c, int64_t n, const T* in, T* out, int epi, T a, const T* z);
 template <typename T> void fill(hgm_ctx* c, int64_t n, T* x, T v);
+template <typename T> void scale(hgm_ctx* c, int64_t n, const T* in, T* out, T a);   // out = a * in
 // x_i = deterministic pseudo-random value in (-1, 1) (splitmix64 of seed + i)
 template <typename T> void fill_hash(hgm_ctx* c, int64_t n, T* x, uint64_t seed);
 template <typename T> void convert(hgm_ctx* c, int64_t n, const double* in, T* out);
@@ -511,6 +512,8 @@ void h2d(hgm_ctx* c, void* dev, const void* host, size_t bytes);
 // another h2d_pinned before the stream has passed the previous one (one per iteration)
 void h2d_pinned(hgm_ctx* c, void* dev, const void* host, size_t bytes);
 void read_scalars(hgm_ctx* c, int first, int count);   // dscal -> hscal (sync)
+// wait for stream s by spinning on hipStreamQuery (no sleeping wake-up after long waits)
+void stream_sync(hipStream_t s);
 // zero-initialised pinned host ring of >= bytes (c->hring / c->hring_dev), after a
 // stream synchronisation (no kernel may still be writing the previous one)
 void pinned_ring(hgm_ctx* c, size_t bytes);

@@ -1928,6 +1928,16 @@ void lsmr_monitor(hgm_ctx* c, int64_t n, const T* p1, const T* p0, double c1, do
     HGM_HIP(hipGetLastError());
 }
 
+// out = a * in
+template <typename T>
+__global__ __launch_bounds__(BS) void k_scale(int64_t n, const T* __restrict__ in, T* __restrict__ out, T a) {
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) out[i] = a * in[i];
+}
+template <typename T> void scale(hgm_ctx* c, int64_t n, const T* in, T* out, T a) {
+    k_scale<T><<<grid_for(n), BS, 0, c->stream>>>(n, in, out, a);
+    HGM_HIP(hipGetLastError());
+}
+
 template <typename T>
 __global__ __launch_bounds__(BS) void k_fill(int64_t n, T* x, T v) {
     for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS) x[i] = v;
@@ -2002,6 +2012,7 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
                                const T*, T*);                                                  \
     template void div_sqrt_nz<T>(hgm_ctx*, int64_t, const T*, T*, const T*);                  \
     template void fill<T>(hgm_ctx*, int64_t, T*, T);                                           \
+    template void scale<T>(hgm_ctx*, int64_t, const T*, T*, T);                                \
     template void fill_hash<T>(hgm_ctx*, int64_t, T*, uint64_t);                               \
     template void convert<T>(hgm_ctx*, int64_t, const double*, T*);                            \
     template void convert_back<T>(hgm_ctx*, int64_t, const T*, double*);                       \

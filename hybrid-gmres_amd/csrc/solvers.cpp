@@ -110,16 +110,16 @@ void stage_out(hgm_ctx* c, double* out, const T* d, int64_t n, bool dev) {
     if (std::is_same<T, double>::value) {
         if (dev) {
             HGM_HIP(hipMemcpyAsync(out, d, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
-            HGM_HIP(hipStreamSynchronize(c->stream));
+            stream_sync(c->stream);
         } else {
             HGM_HIP(hipMemcpyAsync(out, d, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
-            HGM_HIP(hipStreamSynchronize(c->stream));
+            stream_sync(c->stream);
         }
     } else {
         double* tmp = dev ? out : c->buf<double>("out_f64", n);
         convert_back<T>(c, n, d, tmp);
         if (!dev) HGM_HIP(hipMemcpyAsync(out, tmp, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
-        HGM_HIP(hipStreamSynchronize(c->stream));
+        stream_sync(c->stream);
     }
 }
 
@@ -152,7 +152,7 @@ void stage_out_n(hgm_ctx* c, double* out, const T* d, int64_t n, bool dev, const
     }
     if (dev && std::is_same<T, double>::value) {   // straight into the caller's device buffer
         pix_permute<T>(c, o, d, reinterpret_cast<T*>(out), 1);
-        HGM_HIP(hipStreamSynchronize(c->stream));
+        stream_sync(c->stream);
         return;
     }
     T* q = c->buf<T>("out_pix", n);
@@ -316,7 +316,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     if (c->num.recon_serial >= 0) recon_serial = c->num.recon_serial != 0;
     // (a communicator's solve keeps one stream whatever the ring)
     hipStream_t rs_stream = (zc && !recon_serial && !dist_n(c)) ? aux_stream(c) : st;
-    if (rs_stream != st) HGM_HIP(hipStreamSynchronize(rs_stream));
+    if (rs_stream != st) stream_sync(rs_stream);
     pinned_ring(c, sizeof(double) * ring_n);
     const double* hr = c->hring;
     const bool poll = zc && c->num.ring_poll && !parity;
@@ -757,7 +757,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     }
     if (k == maxit) k = maxit - 1;
     const int nit = k + 1;                               // niters = k
-    if (rs_stream != st) HGM_HIP(hipStreamSynchronize(rs_stream));
+    if (rs_stream != st) stream_sync(rs_stream);
     if (!x_assigned) throw Error{HGM_E_NOT_ASSIGNED, "Output argument \"x\" not assigned during call (breakdown at k = 1)"};
     if (!staged) stage_out_n<T>(c, x_out, x, n, dev, po);
     if (c->host_stats) {
@@ -1090,7 +1090,6 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         Ixn = c->buf<double>("lsmr_Ixn", n + 1);
         fill<double>(c, m, Ixm, 0.0);                                          // A*x_0 = 0
         fill<double>(c, n, Ixn, 0.0);                                          // A'A*x_0 = 0
-        apply_B<T>(c, At, b, Atb, EPI_NONE, T(0), nullptr);                    // A'*b (once per solve)
     }
     // One pass over the operator per iteration (as lsqr_t): the step :38-39 and
     // A*v_hat in one pass over At, A*v_{k+1} (:34, the kept A*v) = (A*v_hat) / alpha.
@@ -1115,6 +1114,9 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         nsumsq<T>(c, n, v0, sl + S_ALPHA);
     }
     double alpha = std::sqrt((double)read1<T>(c, fp ? wm + m : sl + S_ALPHA));   // :15
+    // A'*b for the monitors' A'r = A'b - A'A*x: beta * A'*u_0 (u_0 = b / beta, :12-14), the product
+    // just formed, instead of one more pass over the operator per solve (equal up to rounding)
+    if (kept) scale<T>(c, n, Atu0, Atb, (T)beta);
     if (alpha > 0) div_scalar<T>(c, n, v0, v, (T)alpha);                       // :16
     else if (kept) HGM_HIP(hipMemcpyAsync(v, v0, sizeof(T) * n, hipMemcpyDeviceToDevice, c->stream));
     double zetabar = alpha * beta, alphabar = alpha, rho = 1, rhobar = 1, cbar = 1, sbar = 0;   // :19-23
