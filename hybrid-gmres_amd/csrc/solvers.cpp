@@ -315,7 +315,12 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     bool recon_serial = !gem && (int64_t)n >= c->num.recon_serial_n;
     if (c->num.recon_serial >= 0) recon_serial = c->num.recon_serial != 0;
     // (a communicator's solve keeps one stream whatever the ring)
-    hipStream_t rs_stream = (zc && !recon_serial && !dist_n(c)) ? aux_stream(c) : st;
+    // On a communicator the m-space solve's residual-only reconstructions (gem_ab: the kept A*B*Q
+    // columns and b are replicated, so no collective runs in them) go to the auxiliary stream as
+    // well; a reconstruction that forms x all-reduces its error and stays on the step stream, so
+    // the communicator's collectives keep one stream and one order on every rank.
+    const bool rs_aux_dist = dist_n(c) && gem_ab && !recon_serial && zc;
+    hipStream_t rs_stream = (zc && !recon_serial && (!dist_n(c) || rs_aux_dist)) ? aux_stream(c) : st;
     if (rs_stream != st) stream_sync(rs_stream);
     pinned_ring(c, sizeof(double) * ring_n);
     const double* hr = c->hring;
@@ -524,7 +529,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // stream dependency; it writes only x, its own scratch and ring slot kq.
     int x_pending = -1;   // the last reconstruction, when it left x unformed (Gram error monitor)
     auto enqueue_recon = [&](int kq, bool want_x) {
-        StreamScope scope(c, rs_stream, "aux:");
+        StreamScope scope(c, (rs_aux_dist && want_x) ? st : rs_stream, (rs_aux_dist && want_x) ? "" : "aux:");
         const int kk = kq + 1;
         const T* yk = c->hring_dev + offY + (size_t)kq * maxit;
         T* rslot = dr + offM + 2 * (size_t)kq;
@@ -742,7 +747,8 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         // reconstruction on the aux stream, x is staged out behind it there (one sync, no
         // host wake-up in between).
         // (x_out == NULL: nothing to stage, so wait for the last monitors explicitly)
-        if (rs_stream != st && x_assigned && x_out != nullptr) {
+        // (a communicator's last reconstruction formed x on the step stream: staged out there below)
+        if (rs_stream != st && !rs_aux_dist && x_assigned && x_out != nullptr) {
             StreamScope scope(c, rs_stream, "aux:");
             stage_out_n<T>(c, x_out, x, n, dev, po);     // ends with a sync of the aux stream
             staged = true;
