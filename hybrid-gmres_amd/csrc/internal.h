@@ -337,7 +337,9 @@ bool krylov_padded(const hgm_ctx* c, int64_t ldq);
 template <typename T>
 void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, const T* src = nullptr,
          const MdotJob<T>* side = nullptr, PendNorm<T>* defer = nullptr, const T* pend_h = nullptr,
-         const T* xe = nullptr, T* qg = nullptr);
+         const T* xe = nullptr, T* qg = nullptr, const double* cp_src = nullptr, double* cp_dst = nullptr);
+// (cp_src / cp_dst: one value copied into the host ring with a system-scope store by the sweep's
+// first workgroup, instead of a copy_sys launch of its own; a communicator's side dot)
 // Gram error monitor (one-reduction form only, mgs_gram_ok): with xe = x_true the sweep of
 // step kk also writes qg[0..kk+1] = [q_kk'q_0 .. q_kk'q_{kk-1}, q_kk'q_kk, q_kk'x_true] (host
 // ring, system-scope stores), so ||Q y - x_true||^2 = xt'xt - 2 y'(Q'xt) + y'(Q'Q)y needs no

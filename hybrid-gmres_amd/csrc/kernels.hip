@@ -806,9 +806,11 @@ __device__ __forceinline__ void mgs1_substitute(int kk, const T* sr, const T* sG
 template <typename T, int P>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_mgs1_dots(
     int64_t n, const T* Q, int64_t ldq, int kk, const T* __restrict__ w, int npr, T* __restrict__ pr,
-    T* __restrict__ pg, MdotStage<T> side, const T* hpend, const T* __restrict__ xe) {
+    T* __restrict__ pg, MdotStage<T> side, const T* hpend, const T* __restrict__ xe, const double* cp_src,
+    double* cp_dst) {
     using T2 = typename V2<T>::t;
     constexpr int NW = BS / 64;
+    if (cp_dst && blockIdx.x == 0 && threadIdx.x == 0) st_sys(cp_dst, *cp_src);   // (mgs: the ring copy)
     // acc[row][wave]: rows 0..kk = q_c'w, kk+1.. = q_c'q_k (c < kk; with xe also c = kk, then
     // q_k'x_true)
     __shared__ T acc[2 * MGS1_MAXC + 2][NW];
@@ -1206,8 +1208,16 @@ static void mgs_parity(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol
 
 template <typename T>
 void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, const T* src,
-         const MdotJob<T>* side, PendNorm<T>* defer, const T* pend_h, const T* xe, T* qg) {
+         const MdotJob<T>* side, PendNorm<T>* defer, const T* pend_h, const T* xe, T* qg, const double* cp_src,
+         double* cp_dst) {
     if (defer) defer->np = 0;
+    // the ring copy rides on the one-reduction sweep's dots kernel; every other form copies first
+    const int64_t sq = ldq / MGS1_BS;   // (mgs_single's shapes)
+    const bool single = !dist && krylov_padded(c, ldq) && n <= ldq && sq % 4 == 0 && sq >= 4 && sq <= 24;
+    if (cp_dst && !(kk + 1 <= MGS1_MAXC && mgs1_mode(c) == 1 && !c->num.parity && !single)) {
+        copy_sys(c, cp_src, cp_dst);
+        cp_dst = nullptr;
+    }
     if (c->num.parity) {
         HGM_REQUIRE(!dist && !xe && !pend_h, "mgs: parity mode is single-rank, without the fused monitors");
         hipEvent_t t0 = nullptr;
@@ -1256,7 +1266,8 @@ void mgs(hgm_ctx* c, int64_t n, T* Q, int64_t ldq, int kk, T* Hcol, bool dist, c
         STMT;               \
     }
 #define HGM_MGS1_PS(STMT) HGM_MGS1_P(1, STMT) else HGM_MGS1_P(2, STMT) else HGM_MGS1_P(4, STMT) else HGM_REQUIRE(false, "mgs1: tile width")
-        HGM_MGS1_PS((k_mgs1_dots<T, PT><<<npr + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1, pend_h, xe)));
+        HGM_MGS1_PS((k_mgs1_dots<T, PT><<<npr + s1.blocks(), BS, 0, st>>>(n, Q, ldq, kk, src, npr, pr, pg, s1, pend_h, xe,
+                                                                          cp_src, cp_dst)));
         const int nb = npr;
         T* pout = c->buf<T>("mgs_parts", 2 * MAX_PARTS);
         const bool fused = !dist && c->num.mgs_fused;
@@ -1994,7 +2005,7 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
                            const T*, int64_t, const T*, T*);                                   \
     template void normalize_to<T>(hgm_ctx*, int64_t, T*, T*);                                                        \
     template void mgs<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool, const T*, const MdotJob<T>*, PendNorm<T>*,   \
-                         const T*, const T*, T*);                                              \
+                         const T*, const T*, T*, const double*, double*);                      \
     template void cgs2<T>(hgm_ctx*, int64_t, T*, int64_t, int, T*, bool);                      \
     template void gemv<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, int);       \
     template void div_scalar<T>(hgm_ctx*, int64_t, const T*, T*, T);                           \

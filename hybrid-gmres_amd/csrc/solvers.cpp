@@ -461,8 +461,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
                     zx_fused = fused_ab(c, B, fplan, qk, Bq, w, zxf ? xt : nullptr, ride ? w + m : zx_dst);
                 zx_rode = ride && zx_fused;
                 if (dist_n(c)) allreduce(c, w, zx_rode ? m + 1 : m);             // (as apply_A)
-                if constexpr (std::is_same_v<T, double>)
-                    if (zx_rode) copy_sys(c, w + m, dr + offQG + (size_t)kq * LQ + kq + 2);
+                // (the all-reduced side dot goes into the ring with the MGS sweep below)
             } else {
                 apply_B<T>(c, B, qk, Bq, EPI_NONE, T(0), nullptr);                  // B*Q(:,k)
                 apply_A<T>(c, A, Bq, w, EPI_NONE, T(0), nullptr);                   // A*(B*Q(:,k))
@@ -502,9 +501,16 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
                 zx.out = dist_n(c) ? dslot<T>(c, S_AUX2) : zx_ring;   // (the fused pass's zx_dst too)
             }
             // the Gram row's extra dot: x_true (n-space) or b (m-space, unused: the row is for L)
+            const double* cps = nullptr;
+            double* cpd = nullptr;
+            if constexpr (std::is_same_v<T, double>)
+                if (zx_rode) {
+                    cps = reinterpret_cast<const double*>(ABQ ? ABQ + (int64_t)kq * ldaq + m : v + m);
+                    cpd = dr + offQG + (size_t)kq * LQ + kq + 2;
+                }
             mgs<T>(c, dim, Q, ldq, kq, Hcol, dist, (!nspace && ABQ) ? ABQ + (int64_t)kq * ldaq : nullptr,
                    gem_ab ? (zx_fused ? nullptr : &zx) : side, defer, pending_in ? (const T*)pn_h : nullptr,
-                   gem ? (gem_n ? xt : b) : nullptr, gem ? dr + offQG + (size_t)kq * LQ : nullptr);
+                   gem ? (gem_n ? xt : b) : nullptr, gem ? dr + offQG + (size_t)kq * LQ : nullptr, cps, cpd);
             if (gem_ab && dist_n(c) && !zx_rode) {        // x_true'(B*q_k) over the pixel shards
                 allreduce(c, zx.out, 1);
                 if constexpr (std::is_same_v<T, double>) copy_sys(c, zx.out, zx_ring);
