@@ -358,7 +358,9 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // iteration (hybrid_*_rtp.m:32-33); the values are loop-invariant.
     double nb = 0, nxt = 0, beta = 0, xt2 = 0;
     T* q0 = Q;
-    if (poll && dev && rs_stream != st) {
+    // (a communicator all-reduces the x_true norm over the pixel shards: the second branch, whatever
+    // stream the reconstructions use)
+    if (poll && dev && rs_stream != st && !dist_n(c)) {
         // no host round trip before the first step: the norms land in the ring (read at
         // iteration 0) and r0 is divided on the device.  With device inputs the two norms
         // run on the aux stream, beside B*b (x_true in the caller's order: same norm).

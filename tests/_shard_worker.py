@@ -56,6 +56,32 @@ def main():
     ctx.close()
 
 
+def _abn_device(ctx, A_g, B_g, b, xt, maxit):
+    import ctypes as C
+    import torch
+    from hgmres import _lib as L
+    from hgmres.core import _ops
+    ctx_, Ao, Bo = _ops(A_g, B_g, ctx)
+    dev = torch.device("cuda", 0)
+    b_d = torch.from_numpy(np.ascontiguousarray(b, dtype=np.float64)).to(dev)
+    xt_d = torch.from_numpy(np.ascontiguousarray(xt, dtype=np.float64)).to(dev)
+    x_d = torch.zeros(Ao.shape[1], dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    err, res = np.zeros(maxit), np.zeros(maxit)
+    it = C.c_int(0)
+    o = L.hgm_opts()
+    o.flags = L.HGM_DEVICE_PTRS
+    o.orth = L.HGM_MGS
+    o.H_out = None
+    dp = lambda t: C.cast(C.c_void_p(t.data_ptr()), L.dp)   # noqa: E731
+    rc = L.load().hgm_gmres_bounds_ex(ctx_.handle, C.byref(o), Ao._h, Bo._h, dp(b_d), dp(xt_d), 0.0, maxit, 0.0,
+                                      L.HGM_SIDE_AB, 0, dp(x_d), err.ctypes.data_as(L.dp), res.ctypes.data_as(L.dp),
+                                      C.byref(it))
+    assert rc == 0, rc
+    k = it.value
+    return dict(abnd_x=x_d.cpu().numpy(), abnd_err=err[:k].copy(), abnd_res=res[:k].copy())
+
+
 def solve_all(ctx, rank, world):
     """Every sharded solve of the test on rank `rank`'s shard; returns the arrays by tag."""
     P = tomo_problem(64, 90, noise=1e-2, seed=0)
@@ -72,6 +98,9 @@ def solve_all(ctx, rank, world):
     # configs[3]'s AB-GMRES (m-space Arnoldi, replicated basis, one all-reduce per A*(B*q))
     out_ = hgmres.ABgmres_nonhybrid_bounds(A_g, B_g, P.b, xt, 0.0, 12, ctx=ctx, return_H=True)
     res.update(abn_x=out_[0], abn_res=out_[2], abn_err=out_[1], abn_H=out_[-1])
+    # the same solve with device inputs / outputs (HGM_DEVICE_PTRS, bench.py's hand-over): the
+    # setup norms take another branch there (||x_true||^2 must still be summed over the shards)
+    res.update(_abn_device(ctx, A_g, B_g, P.b, xt, 12))
     x, e, r, k, H = hgmres.hybrid_ab_gmres_rtp(A_g, B_g, P.b, xt, 0.0, 12, 1e-2, ctx=ctx, return_H=True)
     res.update(hab_x=x, hab_res=r, hab_err=e, hab_H=H)
     # configs[4]: the Golub-Kahan path on fp32 shards

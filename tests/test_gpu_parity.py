@@ -967,6 +967,12 @@ def test_shard_emulation_two_ranks(tmp_path):
     for tag in ("hba", "abn", "hab"):
         H_ok(o[0][f"{tag}_H"], s[f"{tag}_H"])
         assert np.array_equal(o[0][f"{tag}_H"], o[1][f"{tag}_H"])
+    # the error history over the shards (||x_true|| all-reduced), host and device hand-over alike
+    for r in range(2):
+        hist_ok(o[r]["abn_err"], s["abn_err"], TOL)
+        hist_ok(o[r]["abnd_err"], o[r]["abn_err"], 1e-12)
+        hist_ok(o[r]["abnd_res"], o[r]["abn_res"], 1e-12)
+        assert rel(o[r]["abnd_x"], o[r]["abn_x"]) < 1e-12
     # tiled shards in stored order (bench.py build_shard): the 2-rank solves match the
     # 1-rank solve of the same tiled operator, whose x (stored order) is the reference-order solve's
     from hgmres.core import stored_pixel_index

@@ -36,7 +36,7 @@ def test_one_rank_rccl_matches_single_context():
         s = solve_all(ctx0, 0, 1)
     finally:
         ctx0.close()
-    tols = {"hba": TOL, "abp": TOL, "abn": TOL, "hab": TOL, "tabn": TOL, "thba": TOL,
+    tols = {"hba": TOL, "abp": TOL, "abn": TOL, "abnd": TOL, "hab": TOL, "tabn": TOL, "thba": TOL,
             "lsqr": 1e-7, "lsqr32": 1e-4,          # the Golub-Kahan envelope of the shard test
             "tlsqr32": 1e-4, "tlsmr32": 1e-4}      # (fp32 one-pass shards; the same code path at one rank)
     for tag, tol in tols.items():
