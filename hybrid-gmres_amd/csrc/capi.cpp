@@ -4,6 +4,7 @@
 // and keeps the message for hgm_last_error().
 #include <limits.h>
 #include <link.h>
+#include <sched.h>
 
 #include <chrono>
 #include <cmath>
@@ -126,20 +127,48 @@ static void ensure_stage(hgm_ctx* c, size_t bytes) {
 }
 
 // Host waits of the solvers spin on the stream / event instead of a blocking synchronise, which may
-// sleep and then adds its wake-up to every host round trip (the GPU idles meanwhile); the spin holds
-// one host core while the GPU works.
+// sleep and then adds its wake-up to every host round trip (the GPU idles meanwhile).  The spin is
+// bounded: after HGM_OPT_HOST_SPIN_US of pure spinning every further poll yields the
+// core (sched_yield), so a long wait (a plan build, the stage-out, a rank waiting on its peers)
+// hands the core to RCCL's proxy and other runnable threads; with nothing else runnable the yield
+// returns at once, so the wake-up latency stays that of the spin.  A negative value waits with the
+// blocking hipStreamSynchronize / hipEventSynchronize instead.
+std::atomic<int> g_host_spin_us{200};
+
+void HostPause::operator()() {
+    if (++polls < 64) return;
+    polls = 0;
+    const auto now = std::chrono::steady_clock::now();
+    if (!yielding &&
+        std::chrono::duration_cast<std::chrono::microseconds>(now - t0).count() >= g_host_spin_us.load())
+        yielding = true;
+    if (yielding) sched_yield();
+}
+
 void stream_sync(hipStream_t s) {
+    if (g_host_spin_us.load() < 0) {
+        HGM_HIP(hipStreamSynchronize(s));
+        return;
+    }
+    HostPause pause;
     for (;;) {
         const hipError_t q = hipStreamQuery(s);
         if (q == hipSuccess) return;
         if (q != hipErrorNotReady) HGM_HIP(q);
+        pause();
     }
 }
 static void event_sync(hipEvent_t e) {
+    if (g_host_spin_us.load() < 0) {
+        HGM_HIP(hipEventSynchronize(e));
+        return;
+    }
+    HostPause pause;
     for (;;) {
         const hipError_t q = hipEventQuery(e);
         if (q == hipSuccess) return;
         if (q != hipErrorNotReady) HGM_HIP(q);
+        pause();
     }
 }
 
@@ -551,6 +580,10 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             break;
         case HGM_OPT_FUSED_PLAN_DEV: if (!b01) return bad("fused_plan_dev is 0 or 1"); n.fused_plan_dev = v != 0; break;
         case HGM_OPT_FUSED_REDUCE: if (!b01) return bad("fused_reduce is 0 or 1"); n.fused_reduce = (int)v; break;
+        case HGM_OPT_HOST_SPIN_US:
+            if (!(v == std::floor(v) && std::fabs(v) <= 1e9)) return bad("host_spin_us is an integer");
+            g_host_spin_us.store((int)v);
+            break;
         default: return bad("unknown option");
     }
     return HGM_OK;
@@ -592,6 +625,7 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_FUSED_ACC32: *v = n.fused_acc32; break;
         case HGM_OPT_FUSED_PLAN_DEV: *v = n.fused_plan_dev; break;
         case HGM_OPT_FUSED_REDUCE: *v = n.fused_reduce; break;
+        case HGM_OPT_HOST_SPIN_US: *v = g_host_spin_us.load(); break;
         default: return HGM_E_ARG;
     }
     return HGM_OK;

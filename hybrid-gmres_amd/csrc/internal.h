@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <map>
 #include <string>
@@ -514,8 +516,17 @@ void h2d(hgm_ctx* c, void* dev, const void* host, size_t bytes);
 // another h2d_pinned before the stream has passed the previous one (one per iteration)
 void h2d_pinned(hgm_ctx* c, void* dev, const void* host, size_t bytes);
 void read_scalars(hgm_ctx* c, int first, int count);   // dscal -> hscal (sync)
-// wait for stream s by spinning on hipStreamQuery (no sleeping wake-up after long waits)
+// wait for stream s by spinning on hipStreamQuery (no sleeping wake-up after long waits); the spin
+// yields the core after HGM_OPT_HOST_SPIN_US (process-wide: g_host_spin_us; < 0 = blocking waits)
 void stream_sync(hipStream_t s);
+extern std::atomic<int> g_host_spin_us;
+// the back-off of a host spin loop: call once per poll
+struct HostPause {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    int polls = 0;
+    bool yielding = false;
+    void operator()();
+};
 // zero-initialised pinned host ring of >= bytes (c->hring / c->hring_dev), after a
 // stream synchronisation (no kernel may still be writing the previous one)
 void pinned_ring(hgm_ctx* c, size_t bytes);

@@ -355,11 +355,15 @@ void finalize_operator(hgm_ctx* c, hgm_mat* M) {
             // fetched into one L2 instead of eight (paged kernel, alternating runs: C4 A 2.36 ->
             // 2.31 ms, C3 A 252 -> 238 us, bitwise equal; profiles/r2_c{3,4}_xcd.log)
             M->variant |= SPMV_XCD;
-        } else if (M->nnz >= 50000000) {
+        } else if (M->nnz >= 50000000 && avg <= 256 &&
+                   (double)M->cols * (M->dtype == HGM_F64 ? 8.0 : 4.0) <= 4.0 * 1024 * 1024) {
             // long rows over an L2-resident x at >= 5e7 nnz: the unmatched pixel-driven
             // back-projector of C4 (94 entries per pixel row, 1.6e9 nnz; bench.py --unmatched).
             // Paged streaming with 4 lanes per row: 4.10 -> 2.61 ms (row kernel, 16 lanes), 2 / 8
-            // lanes 2.79 / 2.87 ms, unpaged 3.74 ms (profiles/r4_unmatched_c4_b_variants.log)
+            // lanes 2.79 / 2.87 ms, unpaged 3.74 ms (profiles/r4_unmatched_c4_b_variants.log).
+            // Gated on the shape it was measured on: rows of <= 256 entries and an
+            // x (2.2 MB there) that fits one XCD's 4 MiB L2; other single-band operators keep the
+            // row kernel below.
             M->variant = SPMV_STREAM | SPMV_NT;
             M->sgroup = 4;
         } else {

@@ -198,6 +198,7 @@ static void ring_wait(hgm_ctx* c, const double* ring, const std::vector<size_t>&
     const auto t0 = std::chrono::steady_clock::now();
     auto last = t0;
     bool idle_seen = false;
+    HostPause pause;
     for (;;) {
         bool all = true;
         for (size_t i : idx)
@@ -206,6 +207,7 @@ static void ring_wait(hgm_ctx* c, const double* ring, const std::vector<size_t>&
                 break;
             }
         if (all) break;
+        pause();
         const auto now = std::chrono::steady_clock::now();
         if (now - last > std::chrono::milliseconds(1)) {
             last = now;
@@ -319,6 +321,10 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // columns and b are replicated, so no collective runs in them) go to the auxiliary stream as
     // well; a reconstruction that forms x all-reduces its error and stays on the step stream, so
     // the communicator's collectives keep one stream and one order on every rank.
+    // Scratch invariant: reconstructions on the auxiliary stream and the x-forming ones
+    // on the step stream share the recon_parts / recon_noerr scratch buffers.  That is safe only
+    // because the host waits for reconstruction k's ring slots (ring_wait on both streams) before
+    // it enqueues reconstruction k+1 on either stream, so two reconstructions never run at once.
     const bool rs_aux_dist = dist_n(c) && gem_ab && !recon_serial && zc;
     hipStream_t rs_stream = (zc && !recon_serial && (!dist_n(c) || rs_aux_dist)) ? aux_stream(c) : st;
     if (rs_stream != st) stream_sync(rs_stream);
@@ -883,7 +889,11 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         fa.w = wm;
         fa.side_sq = true;
         fa.side_out = wm + m;
-        const int batch = tol > 0 ? 8 : maxit;
+        // HGM_OPT_LSQR_DEV = 0: the same pass with host scalars -- beta^2 and alpha^2 read back per
+        // iteration, the rotation and the stop test on the host in the same double arithmetic as
+        // k_lsqr_rot (the coefficients uploaded for lsqr_step), so the iterates keep their bits
+        const bool host_sc = !c->num.lsqr_dev;
+        const int batch = tol > 0 && !host_sc ? 8 : maxit;
         int stop = 0;
         for (k = 0; k < maxit && stop == 0;) {
             const int kend = std::min(maxit, k + batch);
@@ -892,10 +902,35 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
                 div_sqrt<T>(c, m, t, u, sl + S_BETA);                                // :24
                 fused_pass<T>(c, At, fp, fa);                                        // :26-27 (+ A*v_hat)
                 if (dist_n(c)) allreduce(c, wm, m + 1);
-                lsqr_rot<T>(c, sl + S_BETA, wm + m, st, coef, phib, k, nb, tol);     // :31-38, :44-46
+                if (host_sc) {
+                    T ss[2] = {T(0), T(0)};
+                    Reader rr(c);
+                    rr.add(&ss[0], sl + S_BETA, sizeof(T));
+                    rr.add(&ss[1], wm + m, sizeof(T));
+                    rr.go();
+                    beta = std::sqrt((double)ss[0]);                                 // :23
+                    alpha = std::sqrt((double)ss[1]);                                // :27
+                    const double rho = std::sqrt(rho_bar * rho_bar + beta * beta);   // :31-38
+                    const double cs = rho_bar / rho, sn = beta / rho;
+                    const double theta = sn * alpha;
+                    rho_bar = -cs * alpha;
+                    const double phi = cs * phi_bar;
+                    phi_bar = sn * phi_bar;
+                    const T cf[2] = {(T)(phi / rho), (T)(theta / rho)};
+                    h2d_pinned(c, coef, cf, sizeof(cf));    // the next Reader syncs past its use
+                    res[k] = std::fabs(phi_bar) / nb;                                // :44
+                    if (res[k] <= tol) stop = k + 1;                                 // :46 (<=)
+                } else {
+                    lsqr_rot<T>(c, sl + S_BETA, wm + m, st, coef, phib, k, nb, tol); // :31-38, :44-46
+                }
                 lsqr_step<T>(c, n, x, w, v, wm + m, coef, st, k, xt, errh + k);     // :28, :40-41, :43
                 if (dist_n(c)) allreduce(c, errh + k, 1);
+                if (stop) {
+                    ++k;
+                    break;
+                }
             }
+            if (host_sc) continue;
             double sv = 0;
             Reader rs(c);
             rs.add(&sv, st + 2, sizeof(double));
@@ -903,11 +938,13 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
             stop = (int)sv;
         }
         k = stop > 0 ? stop - 1 : maxit;
-        std::vector<double> pbh(maxit);
-        Reader rh(c);
-        rh.add(pbh.data(), phib, sizeof(double) * maxit);
-        rh.go();
-        for (int i = 0; i < maxit && i <= k; ++i) res[i] = std::fabs(pbh[i]) / nb;   // :44
+        if (!host_sc) {
+            std::vector<double> pbh(maxit);
+            Reader rh(c);
+            rh.add(pbh.data(), phib, sizeof(double) * maxit);
+            rh.go();
+            for (int i = 0; i < maxit && i <= k; ++i) res[i] = std::fabs(pbh[i]) / nb;   // :44
+        }
     }
     if (dev_scalars) {
         double* st = c->buf<double>("lsqr_st", 4);

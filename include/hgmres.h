@@ -146,9 +146,13 @@ enum hgm_ctx_option {
                                       read-add-write, 2 fp64 accumulators and partials (ds_add_f64) [1] */,
     HGM_OPT_FUSED_PLAN_DEV = 31,   /* ... the row-wave plan's region ray sets and slots built on the device
                                       (an LDS bitmap per region) [1]; 0 the host build (same bytes) */
-    HGM_OPT_FUSED_REDUCE = 32      /* ... the row-wave pass's partial reduction: 1 by bands of 64 rays over
+    HGM_OPT_FUSED_REDUCE = 32,     /* ... the row-wave pass's partial reduction: 1 by bands of 64 rays over
                                       runs of consecutive slots, 0 per ray through its slot list [0] (the
                                       same sums: bitwise equal) */
+    HGM_OPT_HOST_SPIN_US = 33      /* host waits (stream / event / ring polls): microseconds of pure spinning
+                                      before each further poll yields the core (sched_yield) [200]; < 0: the
+                                      blocking hipStreamSynchronize / hipEventSynchronize.  PROCESS-WIDE: the
+                                      last value set on any context applies to every context */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for

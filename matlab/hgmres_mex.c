@@ -25,10 +25,13 @@
  * reproduced; libhgmres' fixed-order parity mode (HGM_OPT_PARITY) runs the
  * reference's sequence of operations in one documented order, in which it is bit-identical to the
  * oracle restatement.  'auto' (the default) selects it for every problem the reference itself runs
- * -- operators of at most HGM_PARITY_AUTO_DIM rows and columns (the n = 32 shaw/heat/deriv2
+ * -- operators of at most HGM_PARITY_AUTO_DIM = 4096 rows and columns (the n = 32 shaw/heat/deriv2
  * drivers, the 32 x 32 phantom of run_2D_phantom.m) -- so gcv_function.m / analyze_regularization.m
  * see oracle-identical outputs there without opting in, and the production kernels (fused,
- * reordered sums) above it.  'on' / 'off' force one or the other.
+ * reordered sums) above it.  'on' / 'off' force one or the other.  NOTE: 'auto' changed the
+ * default in round 4 -- callers at <= 4096 x 4096 now get the fixed-order kernels unless they set
+ * 'off'.  The option is set per call from that call's operator on the gateway's private context
+ * (g_ctx), so no choice outlives its call.
  *
  * Operands: MATLAB sparse (CSC, 64-bit mwIndex) is handed over as is (hgm_mat_create_csc); a
  * dense double matrix (the n = 32 drivers' shaw/deriv2 operators) is handed over as a CSC that

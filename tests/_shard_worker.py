@@ -49,7 +49,7 @@ def main():
                 arr[:] = conn.recv()
 
         ctx.set_host_allreduce(rank, world, allreduce)
-    res = solve_all(ctx, rank, world)
+    res = solve_c4(ctx, rank, world) if len(sys.argv) > 5 and sys.argv[5] == "c4" else solve_all(ctx, rank, world)
     np.savez(os.path.join(out, f"rank{rank}_of{world}.npz"), **res)
     if conn is not None:
         conn.close()
@@ -125,6 +125,12 @@ def solve_all(ctx, rank, world):
     res.update(tabn_x=out_[0], tabn_res=out_[2], tabn_err=out_[1], tabn_H=out_[-1])
     x, e, r, k, H = hgmres.hybrid_ba_gmres_rtp(A2, B2, P.b, xs[tlo:thi], 0.0, 15, 1e-2, ctx=ctx, return_H=True)
     res.update(thba_x=x, thba_res=r, thba_err=e, thba_H=H)
+    # the one-pass LSQR on these shards with a tol stop inside the first batch of 8:
+    # tol between the 5th and 6th residual estimates of a tol = 0 run (the same on every rank)
+    r0 = hgmres.lsqr_solver(A2, P.b, xs[tlo:thi], 0.0, 12, ctx=ctx, At=B2)[2]
+    tol = 0.5 * (r0[4] + r0[5])
+    x, e, r, k = hgmres.lsqr_solver(A2, P.b, xs[tlo:thi], tol, 12, ctx=ctx, At=B2)
+    res.update(tlsqrtol_x=x, tlsqrtol_res=r, tlsqrtol_err=e, tlsqrtol_k=k, tlsqrtol_tol=tol)
     # configs[2]'s GCV on pixel shards: the n-space Arnoldi (sharded basis) once, fminbnd on the
     # cached H with the GLOBAL pixel count as the trace term (gcv_function.m:46-50; bench.py c3gcv),
     # and the one-call gcv_function (the library all-reduces n itself)
@@ -146,5 +152,36 @@ def solve_all(ctx, rank, world):
     return res
 
 
+def solve_c4(ctx, rank, world):
+    """BASELINE configs[3] and [4] at full size, cut exactly as bench.py build_shard cuts them
+    (device-generated 4096^2 / 47-angle operator, 4 x 4-tiled, whole tile columns of stored
+    pixels, B_g = row slice of A', A_g its transpose, 64-column bands), with the fixture's b
+    (tests/golden/c4_4096.npz) in place of the device-formed one:
+    * ABgmres_nonhybrid_bounds, 20 iterations, fp64 (the one pass per shard + the m-vector
+      all-reduce; test_gpu_fullsize.py::test_c4_sharded_two_ranks_vs_oracle);
+    * lsqr_solver / lsmr_solver on the fp32 shards, 5 iterations."""
+    import bench
+    from conftest import load_golden
+    g = load_golden("c4_4096.npz")
+    b = np.ascontiguousarray(g["b"])
+    res = {}
+    for wl, tag in (("c4", "abn"), ("c5", "f32")):
+        A_g, B_g, _, xs, (lo, hi), full = bench.build_shard(ctx, bench.WORKLOADS[wl], rank, world)
+        xt = np.ascontiguousarray(xs[lo:hi])
+        if tag == "abn":
+            out_ = hgmres.ABgmres_nonhybrid_bounds(A_g, B_g, b, xt, 0.0, 20, ctx=ctx, return_H=True)
+            res.update(abn_x=out_[0], abn_err=out_[1], abn_res=out_[2], abn_k=out_[3], abn_H=out_[-1])
+        else:
+            x, e, r, k = hgmres.lsqr_solver(A_g, b, xt, 0.0, 5, ctx=ctx, At=B_g)
+            res.update(lsqr32_x=x, lsqr32_err=e, lsqr32_res=r, lsqr32_k=k)
+            x, e, r, a, k = hgmres.lsmr_solver(A_g, b, xt, 0.0, 5, ctx=ctx, At=B_g)
+            res.update(lsmr32_x=x, lsmr32_err=e, lsmr32_res=r, lsmr32_ar=a, lsmr32_k=k)
+        res.update({f"{tag}_lo": lo, f"{tag}_hi": hi})
+        A_g.close()
+        B_g.close()
+    return res
+
+
 if __name__ == "__main__":
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
     main()

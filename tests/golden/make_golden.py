@@ -135,6 +135,29 @@ def dump_c4(name="c4_4096.npz", k=20):
          "abn_xs": x[::997].copy()}
     np.savez_compressed(os.path.join(OUT, name), **d)
     print("wrote", name, "k", kk, "res", res[-1], "err", err[-1])
+
+
+def dump_c2(name="c2_512.npz", k=20):
+    """BASELINE configs[1] at full size and at the bench's count (bench.py WORKLOADS["c2"]):
+    hybrid_ab_gmres_rtp (hybrid_ab_gmres_rtp.m:1-43), 512^2, 30 angles, nnz 1.0e7, lambda 1e-2,
+    all 20 iterations (the reference re-forms A*Qk each iteration, :28-36: 210 host SpMVs).
+    Inputs: b stored (the host's A*x_true + 1 % noise, numpy default_rng(0)); A and B = A' pinned
+    by the sha256 of their CSR in reference pixel order.  Outputs: H (21 x 20), both histories,
+    x as its norm plus every 97th entry."""
+    from oracle import parallel as OP
+    P = tomo_problem(512, 30, noise=1e-2, seed=0, backprojector="matched")
+    A, B, b, xt = P.A, P.B, P.b, P.x_true
+    OP.build()
+    PA, PB = OP.ParallelCSR(A), OP.ParallelCSR(B)
+    x, e, r, kk, H = R.hybrid_ab_gmres_rtp(PA, PB, b, xt, 0.0, k, 1e-2, return_H=True)
+    st = 97
+    d = {"maxit": k, "lam": 1e-2, "N": 512, "n_angles": 30, "A_sha256": csr_hash(A), "B_sha256": csr_hash(B),
+         "b": b, "sample_stride": st, "hab_H": H, "hab_err": e, "hab_res": r, "hab_k": kk,
+         "hab_xnorm": np.linalg.norm(x), "hab_xs": x[::st].copy()}
+    np.savez_compressed(os.path.join(OUT, name), **d)
+    print("wrote", name, "k", kk, "res", r[-1], "err", e[-1])
+
+
 def dump_shaw_pipeline(name="shaw32_pipeline.npz"):
     """analyze_regularization.m on shaw(32) (restated, hgmres.regtools) with numpy noise and
     mismatch (MATLAB's randn stream cannot be reproduced): inputs, the oracle's outputs in the
@@ -167,6 +190,9 @@ def dump_shaw_pipeline(name="shaw32_pipeline.npz"):
 if __name__ == "__main__":
     if sys.argv[1:] == ["c3"]:
         dump_c3()
+        sys.exit(0)
+    if sys.argv[1:] == ["c2"]:
+        dump_c2()
         sys.exit(0)
     if sys.argv[1:] == ["c4"]:
         dump_c4()

@@ -61,6 +61,46 @@ def _csr_hash(M):
 
 
 # ---------------------------------------------------------------------------------------
+# C2
+# ---------------------------------------------------------------------------------------
+def test_c2_hybrid_ab_gmres_rtp_full_size(gpu_ctx):
+    """configs[1] at the bench's count (bench.py WORKLOADS["c2"]): hybrid_ab_gmres_rtp, 512^2 /
+    30 angles, lambda 1e-2, all 20 iterations of the production path against the oracle fixture
+    tests/golden/c2_512.npz (make_golden.py c2).  Two hand-overs: the bench's (device-generated
+    4 x 4-tiled A, B its device transpose) and the reference-order host CSR upload."""
+    from hgmres.problems import siddon_projector
+    g = load_golden("c2_512.npz")
+    k, lam, st = int(g["maxit"]), float(g["lam"]), int(g["sample_stride"])
+    assert k == 20
+    b = g["b"]
+    xt = shepp_logan(512).ravel(order="F")
+    A = hgmres.SparseOperator.siddon(512, 30, ctx=gpu_ctx)            # tiled pixel order (bench)
+    B = A.T
+    assert _csr_hash(A.to_scipy()) == str(g["A_sha256"])
+    assert _csr_hash(B.to_scipy()) == str(g["B_sha256"])
+    As = siddon_projector(512, 30)
+    Bs = As.T.tocsr()
+    Bs.sort_indices()
+    Ah = hgmres.SparseOperator.from_scipy(As, gpu_ctx)                # reference order (host CSR)
+    Bh = hgmres.SparseOperator.from_scipy(Bs, gpu_ctx)
+    for tag, (Ao, Bo) in (("tiled", (A, B)), ("host", (Ah, Bh))):
+        x, e, r, kk, H = hgmres.hybrid_ab_gmres_rtp(Ao, Bo, b, xt, 0.0, k, lam, ctx=gpu_ctx, return_H=True)
+        dH = H_rel(H, g["hab_H"])
+        per_it = np.maximum(np.abs(r - g["hab_res"]) / g["hab_res"], np.abs(e - g["hab_err"]) / g["hab_err"])
+        print(f"[c2 hab {tag} k={kk}] |dH|/|H|={dH:.2e} |dx_s|={rel(x[::st], g['hab_xs']):.2e} "
+              f"per-iteration history deviation {' '.join(f'{v:.0e}' for v in per_it)}")
+        assert kk == int(g["hab_k"]) == k
+        assert dH <= TOL, (tag, dH)
+        hist_ok(e, g["hab_err"])
+        hist_ok(r, g["hab_res"])
+        assert abs(np.linalg.norm(x) - float(g["hab_xnorm"])) <= TOL * float(g["hab_xnorm"])
+        assert rel(x[::st], g["hab_xs"]) <= TOL
+    for M in (A, B, Ah, Bh):
+        M.close()
+    gc.collect()
+
+
+# ---------------------------------------------------------------------------------------
 # C3
 # ---------------------------------------------------------------------------------------
 def _solve_ok(tag, x, e, r, kk, H, g, st):
@@ -169,6 +209,85 @@ def test_c4_ab_gmres_full_size(gpu_ctx):
     A.close()
     B.close()
     gc.collect()
+
+
+def test_c4_sharded_two_ranks_vs_oracle(tmp_path):
+    """configs[3] as the N-GPU bench runs it, at full size: two pixel shards cut as bench.py
+    build_shard cuts them (whole tile columns of the 4 x 4-tiled stored order, 64-column bands,
+    the one pass A_g*(B_g*q) per shard with its own plan over the shard's N x W window, one
+    m-vector all-reduce per step), run as two processes on this one GPU with the cross-rank
+    sums through the library's host all-reduce hook (the RCCL code path with another
+    transport; RCCL refuses two ranks on one device).  AB-GMRES (ABgmres_nonhybrid_bounds.m:24-40)
+    through the bench's 20 iterations against tests/golden/c4_4096.npz at the north_star bar:
+    H, both histories, x (reassembled from the shards, mapped to reference order).
+    configs[4] likewise: LSQR / LSMR on the fp32 shards, 5 iterations, against the fp32 oracle
+    (oracle/restatement.py lsqr_solver_f32 / lsmr_solver_f32 on the downloaded fp32 operator)
+    within the fp32 envelope of test_c5_fp32_vs_fp32_oracle_full_size."""
+    import os
+    import subprocess
+    import sys
+    import scipy.sparse as sp
+    from hgmres.core import auto_pixel_order, stored_pixel_index
+    from oracle import parallel as OP
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    worker = os.path.join(root, "tests", "_shard_worker.py")
+    port = 31000 + (os.getpid() % 2000)
+    procs = [subprocess.Popen([sys.executable, worker, str(r), "2", str(port), str(tmp_path), "c4"])
+             for r in range(2)]
+    rcs = [p.wait(timeout=900) for p in procs]
+    assert rcs == [0, 0]
+    o = [dict(np.load(os.path.join(tmp_path, f"rank{r}_of2.npz"))) for r in range(2)]
+    g = load_golden("c4_4096.npz")
+    st = int(g["sample_stride"])
+    tile, sup = auto_pixel_order(4096)
+    perm = stored_pixel_index(4096, tile, sup)       # reference pixel -> stored position
+    assert int(o[0]["abn_lo"]) == 0 and int(o[0]["abn_hi"]) == int(o[1]["abn_lo"])
+    x = np.concatenate([o[0]["abn_x"], o[1]["abn_x"]])[perm]
+    H, e, r = o[0]["abn_H"], o[0]["abn_err"], o[0]["abn_res"]
+    dH = H_rel(H, g["abn_H"])
+    print(f"[c4 sharded 2 ranks k={int(o[0]['abn_k'])}] |dH|/|H|={dH:.2e} |dx_s|={rel(x[::st], g['abn_xs']):.2e} "
+          f"res dev {float(np.max(np.abs(r - g['abn_res']) / g['abn_res'])):.2e} "
+          f"err dev {float(np.max(np.abs(e - g['abn_err']) / g['abn_err'])):.2e}")
+    assert int(o[0]["abn_k"]) == int(o[1]["abn_k"]) == 20
+    for k_ in ("abn_H", "abn_err", "abn_res"):            # replicated outputs agree bitwise
+        assert np.array_equal(o[0][k_], o[1][k_]), k_
+    assert dH <= TOL, dH
+    hist_ok(e, g["abn_err"])
+    hist_ok(r, g["abn_res"])
+    assert abs(np.linalg.norm(x) - float(g["abn_xnorm"])) <= TOL * float(g["abn_xnorm"])
+    assert rel(x[::st], g["abn_xs"]) <= TOL
+    # configs[4]: the fp32 shards against the fp32 oracle on the same fp32 operator
+    ctx = hgmres.default_context()
+    Ar = hgmres.SparseOperator.siddon(4096, 47, ctx=ctx, dtype=L.HGM_F32, order="reference")
+    As = Ar.to_scipy()
+    Ar.close()
+    A32 = sp.csr_matrix((As.data.astype(np.float32), As.indices, As.indptr), shape=As.shape)
+    del As
+    gc.collect()
+    OP.build()
+    PA = OP.ParallelCSR(A32)
+    del A32
+    gc.collect()
+    b = g["b"]
+    xt = shepp_logan(4096).ravel(order="F")
+    K = 5
+    refs = {"lsqr32": R.lsqr_solver_f32(PA, b, xt, 0.0, K), "lsmr32": R.lsmr_solver_f32(PA, b, xt, 0.0, K)}
+    del PA
+    gc.collect()
+    for tag, ref in refs.items():
+        nh = 2 if tag == "lsqr32" else 3
+        xs = np.concatenate([o[0][f"{tag}_x"], o[1][f"{tag}_x"]])[perm]
+        hs = [o[0][f"{tag}_err"], o[0][f"{tag}_res"]] + ([o[0]["lsmr32_ar"]] if nh == 3 else [])
+        for r_ in range(2):
+            assert np.array_equal(o[r_][f"{tag}_res"], o[0][f"{tag}_res"])
+        per_it = np.max([np.abs(hs[i] - ref[1 + i]) / np.abs(ref[1 + i]) for i in range(nh)], axis=0)
+        dx = rel(xs, ref[0].astype(np.float64))
+        print(f"[c5 sharded {tag} k={K}] vs fp32 oracle: x {dx:.2e}, per-iteration max history deviation "
+              f"{' '.join(f'{d:.0e}' for d in per_it)}")
+        assert int(o[0][f"{tag}_k"]) == ref[-1] == K
+        for j in range(1, K + 1):
+            assert per_it[j - 1] <= _c5_envelope(j), (tag, j, per_it[j - 1])
+        assert dx <= 5e-3, (tag, dx)
 
 
 # ---------------------------------------------------------------------------------------

@@ -298,6 +298,52 @@ def test_lsmr_device_scalars_match_host_loop(gpu_ctx, dtype):
         assert rel(sd[0], sh[0]) <= bar
 
 
+@pytest.mark.parametrize("dtype", [None, "f32"])
+def test_lsqr_one_pass_scalars_and_tol_stop(gpu_ctx, dtype):
+    """lsqr_solver's one-pass path: device-resident scalars (k_lsqr_rot, the stop test
+    lsqr_solver.m:44-46 on the device, read once per batch of 8) against the same pass with host
+    scalars (lsqr_dev = 0: beta^2 / alpha^2 read back, the rotation :31-38 on the host) -- the same
+    double arithmetic, so the same bits up to sqrt; with tol between two residuals both stop at
+    the same iteration inside the first batch, with the iterations enqueued past the stop leaving
+    x and w as they were; against the two-pass solve and (fp64) the oracle, niters equal and the
+    histories at 1e-10 (fp32: the fp32 envelope, 1e-5, against the fp32 restatement)."""
+    A, At, b, xt = _gkb_pair(gpu_ctx, 256, 47, dtype=dtype)
+    bar = 1e-12 if dtype is None else 1e-5
+    with gpu_ctx.options(fused_ab=1):
+        hgmres.fused_plan_info(A, At)                  # the one pass is taken
+        full = {}
+        for dev_ in (1, 0):
+            with gpu_ctx.options(lsqr_dev=dev_):
+                full[dev_] = hgmres.lsqr_solver(A, b, xt, 0.0, 12, ctx=gpu_ctx, At=At)
+    d, h = full[1], full[0]
+    assert d[3] == h[3] == 12
+    for i in (1, 2):
+        assert hist_dev(d[i], h[i]) <= bar, i
+    assert rel(d[0], h[0]) <= bar
+    res = np.asarray(h[2])
+    tol = 0.5 * (res[4] + res[5])                      # :46 (<=) stops at iteration 6 (1-based)
+    assert res[5] <= tol < res[4]
+    stopped = {}
+    with gpu_ctx.options(fused_ab=1):
+        for dev_ in (1, 0):
+            with gpu_ctx.options(lsqr_dev=dev_):
+                stopped[dev_] = hgmres.lsqr_solver(A, b, xt, tol, 12, ctx=gpu_ctx, At=At)
+    with gpu_ctx.options(fused_ab=0):
+        two = hgmres.lsqr_solver(A, b, xt, tol, 12, ctx=gpu_ctx, At=At)
+    As = A.to_scipy()
+    ref = (R.lsqr_solver(As, b, xt, tol, 12) if dtype is None else R.lsqr_solver_f32(As, b, xt, tol, 12))
+    sd, sh = stopped[1], stopped[0]
+    assert sd[3] == sh[3] == two[3] == ref[3] == 6
+    devs = dict(dev_vs_host=max(hist_dev(sd[1], sh[1]), hist_dev(sd[2], sh[2]), rel(sd[0], sh[0])),
+                vs_two_pass=max(hist_dev(sd[1], two[1]), hist_dev(sd[2], two[2]), rel(sd[0], two[0])),
+                vs_oracle=max(hist_dev(sd[1], ref[1]), hist_dev(sd[2], ref[2]), rel(sd[0], ref[0])))
+    print(f"[lsqr one pass tol stop {dtype or 'f64'}] k={sd[3]} " + " ".join(f"{a}={v:.1e}" for a, v in devs.items()))
+    assert devs["dev_vs_host"] <= bar
+    # fp32: iterations 5-6 are past the fp32 envelope's 1e-5 (DESIGN.md §6: 1e-3 from iteration 5)
+    assert devs["vs_two_pass"] <= (TOL if dtype is None else 1e-3)
+    assert devs["vs_oracle"] <= (TOL if dtype is None else 1e-3)
+
+
 def test_fused_spmv_ab_fp32(gpu_ctx):
     """hgm_spmv_ab on an fp32 pair runs the fp32 one-pass kernel: within fp32 rounding of the
     two-pass product, bitwise repeatable."""

@@ -988,6 +988,15 @@ def test_shard_emulation_two_ranks(tmp_path):
     import scipy.optimize as so
     from hgmres import _lib as L
     P = tomo_problem(64, 90, noise=1e-2, seed=0)
+    # the one-pass LSQR with a tol stop on the tiled shards (device scalars, batch of 8): the
+    # oracle's iteration count and histories at that tol
+    tol = float(o[0]["tlsqrtol_tol"])
+    assert tol == float(o[1]["tlsqrtol_tol"])
+    xo, eo, ro, ko = R.lsqr_solver(P.A, P.b, P.x_true, tol, 12)
+    assert int(o[0]["tlsqrtol_k"]) == int(o[1]["tlsqrtol_k"]) == ko == 6
+    hist_ok(o[0]["tlsqrtol_res"], ro, TOL)
+    hist_ok(o[0]["tlsqrtol_err"], eo, TOL)
+    assert rel(np.concatenate([o[0]["tlsqrtol_x"], o[1]["tlsqrtol_x"]])[perm], xo) < TOL
     # sharded GCV (configs[2]): H of the sharded Arnoldi, the GCV lambda with the global trace n
     Ho, beta_o = R.arnoldi(P.A, P.B, P.b, 20, "ba")
     H_ok(o[0]["gcv_H"], Ho)
