@@ -741,6 +741,18 @@ HGM_API int hgm_mat_create_siddon_ordered(hgm_ctx* c, int N, int n_angles, doubl
     return HGM_OK;
 }
 
+HGM_API int hgm_mat_create_fanbeam(hgm_ctx* c, int N, int n_angles, double R, double span, double det_offset,
+                                   int dtype, int tile, int super_block, hgm_mat** out) {
+    if (!c || !out) return HGM_E_ARG;
+    *out = nullptr;
+    HGM_TRY(c, {
+        HGM_HIP(hipSetDevice(c->device));
+        *out = fanbeam(c, N, n_angles, R, span, det_offset, dtype, tile, super_block);
+        finalize_operator(c, *out);
+    });
+    return HGM_OK;
+}
+
 HGM_API int hgm_mat_create_backprojector(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype, int tile,
                                          int super_block, hgm_mat** out) {
     if (!c || !out) return HGM_E_ARG;

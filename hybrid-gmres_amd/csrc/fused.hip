@@ -1504,8 +1504,22 @@ const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
     }
     if (!Bm->fused && Bm->fused_failed_key != key) {   // (a refused tuple is not re-planned)
         try {
-            Bm->fused = rw ? fused_plan_build_rw(c, B, nu.fused_wregion, nu.fused_waves, nu.fused_group)
-                           : fused_plan_build(c, B, nu.fused_region);
+            if (rw) {
+                // a region crossed by more rays than the LDS holds (many angles: the fan-beam
+                // geometry over a full turn, ~7,400 rays per 32 x 32 region at 180 angles) is
+                // retried with regions of half the side (about half the rays) before the pair
+                // falls back to the two-pass path
+                for (int R = nu.fused_wregion;; R /= 2) {
+                    try {
+                        Bm->fused = fused_plan_build_rw(c, B, R, nu.fused_waves, nu.fused_group);
+                        break;
+                    } catch (const Error& e) {
+                        if (e.code != HGM_E_ARG || R / 2 < 16 || R % 2) throw;
+                    }
+                }
+            } else {
+                Bm->fused = fused_plan_build(c, B, nu.fused_region);
+            }
             Bm->fused_key = key;
             Bm->fused_failed_key = -1;
         } catch (const Error& e) {

@@ -441,6 +441,8 @@ void free_page_index(hgm_mat* M);
 void finalize_operator(hgm_ctx* c, hgm_mat* M);
 int64_t auto_band_width(const hgm_mat* M);
 hgm_mat* siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype, int tile = 1, int super = 0);
+hgm_mat* fanbeam(hgm_ctx* c, int N, int n_angles, double R, double span, double det_offset, int dtype, int tile = 1,
+                 int super = 0);
 hgm_mat* backprojector(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype, int tile = 1, int super = 0);
 // n-vector between the reference order and a pixel order o: dir 0: out[stored(p)] = in[p]
 // (reference -> stored), dir 1: out[p] = in[stored(p)] (stored -> reference)

@@ -588,13 +588,14 @@ struct RayGeom {
     bool cx, cy, hit;
 };
 
-__device__ __forceinline__ RayGeom ray_geom(int N, double c, double s_, double sd) {
+// a ray x(t) = (x0, y0) + t (c, s_) (unit direction; hgmres/problems.py::_siddon_rays)
+__device__ __forceinline__ RayGeom ray_geom_xy(int N, double x0, double y0, double c, double s_) {
     RayGeom g;
     const double half = N / 2.0;
     g.c = c;
     g.s = s_;
-    g.x0 = -sd * s_;
-    g.y0 = sd * c;
+    g.x0 = x0;
+    g.y0 = y0;
     g.cx = fabs(c) > 1e-12;
     g.cy = fabs(s_) > 1e-12;
     const double inf = INFINITY;
@@ -617,6 +618,10 @@ __device__ __forceinline__ RayGeom ray_geom(int N, double c, double s_, double s
     g.tmax = fmin(txmax, tymax);
     g.hit = g.tmin < g.tmax;
     return g;
+}
+// parallel ray at signed detector offset sd (_siddon_chunk: x0 = -s sin, y0 = s cos)
+__device__ __forceinline__ RayGeom ray_geom(int N, double c, double s_, double sd) {
+    return ray_geom_xy(N, -sd * s_, sd * c, c, s_);
 }
 
 // Walk the merged, sorted crossing sequence [tmin, x/y-plane crossings in range, tmax]
@@ -768,6 +773,28 @@ __global__ __launch_bounds__(BS) void k_siddon(int N, int p, int64_t m, const do
     for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < m; r += (int64_t)gridDim.x * BS) {
         const int a = (int)(r / p), d = (int)(r % p);
         const RayGeom g = ray_geom(N, cth[a], sth[a], sdet[d]);
+        if (FILL) siddon_walk<true, T>(N, g, rp[r], ci, val, tile, super);
+        else counts[r] = siddon_walk<false, T>(N, g, 0, nullptr, nullptr);
+    }
+}
+
+// Fan-beam, curved (equiangular) detector (hgmres/problems.py::fan_geometry; the CTtype
+// 'fancurved' of run_2D_phantom.m:12-13): ray r = a*p + d leaves the source D (cos b_a, sin b_a)
+// towards the centre rotated by omega_d, u = -(cos(b+w), sin(b+w)) by the angle-addition formula
+// from the host's libm cos / sin of b_a and omega_d (no FMA: -ffp-contract=off), so the rays
+// are bitwise those of the numpy twin.
+template <bool FILL, typename T>
+__global__ __launch_bounds__(BS) void k_fanbeam(int N, int p, int64_t m, double D, const double* __restrict__ cb,
+                                                const double* __restrict__ sb, const double* __restrict__ co,
+                                                const double* __restrict__ so, int64_t* __restrict__ counts,
+                                                const int64_t* __restrict__ rp, int32_t* __restrict__ ci,
+                                                T* __restrict__ val, int tile, int super) {
+    for (int64_t r = (int64_t)blockIdx.x * BS + threadIdx.x; r < m; r += (int64_t)gridDim.x * BS) {
+        const int a = (int)(r / p), d = (int)(r % p);
+        const double x0 = D * cb[a], y0 = D * sb[a];
+        const double ux = -(cb[a] * co[d] - sb[a] * so[d]);
+        const double uy = -(sb[a] * co[d] + cb[a] * so[d]);
+        const RayGeom g = ray_geom_xy(N, x0, y0, ux, uy);
         if (FILL) siddon_walk<true, T>(N, g, rp[r], ci, val, tile, super);
         else counts[r] = siddon_walk<false, T>(N, g, 0, nullptr, nullptr);
     }
@@ -934,6 +961,81 @@ hgm_mat* siddon(hgm_ctx* c, int N, int n_angles, double det_offset, int dtype, i
         throw;
     }
     (void)hipFree(dc); (void)hipFree(ds); (void)hipFree(dd); (void)hipFree(counts); (void)hipFree(rp); (void)hipFree(tmp);
+    return M;
+}
+
+hgm_mat* fanbeam(hgm_ctx* c, int N, int n_angles, double R, double span, double det_offset, int dtype, int tile,
+                 int super) {
+    HGM_REQUIRE(N > 0 && n_angles > 0, "fanbeam: N and n_angles must be positive");
+    HGM_REQUIRE(R > 1.0 / std::sqrt(2.0), "fanbeam: the source must lie outside the image (R > 1/sqrt(2))");
+    if (tile < 1) tile = 1;
+    if (super < 2) super = 0;
+    HGM_REQUIRE(N % tile == 0 && (super == 0 || (N % super == 0 && super % tile == 0)),
+                "fanbeam: tile must divide N (and super), super must divide N");
+    if (!(span > 0)) span = 2.0 * std::asin(1.0 / (std::sqrt(2.0) * R));
+    HGM_REQUIRE(span < M_PI, "fanbeam: span must be below pi");
+    hipStream_t st = c->stream;
+    const int p = (int)std::ceil(std::sqrt(2.0) * N);
+    const int64_t m = (int64_t)p * n_angles;
+    const double D = R * N, dom = span / p;
+    // geometry on the host with C libm (problems.py fan_geometry: math.cos / math.sin, same libm)
+    std::vector<double> cb(n_angles), sb(n_angles), co(p), so(p);
+    for (int a = 0; a < n_angles; ++a) {
+        const double b = a * (2.0 * M_PI / n_angles);
+        cb[a] = std::cos(b);
+        sb[a] = std::sin(b);
+    }
+    for (int d = 0; d < p; ++d) {
+        const double w = (((double)d - (p - 1) / 2.0) + det_offset) * dom;
+        co[d] = std::cos(w);
+        so[d] = std::sin(w);
+    }
+    double* geo = nullptr;
+    int64_t *counts = nullptr, *rp = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    hgm_mat* M = nullptr;
+    auto release = [&]() {
+        (void)hipFree(geo); (void)hipFree(counts); (void)hipFree(rp); (void)hipFree(tmp);
+    };
+    try {
+        HGM_HIP(hipMalloc(&geo, 8 * (2 * (size_t)n_angles + 2 * (size_t)p)));
+        double *dcb = geo, *dsb = geo + n_angles, *dco = geo + 2 * n_angles, *dso = geo + 2 * n_angles + p;
+        HGM_HIP(hipMalloc(&counts, 8 * (m + 1)));
+        HGM_HIP(hipMalloc(&rp, 8 * (m + 1)));
+        HGM_HIP(hipMemcpyAsync(dcb, cb.data(), 8 * n_angles, hipMemcpyHostToDevice, st));
+        HGM_HIP(hipMemcpyAsync(dsb, sb.data(), 8 * n_angles, hipMemcpyHostToDevice, st));
+        HGM_HIP(hipMemcpyAsync(dco, co.data(), 8 * p, hipMemcpyHostToDevice, st));
+        HGM_HIP(hipMemcpyAsync(dso, so.data(), 8 * p, hipMemcpyHostToDevice, st));
+        HGM_HIP(hipMemsetAsync(counts, 0, 8 * (m + 1), st));
+        const int g = grid_cap(m);
+        k_fanbeam<false, double><<<g, BS, 0, st>>>(N, p, m, D, dcb, dsb, dco, dso, counts, nullptr, nullptr, nullptr,
+                                                   1, 0);
+        HGM_HIP(hipGetLastError());
+        HGM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, rp, (int)(m + 1), st));
+        HGM_HIP(hipMalloc(&tmp, tmp_bytes));
+        HGM_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, counts, rp, (int)(m + 1), st));
+        int64_t nnz = 0;
+        HGM_HIP(hipMemcpyAsync(&nnz, rp + m, 8, hipMemcpyDeviceToHost, st));
+        HGM_HIP(hipStreamSynchronize(st));
+        HGM_REQUIRE(nnz < (int64_t)INT32_MAX * 2, "fanbeam: nnz overflow");
+        M = mat_alloc(c, m, (int64_t)N * N, nnz, dtype);
+        HGM_HIP(hipMemcpyAsync(M->rp, rp, 8 * (m + 1), hipMemcpyDeviceToDevice, st));
+        if (tile > 1 || super > 1) M->col_order = PixOrder{N, tile, super};
+        if (dtype == HGM_F32)
+            k_fanbeam<true, float><<<g, BS, 0, st>>>(N, p, m, D, dcb, dsb, dco, dso, nullptr, M->rp, M->ci,
+                                                     (float*)M->val, tile, super);
+        else
+            k_fanbeam<true, double><<<g, BS, 0, st>>>(N, p, m, D, dcb, dsb, dco, dso, nullptr, M->rp, M->ci,
+                                                      (double*)M->val, tile, super);
+        HGM_HIP(hipGetLastError());
+        HGM_HIP(hipStreamSynchronize(st));
+    } catch (...) {
+        release();
+        mat_free(M);
+        throw;
+    }
+    release();
     return M;
 }
 

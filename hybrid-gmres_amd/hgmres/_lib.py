@@ -68,6 +68,8 @@ _SIGS = {
     "hgm_mat_create_siddon": (c_int, [c_void_p, c_int, c_int, c_double, c_int, P(c_void_p)]),
     "hgm_mat_create_siddon_ordered": (c_int, [c_void_p, c_int, c_int, c_double, c_int, c_int, c_int,
                                               P(c_void_p)]),
+    "hgm_mat_create_fanbeam": (c_int, [c_void_p, c_int, c_int, c_double, c_double, c_double, c_int, c_int, c_int,
+                                       P(c_void_p)]),
     "hgm_mat_order": (c_int, [c_void_p, c_int, P(c_int), P(c_int), P(c_int)]),
     "hgm_mat_create_backprojector": (c_int, [c_void_p, c_int, c_int, c_double, c_int, c_int, c_int, P(c_void_p)]),
     "hgm_mat_row_slice": (c_int, [c_void_p, c_void_p, c_int64, c_int64, P(c_void_p)]),

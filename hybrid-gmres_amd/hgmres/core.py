@@ -258,6 +258,23 @@ class SparseOperator:
         return cls._wrap(ctx, h)
 
     @classmethod
+    def fanbeam(cls, N, n_angles, ctx: Context | None = None, R=None, span=None, dtype=L.HGM_F64, det_offset=None,
+                order="auto"):
+        """Fan-beam (curved detector) projector generated on the device, bit-identical to
+        :func:`hgmres.problems.fanbeam_projector` (the 'fancurved' geometry of
+        run_2D_phantom.m:12-13).  ``span=None``: the fan covering the image's circumscribed
+        circle; ``order`` as for :meth:`siddon`."""
+        from .problems import DETECTOR_OFFSET, FAN_R
+        ctx = ctx or default_context()
+        off = DETECTOR_OFFSET if det_offset is None else det_offset
+        tile, sup = auto_pixel_order(N) if order == "auto" else ((1, 0) if order == "reference" else order)
+        h = C.c_void_p()
+        _check(L.load().hgm_mat_create_fanbeam(ctx.handle, N, n_angles, float(FAN_R if R is None else R),
+                                               float(0.0 if span is None else span), off, dtype, int(tile), int(sup),
+                                               C.byref(h)), ctx)
+        return cls._wrap(ctx, h)
+
+    @classmethod
     def pixel_backprojector(cls, N, n_angles, ctx: Context | None = None, dtype=L.HGM_F64, det_offset=None,
                             order="auto"):
         """Unmatched pixel-driven back-projector B (n x m) generated on the device, bit-identical

@@ -50,12 +50,18 @@ def geometry(N: int, n_angles: int):
 
 
 def _siddon_chunk(N, cos_t, sin_t, s):
-    """Siddon ray tracing for a chunk of rays.  Returns (counts, cols, vals)
-    with the entries of each ray ordered along the ray (increasing t)."""
+    """Siddon ray tracing for a chunk of parallel rays (direction (cos_t, sin_t), signed
+    detector offset s from the centre).  Returns (counts, cols, vals) with the entries of each
+    ray ordered along the ray (increasing t)."""
+    return _siddon_rays(N, -s * sin_t, s * cos_t, cos_t, sin_t)
+
+
+def _siddon_rays(N, x0, y0, cos_t, sin_t):
+    """Siddon ray tracing for a chunk of rays x(t) = (x0, y0) + t (cos_t, sin_t) (unit direction)
+    over the N x N grid of unit pixels centred on the origin.  Returns (counts, cols, vals)
+    with the entries of each ray ordered along the ray (increasing t).  Mirrored by the device
+    generators' ray_geom / siddon_walk (csrc/ops.hip)."""
     half = N / 2.0
-    R = s.shape[0]
-    x0 = -s * sin_t
-    y0 = s * cos_t
     grid = np.arange(N + 1, dtype=np.float64) - half
     eps = 1e-12
     cx = np.abs(cos_t) > eps
@@ -116,6 +122,68 @@ def siddon_projector(N: int, n_angles: int, chunk_elems: int = 1 << 24) -> sp.cs
         cols_all.append(col)
         vals_all.append(val)
         ray = r1
+    counts = np.concatenate(counts_all)
+    indptr = np.zeros(m + 1, dtype=np.int64)
+    np.cumsum(counts, out=indptr[1:])
+    A = sp.csr_matrix((np.concatenate(vals_all), np.concatenate(cols_all), indptr), shape=(m, N * N))
+    A.has_sorted_indices = False
+    return A
+
+
+FAN_R = 2.0          # source-to-centre distance in units of N (AIR Tools II fanbeamtomo's default R)
+
+
+def fan_geometry(N: int, n_angles: int, R: float = FAN_R, span: float | None = None,
+                 det_offset: float = DETECTOR_OFFSET):
+    """Fan-beam, curved (equiangular) detector geometry -- the CTtype 'fancurved' of
+    run_2D_phantom.m:12-13 (PRtomo_mismatched, not vendored by the reference: its exact
+    parameters are unknown, so this follows the published AIR Tools II fanbeamtomo conventions):
+    * source angles beta_a = a * 2 pi / n_angles (a full turn), the source at distance D = R N
+      from the centre, S_a = D (cos beta_a, sin beta_a);
+    * p = ceil(sqrt(2) N) rays per source position at fan angles
+      omega_d = ((d - (p-1)/2) + det_offset) * span / p, d = 0..p-1 (equiangular bins: a curved
+      detector on an arc around the source);
+    * span (radians) defaults to the fan that just covers the image's circumscribed circle,
+      2 asin(1 / (sqrt(2) R));
+    * ray (a, d) leaves S_a towards the centre rotated by omega_d: direction
+      u = -(cos(beta + omega), sin(beta + omega)), formed by the angle-addition formula from the
+      C-libm cos / sin of beta and omega (the same IEEE operations on the host and the device).
+    Row index a * p + d (source-angle-major, as the parallel geometry).  Returns
+    (p, x0, y0, ux, uy) per ray."""
+    p = int(math.ceil(math.sqrt(2.0) * N))
+    if span is None:
+        span = 2.0 * math.asin(1.0 / (math.sqrt(2.0) * R))
+    D = R * N
+    dom = span / p
+    cb = np.array([math.cos(a * (2.0 * math.pi / n_angles)) for a in range(n_angles)])
+    sb = np.array([math.sin(a * (2.0 * math.pi / n_angles)) for a in range(n_angles)])
+    om = [((d - (p - 1) / 2.0) + det_offset) * dom for d in range(p)]
+    co = np.array([math.cos(w) for w in om])
+    so = np.array([math.sin(w) for w in om])
+    cbr, sbr = np.repeat(cb, p), np.repeat(sb, p)
+    cor, sor = np.tile(co, n_angles), np.tile(so, n_angles)
+    x0 = D * cbr
+    y0 = D * sbr
+    ux = -(cbr * cor - sbr * sor)
+    uy = -(sbr * cor + cbr * sor)
+    return p, x0, y0, ux, uy
+
+
+def fanbeam_projector(N: int, n_angles: int, R: float = FAN_R, span: float | None = None,
+                      det_offset: float = DETECTOR_OFFSET, chunk_elems: int = 1 << 24) -> sp.csr_matrix:
+    """Ray-major CSR of the fan-beam (curved detector) line-integral operator (fan_geometry),
+    entries of each row in along-ray order; bit-identical to the device generator
+    ``hgm_mat_create_fanbeam``."""
+    p, x0, y0, ux, uy = fan_geometry(N, n_angles, R, span, det_offset)
+    m = p * n_angles
+    rays_per_chunk = max(1, chunk_elems // (2 * N + 4))
+    counts_all, cols_all, vals_all = [], [], []
+    for r0 in range(0, m, rays_per_chunk):
+        sl = slice(r0, min(m, r0 + rays_per_chunk))
+        cnt, col, val = _siddon_rays(N, x0[sl], y0[sl], ux[sl], uy[sl])
+        counts_all.append(cnt)
+        cols_all.append(col)
+        vals_all.append(val)
     counts = np.concatenate(counts_all)
     indptr = np.zeros(m + 1, dtype=np.int64)
     np.cumsum(counts, out=indptr[1:])
@@ -203,10 +271,19 @@ class TomoProblem:
 
 
 def tomo_problem(N: int, n_angles: int, noise: float = 1e-2, seed: int = 0,
-                 backprojector: str = "matched") -> TomoProblem:
+                 backprojector: str = "matched", geometry_kind: str = "parallel") -> TomoProblem:
     """Build (A, B, b, x_true).  ``backprojector`` is ``"matched"`` (B = A^T)
-    or ``"pixel"`` (unmatched pixel-driven B)."""
-    A = siddon_projector(N, n_angles)
+    or ``"pixel"`` (unmatched pixel-driven B, parallel beam only).  ``geometry_kind``:
+    ``"parallel"`` (Siddon, angles over [0, pi)) or ``"fan"`` (curved-detector fan beam over a
+    full turn, :func:`fan_geometry`)."""
+    if geometry_kind == "fan":
+        if backprojector != "matched":
+            raise ValueError("the fan-beam geometry pairs with the matched back-projector only")
+        A = fanbeam_projector(N, n_angles)
+    elif geometry_kind == "parallel":
+        A = siddon_projector(N, n_angles)
+    else:
+        raise ValueError("geometry_kind must be 'parallel' or 'fan'")
     p = geometry(N, n_angles)[0]
     x_true = shepp_logan(N).ravel(order="F")
     b_exact = A @ x_true

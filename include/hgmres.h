@@ -218,6 +218,16 @@ HGM_API int hgm_mat_create_siddon(hgm_ctx* ctx, int N, int n_angles, double det_
  * tile must divide N (and super); super must divide N. */
 HGM_API int hgm_mat_create_siddon_ordered(hgm_ctx* ctx, int N, int n_angles, double det_offset,
                                           int dtype, int tile, int super_block, hgm_mat** out);
+/* Fan-beam projector with a curved (equiangular) detector generated on the device -- the CTtype
+ * 'fancurved' of run_2D_phantom.m:12-13 (PRtomo_mismatched is not vendored by the reference; the
+ * geometry follows AIR Tools II fanbeamtomo's published conventions, hgmres.problems.fan_geometry,
+ * bit-identical to hgmres.problems.fanbeam_projector): n_angles source positions over a full turn
+ * at distance R*N from the centre (R > 1/sqrt(2)), p = ceil(sqrt(2) N) rays per source at
+ * equiangular fan angles ((d - (p-1)/2) + det_offset) * span / p; span <= 0 selects the fan that
+ * covers the image's circumscribed circle, 2 asin(1 / (sqrt(2) R)).  Rows a*p + d; tile /
+ * super_block: stored pixel (column) order as for hgm_mat_create_siddon_ordered. */
+HGM_API int hgm_mat_create_fanbeam(hgm_ctx* ctx, int N, int n_angles, double R, double span, double det_offset,
+                                   int dtype, int tile, int super_block, hgm_mat** out);
 /* Unmatched pixel-driven back-projector B (n x m, pixel-major) generated on the device:
  * for every pixel centre and angle, linear interpolation between the two nearest detector
  * bins (bit-identical to hgmres.problems.pixel_driven_backprojector; the role of

@@ -128,9 +128,26 @@ def test_fused_region_overflow_falls_back(gpu_ctx, kind):
     A, B, b, xt = _device_problem(gpu_ctx, 256, 47)
     with gpu_ctx.options(fused_ab=0):
         ref = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True)
-    opts = _fused_opts(0, 128) if kind == 0 else _fused_opts(1, 64)
-    with gpu_ctx.options(**opts):
-        out = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True)
+    if kind == 1:
+        # the row-wave plan retries a refused region with half its side (round 5): 64 -> 32, the
+        # default plan, bit for bit
+        with gpu_ctx.options(**_fused_opts(1, 64)):
+            out = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True)
+        with gpu_ctx.options(**_fused_opts(1, 32)):
+            dflt = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True)
+        for a_, b_ in zip(out, dflt):
+            assert np.array_equal(np.asarray(a_), np.asarray(b_))
+        # refused at every size: 24 x 24 regions at 180 angles (~5,600 rays) and 12 < 16 -> two passes
+        A, B, b, xt = _device_problem(gpu_ctx, 256, 180)
+        with gpu_ctx.options(fused_ab=0):
+            ref = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True)
+        with gpu_ctx.options(**_fused_opts(1, 24)):
+            with pytest.raises(hgmres.HgmError):
+                hgmres.fused_plan_info(A, B)
+            out = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True)
+    else:
+        with gpu_ctx.options(**_fused_opts(0, 128)):
+            out = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, 8, ctx=gpu_ctx, return_H=True)
     for a_, b_ in zip(out, ref):
         assert np.array_equal(np.asarray(a_), np.asarray(b_))
 
