@@ -65,7 +65,7 @@ def test_fanbeam_gmres_family_vs_oracle(gpu_ctx):
     try:
         info = hgmres.fused_plan_info(A, B)
         print(f"[fan 64^2/90] one-pass plan accepted: {info['nslot']} slots")
-    except hgmres.HgmError as e:
+    except (ValueError, hgmres.HgmError) as e:
         print(f"[fan 64^2/90] one-pass plan refused ({e}): two-pass path")
     Ah = hgmres.SparseOperator.from_scipy(P.A, gpu_ctx)
     Bh = hgmres.SparseOperator.from_scipy(P.B, gpu_ctx)
