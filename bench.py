@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--same-device", action="store_true", help="run every rank on GPU 0 (shard emulation)")
     ap.add_argument("--shard1", action="store_true",
                     help="N=1: the sharded code path on a one-rank RCCL communicator (transport rehearsal)")
+    ap.add_argument("--shard-of", type=int, default=1, metavar="N",
+                    help="with --shard1: solve rank 0's pixel shard of an N-way cut (per-rank kernel costs at "
+                         "N GPUs, without the transport; the solve is then of that shard alone)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="experiment: per-context numerics option (hgm_ctx_set_option), e.g. mgs_fused=0")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -246,7 +249,8 @@ def main():
             ctx = host_allreduce_context(local, rank, world)
         else:
             ctx = init_context(local, rank, world, one_rank_comm=args.shard1)
-        A, B, b, x_true, (lo, hi), full = build_shard(ctx, wl, rank, world)
+        cut = args.shard_of if args.shard1 else world
+        A, B, b, x_true, (lo, hi), full = build_shard(ctx, wl, rank, cut)
     else:
         ctx = hgmres.Context(local)
         A, B, b, x_true = build_problem(ctx, wl, seed=rank)
@@ -438,7 +442,9 @@ def main():
                             f"tol=0, lambda={lam}, orth={args.orth}, "
                             f"residual={'explicit A*x' if args.explicit_residual else '(A*Q)*y'}",
                 "global_batch": 1 if shard else world,
-                "parallelism": (f"pixel-sharded over {world} ranks ({args.comm} all-reduce of the m-vector)"
+                "parallelism": (f"rank 0's shard of a {args.shard_of}-way pixel cut on a one-rank communicator "
+                                f"(per-rank kernel costs; not a global solve)" if args.shard1 and args.shard_of > 1 else
+                                f"pixel-sharded over {world} ranks ({args.comm} all-reduce of the m-vector)"
                                 if shard else
                                 "replicas: one independent slice per GPU" if world > 1 else "single GPU"),
                 "step": (f"GCV lambda selection ({gcv['k']} Arnoldi steps + fminbnd on the cached H) and one "

@@ -580,6 +580,7 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             break;
         case HGM_OPT_FUSED_PLAN_DEV: if (!b01) return bad("fused_plan_dev is 0 or 1"); n.fused_plan_dev = v != 0; break;
         case HGM_OPT_FUSED_REDUCE: if (!b01) return bad("fused_reduce is 0 or 1"); n.fused_reduce = (int)v; break;
+        case HGM_OPT_FUSED_ROWPAIR: if (!b01) return bad("fused_rowpair is 0 or 1"); n.fused_rowpair = v != 0; break;
         case HGM_OPT_HOST_SPIN_US:
             if (!(v == std::floor(v) && std::fabs(v) <= 1e9)) return bad("host_spin_us is an integer");
             g_host_spin_us.store((int)v);
@@ -625,6 +626,7 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_FUSED_ACC32: *v = n.fused_acc32; break;
         case HGM_OPT_FUSED_PLAN_DEV: *v = n.fused_plan_dev; break;
         case HGM_OPT_FUSED_REDUCE: *v = n.fused_reduce; break;
+        case HGM_OPT_FUSED_ROWPAIR: *v = n.fused_rowpair; break;
         case HGM_OPT_HOST_SPIN_US: *v = g_host_spin_us.load(); break;
         default: return HGM_E_ARG;
     }

@@ -63,6 +63,8 @@ struct FusedPlan {
     int elem = 8;                 // value size (kind 1: fp64 or fp32; the slots are byte offsets)
     int region = 0, waves = 0, maxr = 0, group = 0, depth = 0;
     bool pairs = false;
+    bool rowpair = false;         // kind 1: units of two consecutive rows (k_fused_rw RP; runs split so
+                                  // every unit spans one chunk)
     int64_t nreg = 0, nsub = 0, nlr = 0, nslot = 0, m = 0, maxlen = 0;
     // kind 1: per (region, wave) a range of row runs; the region's rays; every entry's index
     // among its region's rays
@@ -565,7 +567,18 @@ __device__ __forceinline__ void lds_add(T* p, T t) {
 //      workgroups per CU: 72 KB of LDS).
 template <typename T, int AM> struct AccT { using t = T; };
 template <> struct AccT<float, 2> { using t = double; };
-template <typename T, bool GK, int AM, int W, int MAXR, int G, int NCH, int D, bool PR, int DBG = 0>
+//
+// RP (row pairs, round 5): the G rows of a batch go as G/2 units of two consecutive rows, whose
+// entries are contiguous in B's CSR: one chunk of CH entries from the unit's first pair carries
+// both rows (the first row from lane 0, the second right after it), so a row of ~60 entries no
+// longer leaves half the lanes idle.  The products are split by row into P[2u] / P[2u+1] (the
+// butterfly then sums rows exactly as without RP), and each wave has TWO private accumulator
+// arrays, one per row parity of a unit: both rows of a unit add in one LDS instruction, and since
+// the first row's lanes address array 0 and the second row's array 1, the addresses of one
+// instruction stay distinct (two consecutive pixel rows share most of their rays).  The
+// determinism invariant of lds_add holds per array; the arrays are added in a fixed order at the
+// end.  The plan keeps every unit's span within one chunk (fused_plan_build_rw splits runs).
+template <typename T, bool GK, int AM, int W, int MAXR, int G, int NCH, int D, bool PR, int DBG = 0, bool RP = false>
 __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__ reg_base, const int32_t* __restrict__ ray_tab,
                                                      const int32_t* __restrict__ wrun, const int2* __restrict__ runs,
                                                      const int64_t* __restrict__ rp, const T* __restrict__ val,
@@ -574,13 +587,15 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                                                      const T* __restrict__ xt, T* __restrict__ zx_part,
                                                      const T* ev, const T* __restrict__ easq, T* zout, int side_sq) {
     static_assert(D >= 2 && D <= 4, "ring depth");
+    static_assert(!RP || (PR && NCH == 1 && DBG == 0 && G % 2 == 0), "row pairs: pairs, one chunk");
+    constexpr int NA = RP ? 2 : 1;               // private accumulator arrays per wave
     using TA = typename AccT<T, AM>::t;
     constexpr int EPL = PR ? 2 : 1;              // entries per lane per chunk
     constexpr int CH = 64 * EPL;                 // entries per chunk
     constexpr int ES = (int)sizeof(T);
     constexpr int AS = (int)(sizeof(TA) / sizeof(T));   // accumulator offset = slot offset * AS
     __shared__ T qloc[MAXR];                     // (the last 64: the lanes' dummy slots)
-    __shared__ TA acc[W][MAXR];
+    __shared__ TA acc[W][NA][MAXR];
     const int g = blockIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int ln = threadIdx.x & 63;
@@ -589,7 +604,9 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     for (int k = threadIdx.x; k < nr; k += 64 * W) {
         qloc[k] = q[ray_tab[pb + k]];
 #pragma unroll
-        for (int w = 0; w < W; ++w) acc[w][k] = TA(0);
+        for (int w = 0; w < W; ++w)
+#pragma unroll
+            for (int h = 0; h < NA; ++h) acc[w][h][k] = TA(0);
     }
     if (threadIdx.x < 64) qloc[MAXR - 64 + threadIdx.x] = T(0);
     // the epilogue coefficient: the bits the host takes from the same sum of squares
@@ -597,7 +614,8 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     int ua = wrun[g * W + wv];
     const int ub = wrun[g * W + wv + 1];
     __syncthreads();
-    TA* __restrict__ ac = acc[wv];
+    TA* __restrict__ ac = &acc[wv][0][0];
+    constexpr uint32_t POFF = (uint32_t)(MAXR * sizeof(TA));   // (RP) the second array, in bytes
     // the wave's runs (<= 64, the plan checks) in lanes: readlane in the loop, no loads there
     // (a conditional load makes the compiler wait for every load in flight after it, and scalar
     // loads' lgkmcnt waits would also wait on the LDS)
@@ -651,6 +669,32 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
         const int bspan = PR ? (int)((readlane64(rpv, G) - eb + 1) & ~int64_t(1)) : 0;
         const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + eb, bspan * ES);
         const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lidx + eb, bspan * 2);
+        if constexpr (RP) {
+#pragma unroll
+            for (int u = 0; u < G / 2; ++u) {
+                // unit u = rows 2u, 2u+1 (a single row, or none, at the batch's end: lengths 0)
+                const int64_t e0 = readlane64(rpv, 2 * u), e1 = readlane64(rpv, 2 * u + 1),
+                              e2 = readlane64(rpv, 2 * u + 2);
+                b.len[2 * u] = (int)(e1 - e0);
+                b.len[2 * u + 1] = (int)(e2 - e1);
+                const int off = (int)(e0 & 1);
+                const int rel = (int)(e0 - eb) - off;
+                b.off[2 * u] = off;
+                const bool in = 2 * ln < (int)(e2 - e0) + off;
+                const int vo = in ? 2 * ln * ES : (1 << 30), lo = in ? 2 * ln * 2 : (1 << 30);
+                if constexpr (ES == 8) {
+                    const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, vo, rel * ES, 2));
+                    b.v[u][0][0] = t.x;
+                    b.v[u][0][EPL - 1] = t.y;
+                } else {
+                    const float2 t = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rv, vo, rel * ES, 2));
+                    b.v[u][0][0] = t.x;
+                    b.v[u][0][EPL - 1] = t.y;
+                }
+                b.s[u][0] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, lo, rel * 2, 2);
+            }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < G; ++j) {
             if constexpr (PR) {
@@ -710,8 +754,33 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     auto process = [&](RB& b) {
         T P[G];
         uint32_t k[G][NCH][EPL];
+        bool ia[RP ? G / 2 : 1][EPL];             // (RP) entry of its unit's first row
+        if constexpr (RP) {
 #pragma unroll
-        for (int j = 0; j < G; ++j) {
+            for (int u = 0; u < G / 2; ++u) {
+                const int la = b.len[2 * u], lab = la + b.len[2 * u + 1];
+                T pa = T(0), pb = T(0);
+#pragma unroll
+                for (int e = 0; e < EPL; ++e) {
+                    const int pos = EPL * ln - b.off[2 * u] + e;
+                    const bool inA = (uint32_t)pos < (uint32_t)la;
+                    const bool in = (uint32_t)pos < (uint32_t)lab;
+                    const uint32_t sl = e ? b.s[u][0] >> 16 : b.s[u][0] & 0xffffu;
+                    const uint32_t dm = (uint32_t)(MAXR - 64 + ln) * (uint32_t)ES;
+                    const uint32_t kq = in ? sl : dm;
+                    const T p = b.v[u][0][e] * *reinterpret_cast<const T*>(reinterpret_cast<const char*>(qloc) + kq);
+                    pa = pa + (inA ? p : T(0));
+                    pb = pb + (inA ? T(0) : p);
+                    // the accumulator: array 0 for the unit's first row, 1 for its second, the dummy
+                    k[u][0][e] = in ? sl * AS + (inA ? 0u : POFF) : dm * AS;
+                    ia[u][e] = inA;
+                }
+                P[2 * u] = pa;
+                P[2 * u + 1] = pb;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < G && !RP; ++j) {
             T p = T(0);
 #pragma unroll
             for (int c = 0; c < NCH; ++c)
@@ -751,8 +820,27 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
         } else {
             zx = zx + zs * b.xv;
         }
+        if constexpr (RP) {
 #pragma unroll
-        for (int j = 0; j < G; ++j) {
+            for (int u = 0; u < G / 2; ++u) {
+                const T za = lane_bcast(zs, 2 * u * GL), zb = lane_bcast(zs, (2 * u + 1) * GL);
+#pragma unroll
+                for (int e = 0; e < EPL; ++e) {
+                    const T sj = ia[u][e] ? za : zb;
+                    TA* pa = reinterpret_cast<TA*>(reinterpret_cast<char*>(ac) + k[u][0][e]);
+                    if constexpr (AM == 2) {
+                        lds_add(pa, (double)b.v[u][0][e] * (double)sj);
+                    } else if constexpr (AM == 1) {
+                        const T t = b.v[u][0][e] * sj;
+                        *pa = *pa + t;
+                    } else {
+                        lds_add(pa, b.v[u][0][e] * sj);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < G && !RP; ++j) {
             const T sj = lane_bcast(zs, j * GL);
 #pragma unroll
             for (int c = 0; c < NCH; ++c)
@@ -808,9 +896,13 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     // array of their own would push the workgroup past half the LDS, one workgroup per CU)
     if (zx_part && ln == 0) qloc[wv] = zx;
     for (int k = threadIdx.x; k < nr; k += 64 * W) {
-        TA t = acc[0][k];
+        TA t = acc[0][0][k];
+        if constexpr (RP) t += acc[0][1][k];
 #pragma unroll
-        for (int w = 1; w < W; ++w) t += acc[w][k];
+        for (int w = 1; w < W; ++w) {
+            t += acc[w][0][k];
+            if constexpr (RP) t += acc[w][1][k];
+        }
         part[pb + k] = t;
     }
     if (zx_part) {
@@ -1234,7 +1326,7 @@ static void plan_bands(FusedPlan* P, const std::vector<int32_t>& ray_tab, const 
 // The device part of the row-wave plan: ray sets, slots (lidx) and ray_tab by k_plan_count /
 // k_plan_fill, then the ray-major reduction index by a counting sort of ray_tab on the host
 // (slots in increasing order = regions in order, as the host build).
-static FusedPlan* fused_plan_dev_finish(hgm_ctx* c, const hgm_mat* B, int R, int W, int G, int es, int64_t nreg,
+static FusedPlan* fused_plan_dev_finish(hgm_ctx* c, const hgm_mat* B, int R, int W, int G, bool rowpair, int es, int64_t nreg,
                                         int64_t maxlen, const std::vector<int32_t>& wrun,
                                         const std::vector<int2>& runs,
                                         std::chrono::steady_clock::time_point t0) {
@@ -1250,6 +1342,7 @@ static FusedPlan* fused_plan_dev_finish(hgm_ctx* c, const hgm_mat* B, int R, int
         P->group = G;
         P->depth = c->num.fused_depth;
         P->pairs = c->num.fused_pairs;
+        P->rowpair = rowpair;
         P->maxlen = maxlen;
         P->nreg = nreg;
         P->m = m;
@@ -1368,6 +1461,32 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
             }
         }
     });
+    // Row pairs (k_fused_rw RP): the kernel pairs rows 2i, 2i+1 of each run (batches start at even
+    // offsets) and loads a pair as one chunk of 128 entries from its first row's first pair, so a
+    // pair whose span (both rows + the alignment entry) exceeds 128 is not allowed: the run is cut
+    // after the pair's first row, which then goes alone (C4: ~2.6 % of the pairs, ~4 cuts per wave).
+    const bool rowpair = c->num.fused_rowpair && c->num.fused_pairs && G % 2 == 0 && maxlen + 1 <= 128;
+    if (rowpair) {
+        parallel_for((int64_t)wr.size(), [&](int64_t i) {
+            std::vector<int2> out;
+            for (const int2& r : wr[(size_t)i]) {
+                int s0 = r.x;
+                const int end = r.x + r.y;
+                int s = r.x;
+                while (s < end) {
+                    if (s + 1 < end && (rp[s + 2] - rp[s]) + (rp[s] & 1) > 128) {
+                        out.push_back(make_int2(s0, s + 1 - s0));   // the run ends with row s alone
+                        s0 = s + 1;
+                        s = s + 1;
+                    } else {
+                        s += 2;
+                    }
+                }
+                if (s0 < end) out.push_back(make_int2(s0, end - s0));
+            }
+            wr[(size_t)i].swap(out);
+        });
+    }
     std::vector<int32_t> wrun((size_t)nreg * W + 1, 0);
     for (size_t i = 0; i < wr.size(); ++i) {
         HGM_REQUIRE(wr[i].size() <= 64, "fused A*(B*q): more than 64 row runs per wave");
@@ -1375,7 +1494,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
     }
     std::vector<int2> runs(std::max<int32_t>(wrun.back(), 1));
     for (size_t i = 0; i < wr.size(); ++i) std::copy(wr[i].begin(), wr[i].end(), runs.begin() + wrun[i]);
-    if (dev_build) return fused_plan_dev_finish(c, B, R, W, G, es, nreg, maxlen, wrun, runs, t0);
+    if (dev_build) return fused_plan_dev_finish(c, B, R, W, G, rowpair, es, nreg, maxlen, wrun, runs, t0);
     // region ray sets and every entry's slot among them (a dense map per thread)
     std::vector<std::vector<int32_t>> rrays(nreg);
     std::vector<uint16_t> lidx(std::max<int64_t>(nnz, 1) + 256, 0);
@@ -1436,6 +1555,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
         P->group = G;
         P->depth = c->num.fused_depth;
         P->pairs = c->num.fused_pairs;
+        P->rowpair = rowpair;
         P->maxr = maxr;
         P->maxlen = maxlen;
         P->nreg = nreg;
@@ -1488,7 +1608,7 @@ static int64_t fused_key(const Numerics& nu) {
     if (!rw) return ((int64_t)nu.fused_region << 1);
     return 1 | ((int64_t)nu.fused_wregion << 1) | ((int64_t)nu.fused_waves << 10) | ((int64_t)nu.fused_group << 13) |
            ((int64_t)nu.fused_depth << 17) | ((int64_t)nu.fused_pairs << 20) | ((int64_t)nu.fused_acc32 << 21) |
-           ((int64_t)nu.fused_plan_dev << 23);
+           ((int64_t)nu.fused_plan_dev << 23) | ((int64_t)nu.fused_rowpair << 24);
 }
 
 // The plan of B, built on first use (a failure to plan leaves the two-pass path in place).
@@ -1548,15 +1668,31 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
     const int dbg = c->num.fused_dbg;
     const int am = sizeof(T) == 4 ? c->num.fused_acc32 : 0;   // accumulation mode (k_fused_rw AM)
     const bool side = fa.side_out != nullptr && (fa.xt != nullptr || fa.side_sq);
-#define HGM_RWL(AMV, WV, MRV, GV, NCV, DV, PV, DBV)                                                                  \
+#define HGM_RWL(AMV, WV, MRV, GV, NCV, DV, PV, DBV) HGM_RWLR(AMV, WV, MRV, GV, NCV, DV, PV, DBV, false)
+#define HGM_RWLR(AMV, WV, MRV, GV, NCV, DV, PV, DBV, RPV)                                                            \
     {                                                                                                                 \
         if (!dry)                                                                                                     \
-            launch(c, false, k_fused_rw<T, GK, AMV, WV, MRV, GV, NCV, DV, PV, DBV>, dim3((unsigned)P->nreg),        \
+            launch(c, false, k_fused_rw<T, GK, AMV, WV, MRV, GV, NCV, DV, PV, DBV, RPV>, dim3((unsigned)P->nreg),   \
                    dim3(64 * WV), (const int64_t*)P->reg_base, (const int32_t*)P->ray_tab, (const int32_t*)P->wrun, \
                    (const int2*)P->runs, (const int64_t*)B->rp, (const T*)B->val, (const uint16_t*)P->lidx, fa.q,  \
                    fa.zraw, (typename AccT<T, AMV>::t*)P->part, side ? fa.xt : nullptr,                            \
                    side ? (T*)P->zx_part : nullptr, fa.ev, fa.easq, fa.zout, fa.side_sq ? 1 : 0);                  \
         return true;                                                                                                  \
+    }
+    if (P->rowpair) {
+        // row pairs: the production accumulation, four waves, one chunk, 8-row batches, depth 2
+        if (dbg || W != 4 || G != 8 || NC != 1 || !PRm || D != 2) {
+            if (dry) return false;
+            throw Error{HGM_E_ARG, "fused A*(B*q): row pairs take 4 waves, 8 rows, one chunk, pairs, depth 2"};
+        }
+        constexpr int AMP = sizeof(T) == 4 ? 1 : 0;
+        if (am == AMP) {
+            if (MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, true)
+            if (MR == 1536) HGM_RWLR(AMP, 4, 1536, 8, 1, 2, true, 0, true)
+            if (MR == 1088) HGM_RWLR(AMP, 4, 1088, 8, 1, 2, true, 0, true)
+        }
+        if (dry) return false;
+        throw Error{HGM_E_ARG, "fused A*(B*q): no row-pair kernel for this plan's shape and the options"};
     }
     if constexpr (GK) {
         constexpr int AMP = sizeof(T) == 4 ? 1 : 0;    // the production accumulation of this T
@@ -1613,6 +1749,7 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
         }
     }
 #undef HGM_RWL
+#undef HGM_RWLR
     if (dry) return false;
     throw Error{HGM_E_ARG, "fused A*(B*q): no row-wave kernel for this plan and options"};
 }

@@ -124,8 +124,10 @@ enum hgm_ctx_option {
                                       (creation, hgm_mat_set_bands) */
     HGM_OPT_FUSED_AB = 18,         /* the m-space operator A*(B*q) of the AB solvers in ONE pass over B's
                                       pixel-major entries when B is A' value for value (a device transpose
-                                      pair over a tiled pixel grid), single rank [1]: the kept B*q and
-                                      A*(B*q) come out of one kernel (plan built on first use) */
+                                      pair over a tiled pixel grid, or a pixel shard of whole tile columns
+                                      of one: on a communicator every rank runs it on its shard, followed by
+                                      the m-vector all-reduce) [1]: the kept B*q and A*(B*q) come out of one
+                                      kernel (plan built on first use) */
     HGM_OPT_FUSED_REGION = 19,     /* ... pixel square (side) per workgroup of that pass [64] */
     HGM_OPT_FUSED_BS = 20,         /* ... threads per workgroup: 512 or 1024 [1024] (same summation order) */
     HGM_OPT_FUSED_DBG = 21,        /* ... timing experiments only: bits skip its phases, results WRONG [0] */
@@ -152,7 +154,9 @@ enum hgm_ctx_option {
     HGM_OPT_HOST_SPIN_US = 33      /* host waits (stream / event / ring polls): microseconds of pure spinning
                                       before each further poll yields the core (sched_yield) [200]; < 0: the
                                       blocking hipStreamSynchronize / hipEventSynchronize.  PROCESS-WIDE: the
-                                      last value set on any context applies to every context */
+                                      last value set on any context applies to every context */,
+    HGM_OPT_FUSED_ROWPAIR = 34     /* ... row-wave pass: two consecutive pixel rows per 128-entry chunk, each
+                                      row parity into a private accumulator array of the wave [0] */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for

@@ -39,13 +39,14 @@ for vname in variants:
     # | d<bits> (phase-skip timing)
     mf = re.fullmatch(r"f(\d+)(?:x(\d))?(?:r(\d+))?", vname)
     # row-wave pass: waves, region, rows per batch, ring depth, pairs
-    mw = re.fullmatch(r"w(\d)r(\d+)(?:g(\d))?(?:d(\d))?(?:p(\d))?(?:a(\d))?", vname)
+    mw = re.fullmatch(r"w(\d)r(\d+)(?:g(\d))?(?:d(\d))?(?:p(\d))?(?:a(\d))?(?:q(\d))?", vname)
     if vname.startswith("e"):                                   # row-wave pass, phase-skip timing
         o = dict(fused_ab=1, fused_kind=1, fused_dbg=int(vname[1:]), fused_acc32=1)
     elif mw:
         o = dict(fused_ab=1, fused_kind=1, fused_waves=int(mw.group(1)), fused_wregion=int(mw.group(2)),
                  fused_group=int(mw.group(3) or 8), fused_depth=int(mw.group(4) or 2),
-                 fused_pairs=int(mw.group(5) or 1), fused_acc32=int(mw.group(6) or 1))
+                 fused_pairs=int(mw.group(5) or 1), fused_acc32=int(mw.group(6) or 1),
+                 fused_rowpair=int(mw.group(7) or 0))
     elif vname == "two":
         o = dict(fused_ab=0)
     elif mf:

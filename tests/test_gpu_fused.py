@@ -463,3 +463,66 @@ def test_fused_reduce_by_band_is_bitwise(gpu_ctx, N, na, dtype):
             outs[red] = o
     for a_, b_ in zip(outs[0], outs[1]):
         assert np.array_equal(np.asarray(a_), np.asarray(b_))
+
+
+# ---------------------------------------------------------------------------------------------
+# Row pairs (HGM_OPT_FUSED_ROWPAIR, k_fused_rw RP, round 5): two consecutive pixel rows per
+# 128-entry chunk, each row parity into its own private accumulator array per wave.  Another
+# fixed summation order: the same bars as the default pass (two-pass and oracle at 1e-10,
+# bitwise repeats; GKB in its production envelope), on geometries whose pairs overflow a chunk
+# (the plan cuts those runs) and ones that never do.
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("N,na", [(256, 47), (512, 30), (100, 17), (200, 60)])
+def test_fused_rowpair_gmres_matches_oracle(gpu_ctx, N, na):
+    A, B, b, xt = _device_problem(gpu_ctx, N, na)
+    k = 20
+    with gpu_ctx.options(fused_ab=0):
+        ref2 = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
+    with gpu_ctx.options(fused_ab=1, fused_rowpair=1):
+        info = hgmres.fused_plan_info(A, B)
+        out = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
+        again = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
+        bq1, ab1 = hgmres.spmv_ab(A, B, b)
+    with gpu_ctx.options(fused_ab=1, fused_rowpair=0):
+        bq0, ab0 = hgmres.spmv_ab(A, B, b)
+    for a_, b_ in zip(out, again):
+        assert np.array_equal(np.asarray(a_), np.asarray(b_))
+    dH = float(np.max(np.abs(out[-1] - ref2[-1])) / np.max(np.abs(ref2[-1])))
+    print(f"[rowpair N={N} angles={na}] slots {info['nslot']}: |dH| vs two-pass {dH:.1e}, x {rel(out[0], ref2[0]):.1e}, "
+          f"A(Bq) vs default pass {rel(ab1, ab0):.1e}, Bq {rel(bq1, bq0):.1e}")
+    assert rel(bq1, bq0) <= 1e-14 and rel(ab1, ab0) <= 1e-14
+    assert dH <= TOL and rel(out[0], ref2[0]) <= TOL
+    As = A.to_scipy()
+    xo, eo, ro, ko, Ho = R.ABgmres_nonhybrid_bounds(As, As.T.tocsr(), b, xt, 0.0, k, return_H=True)
+    assert float(np.max(np.abs(out[-1] - Ho)) / np.max(np.abs(Ho))) <= TOL
+    assert rel(out[0], xo) <= TOL and hist_dev(out[1], eo) <= TOL and hist_dev(out[2], ro) <= TOL
+
+
+@pytest.mark.parametrize("dtype", [None, "f32"])
+def test_fused_rowpair_gkb_matches_oracle(gpu_ctx, dtype):
+    A, At, b, xt = _gkb_pair(gpu_ctx, 256, 47, dtype=dtype)
+    k = 8 if dtype is None else 4
+    with gpu_ctx.options(fused_ab=1, fused_rowpair=1):
+        hgmres.fused_plan_info(A, At)
+        q1 = hgmres.lsqr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+        q1b = hgmres.lsqr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+        m1 = hgmres.lsmr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+    with gpu_ctx.options(fused_ab=1, fused_rowpair=0):
+        q0 = hgmres.lsqr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+        m0 = hgmres.lsmr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
+    for a_, b_ in zip(q1, q1b):
+        assert np.array_equal(np.asarray(a_), np.asarray(b_))
+    As = A.to_scipy()
+    if dtype is None:
+        qo, mo = R.lsqr_solver(As, b, xt, 0.0, k), R.lsmr_solver(As, b, xt, 0.0, k)
+    else:
+        qo, mo = R.lsqr_solver_f32(As, b, xt, 0.0, k), R.lsmr_solver_f32(As, b, xt, 0.0, k)
+    dev = dict(lsqr_x=rel(q1[0], qo[0]), lsqr_res=hist_dev(q1[2], qo[2]), lsmr_x=rel(m1[0], mo[0]),
+               lsmr_res=hist_dev(m1[2], mo[2]), lsmr_ar=hist_dev(m1[3], mo[3]))
+    dev0 = dict(lsqr_x=rel(q0[0], qo[0]), lsqr_res=hist_dev(q0[2], qo[2]), lsmr_x=rel(m0[0], mo[0]),
+                lsmr_res=hist_dev(m0[2], mo[2]), lsmr_ar=hist_dev(m0[3], mo[3]))
+    print(f"[rowpair gkb {dtype or 'f64'} k={k}] " + " ".join(f"{a}={v:.1e}" for a, v in dev.items()) +
+          " | default pass: " + " ".join(f"{a}={v:.1e}" for a, v in dev0.items()))
+    bar = TOL if dtype is None else 1e-5
+    for key in dev:
+        assert dev[key] <= max(bar, 3 * dev0[key]), key
