@@ -580,7 +580,10 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             break;
         case HGM_OPT_FUSED_PLAN_DEV: if (!b01) return bad("fused_plan_dev is 0 or 1"); n.fused_plan_dev = v != 0; break;
         case HGM_OPT_FUSED_REDUCE: if (!b01) return bad("fused_reduce is 0 or 1"); n.fused_reduce = (int)v; break;
-        case HGM_OPT_FUSED_ROWPAIR: if (!b01) return bad("fused_rowpair is 0 or 1"); n.fused_rowpair = v != 0; break;
+        case HGM_OPT_FUSED_ROWPAIR:
+            if (!(v == 0 || v == 1 || v == 2 || v == 3)) return bad("fused_rowpair is 0, 1, 2 or 3");
+            n.fused_rowpair = (int)v;
+            break;
         case HGM_OPT_HOST_SPIN_US:
             if (!(v == std::floor(v) && std::fabs(v) <= 1e9)) return bad("host_spin_us is an integer");
             g_host_spin_us.store((int)v);

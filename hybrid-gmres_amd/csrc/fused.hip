@@ -63,8 +63,8 @@ struct FusedPlan {
     int elem = 8;                 // value size (kind 1: fp64 or fp32; the slots are byte offsets)
     int region = 0, waves = 0, maxr = 0, group = 0, depth = 0;
     bool pairs = false;
-    bool rowpair = false;         // kind 1: units of two consecutive rows (k_fused_rw RP; runs split so
-                                  // every unit spans one chunk)
+    int rowpair = 0;              // kind 1: units of two consecutive rows (k_fused_rw RP 1 / 2; runs
+                                  // split so every unit spans one chunk)
     int64_t nreg = 0, nsub = 0, nlr = 0, nslot = 0, m = 0, maxlen = 0;
     // kind 1: per (region, wave) a range of row runs; the region's rays; every entry's index
     // among its region's rays
@@ -578,7 +578,13 @@ template <> struct AccT<float, 2> { using t = double; };
 // instruction stay distinct (two consecutive pixel rows share most of their rays).  The
 // determinism invariant of lds_add holds per array; the arrays are added in a fixed order at the
 // end.  The plan keeps every unit's span within one chunk (fused_plan_build_rw splits runs).
-template <typename T, bool GK, int AM, int W, int MAXR, int G, int NCH, int D, bool PR, int DBG = 0, bool RP = false>
+// RP = 3 is RP 1 with ONE accumulator array per wave (no extra LDS: the occupancy of the plain
+// pass) and each unit's two rows added by two instructions, every lane of the other row on its
+// dummy slot.
+// RP = 2 places the second row at its own pair-aligned start on the lane after the first row's last
+// pair (row membership per lane, not per entry: fewer instructions per unit); a unit then fits when
+// the two rows' pair counts add up to <= 64 lanes.
+template <typename T, bool GK, int AM, int W, int MAXR, int G, int NCH, int D, bool PR, int DBG = 0, int RP = 0>
 __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__ reg_base, const int32_t* __restrict__ ray_tab,
                                                      const int32_t* __restrict__ wrun, const int2* __restrict__ runs,
                                                      const int64_t* __restrict__ rp, const T* __restrict__ val,
@@ -588,7 +594,7 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                                                      const T* ev, const T* __restrict__ easq, T* zout, int side_sq) {
     static_assert(D >= 2 && D <= 4, "ring depth");
     static_assert(!RP || (PR && NCH == 1 && DBG == 0 && G % 2 == 0), "row pairs: pairs, one chunk");
-    constexpr int NA = RP ? 2 : 1;               // private accumulator arrays per wave
+    constexpr int NA = (RP == 1 || RP == 2) ? 2 : 1;   // private accumulator arrays per wave
     using TA = typename AccT<T, AM>::t;
     constexpr int EPL = PR ? 2 : 1;              // entries per lane per chunk
     constexpr int CH = 64 * EPL;                 // entries per chunk
@@ -669,7 +675,40 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
         const int bspan = PR ? (int)((readlane64(rpv, G) - eb + 1) & ~int64_t(1)) : 0;
         const __amdgpu_buffer_rsrc_t rv = buf_rsrc(val + eb, bspan * ES);
         const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lidx + eb, bspan * 2);
-        if constexpr (RP) {
+        if constexpr (RP == 2) {
+#pragma unroll
+            for (int u = 0; u < G / 2; ++u) {
+                // unit u = rows 2u, 2u+1: the first row's pairs from lane 0, the second row's from
+                // lane LA at its own pair-aligned start
+                const int64_t e0 = readlane64(rpv, 2 * u), e1 = readlane64(rpv, 2 * u + 1),
+                              e2 = readlane64(rpv, 2 * u + 2);
+                const int lenA = (int)(e1 - e0), lenB = (int)(e2 - e1);
+                const int offA = (int)(e0 & 1), offB = (int)(e1 & 1);
+                b.len[2 * u] = lenA;
+                b.len[2 * u + 1] = lenB;
+                b.off[2 * u] = offA;
+                b.off[2 * u + 1] = offB;
+                const int LA = (lenA + offA + 1) >> 1;
+                const int relA = (int)(e0 - eb) - offA, relB = (int)(e1 - eb) - offB;
+                const bool isA = ln < LA;
+                const int li = isA ? ln : ln - LA;
+                const bool in = 2 * li < (isA ? lenA + offA : lenB + offB);
+                const int base = (isA ? relA : relB) + 2 * li;      // entry index from eb
+                const int vo = in ? base * ES : (1 << 30), lo = in ? base * 2 : (1 << 30);
+                if constexpr (ES == 8) {
+                    const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, vo, 0, 2));
+                    b.v[u][0][0] = t.x;
+                    b.v[u][0][EPL - 1] = t.y;
+                } else {
+                    const float2 t = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rv, vo, 0, 2));
+                    b.v[u][0][0] = t.x;
+                    b.v[u][0][EPL - 1] = t.y;
+                }
+                b.s[u][0] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, lo, 0, 2);
+            }
+            return;
+        }
+        if constexpr (RP == 1 || RP == 3) {
 #pragma unroll
             for (int u = 0; u < G / 2; ++u) {
                 // unit u = rows 2u, 2u+1 (a single row, or none, at the batch's end: lengths 0)
@@ -755,7 +794,32 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
         T P[G];
         uint32_t k[G][NCH][EPL];
         bool ia[RP ? G / 2 : 1][EPL];             // (RP) entry of its unit's first row
-        if constexpr (RP) {
+        bool la_[RP == 2 ? G / 2 : 1];            // (RP 2) lane of its unit's first row
+        uint32_t kb[RP == 3 ? G / 2 : 1][EPL];    // (RP 3) the second row's accumulator address
+        if constexpr (RP == 2) {
+#pragma unroll
+            for (int u = 0; u < G / 2; ++u) {
+                const int offA = b.off[2 * u], offB = b.off[2 * u + 1];
+                const int LA = (b.len[2 * u] + offA + 1) >> 1;     // lanes of the first row
+                const bool isA = ln < LA;
+                la_[u] = isA;
+                const int pos0 = isA ? 2 * ln - offA : 2 * (ln - LA) - offB;
+                const int len = isA ? b.len[2 * u] : b.len[2 * u + 1];
+                const uint32_t aoff = isA ? 0u : POFF;
+                T p = T(0);
+#pragma unroll
+                for (int e = 0; e < EPL; ++e) {
+                    const bool ok = (uint32_t)(pos0 + e) < (uint32_t)len;
+                    const uint32_t sl = e ? b.s[u][0] >> 16 : b.s[u][0] & 0xffffu;
+                    const uint32_t dm = (uint32_t)(MAXR - 64 + ln) * (uint32_t)ES;
+                    const uint32_t kq = ok ? sl : dm;
+                    p += b.v[u][0][e] * *reinterpret_cast<const T*>(reinterpret_cast<const char*>(qloc) + kq);
+                    k[u][0][e] = ok ? sl * AS + aoff : dm * AS;
+                }
+                P[2 * u] = isA ? p : T(0);
+                P[2 * u + 1] = isA ? T(0) : p;
+            }
+        } else if constexpr (RP == 1 || RP == 3) {
 #pragma unroll
             for (int u = 0; u < G / 2; ++u) {
                 const int la = b.len[2 * u], lab = la + b.len[2 * u + 1];
@@ -772,7 +836,14 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                     pa = pa + (inA ? p : T(0));
                     pb = pb + (inA ? T(0) : p);
                     // the accumulator: array 0 for the unit's first row, 1 for its second, the dummy
-                    k[u][0][e] = in ? sl * AS + (inA ? 0u : POFF) : dm * AS;
+                    // (RP 3: one array, the two rows' adds in two instructions, each other lane on
+                    // its dummy)
+                    if constexpr (RP == 3) {
+                        k[u][0][e] = inA ? sl * AS : dm * AS;
+                        kb[u][e] = (in && !inA) ? sl * AS : dm * AS;
+                    } else {
+                        k[u][0][e] = in ? sl * AS + (inA ? 0u : POFF) : dm * AS;
+                    }
                     ia[u][e] = inA;
                 }
                 P[2 * u] = pa;
@@ -820,13 +891,35 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
         } else {
             zx = zx + zs * b.xv;
         }
-        if constexpr (RP) {
+        if constexpr (RP == 3) {
 #pragma unroll
             for (int u = 0; u < G / 2; ++u) {
                 const T za = lane_bcast(zs, 2 * u * GL), zb = lane_bcast(zs, (2 * u + 1) * GL);
 #pragma unroll
+                for (int h = 0; h < 2; ++h) {         // the unit's first row, then its second
+#pragma unroll
+                    for (int e = 0; e < EPL; ++e) {
+                        const T sj = h ? zb : za;
+                        TA* pa = reinterpret_cast<TA*>(reinterpret_cast<char*>(ac) + (h ? kb[u][e] : k[u][0][e]));
+                        if constexpr (AM == 2) {
+                            lds_add(pa, (double)b.v[u][0][e] * (double)sj);
+                        } else if constexpr (AM == 1) {
+                            const T t = b.v[u][0][e] * sj;
+                            *pa = *pa + t;
+                        } else {
+                            lds_add(pa, b.v[u][0][e] * sj);
+                        }
+                    }
+                }
+            }
+        } else if constexpr (RP) {
+#pragma unroll
+            for (int u = 0; u < G / 2; ++u) {
+                const T za = lane_bcast(zs, 2 * u * GL), zb = lane_bcast(zs, (2 * u + 1) * GL);
+                const T s2 = RP == 2 ? (la_[u] ? za : zb) : T(0);
+#pragma unroll
                 for (int e = 0; e < EPL; ++e) {
-                    const T sj = ia[u][e] ? za : zb;
+                    const T sj = RP == 2 ? s2 : (ia[u][e] ? za : zb);
                     TA* pa = reinterpret_cast<TA*>(reinterpret_cast<char*>(ac) + k[u][0][e]);
                     if constexpr (AM == 2) {
                         lds_add(pa, (double)b.v[u][0][e] * (double)sj);
@@ -897,11 +990,11 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     if (zx_part && ln == 0) qloc[wv] = zx;
     for (int k = threadIdx.x; k < nr; k += 64 * W) {
         TA t = acc[0][0][k];
-        if constexpr (RP) t += acc[0][1][k];
+        if constexpr (NA == 2) t += acc[0][1][k];
 #pragma unroll
         for (int w = 1; w < W; ++w) {
             t += acc[w][0][k];
-            if constexpr (RP) t += acc[w][1][k];
+            if constexpr (NA == 2) t += acc[w][1][k];
         }
         part[pb + k] = t;
     }
@@ -1326,7 +1419,7 @@ static void plan_bands(FusedPlan* P, const std::vector<int32_t>& ray_tab, const 
 // The device part of the row-wave plan: ray sets, slots (lidx) and ray_tab by k_plan_count /
 // k_plan_fill, then the ray-major reduction index by a counting sort of ray_tab on the host
 // (slots in increasing order = regions in order, as the host build).
-static FusedPlan* fused_plan_dev_finish(hgm_ctx* c, const hgm_mat* B, int R, int W, int G, bool rowpair, int es, int64_t nreg,
+static FusedPlan* fused_plan_dev_finish(hgm_ctx* c, const hgm_mat* B, int R, int W, int G, int rowpair, int es, int64_t nreg,
                                         int64_t maxlen, const std::vector<int32_t>& wrun,
                                         const std::vector<int2>& runs,
                                         std::chrono::steady_clock::time_point t0) {
@@ -1465,7 +1558,15 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
     // offsets) and loads a pair as one chunk of 128 entries from its first row's first pair, so a
     // pair whose span (both rows + the alignment entry) exceeds 128 is not allowed: the run is cut
     // after the pair's first row, which then goes alone (C4: ~2.6 % of the pairs, ~4 cuts per wave).
-    const bool rowpair = c->num.fused_rowpair && c->num.fused_pairs && G % 2 == 0 && maxlen + 1 <= 128;
+    const int rpmode = c->num.fused_rowpair;
+    const bool rowpair = rpmode && c->num.fused_pairs && G % 2 == 0 && maxlen + 1 <= 128;
+    // does the unit (s, s+1) fit one chunk: mode 1 both rows contiguous from s's first pair (<= 128
+    // entries), mode 2 each row from its own first pair (<= 64 lanes of pairs together)
+    auto fits = [&](int64_t s) {
+        if (rpmode != 2) return (rp[s + 2] - rp[s]) + (rp[s] & 1) <= 128;
+        const int64_t la = rp[s + 1] - rp[s] + (rp[s] & 1), lb = rp[s + 2] - rp[s + 1] + (rp[s + 1] & 1);
+        return (la + 1) / 2 + (lb + 1) / 2 <= 64;
+    };
     if (rowpair) {
         parallel_for((int64_t)wr.size(), [&](int64_t i) {
             std::vector<int2> out;
@@ -1474,7 +1575,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
                 const int end = r.x + r.y;
                 int s = r.x;
                 while (s < end) {
-                    if (s + 1 < end && (rp[s + 2] - rp[s]) + (rp[s] & 1) > 128) {
+                    if (s + 1 < end && !fits(s)) {
                         out.push_back(make_int2(s0, s + 1 - s0));   // the run ends with row s alone
                         s0 = s + 1;
                         s = s + 1;
@@ -1494,7 +1595,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
     }
     std::vector<int2> runs(std::max<int32_t>(wrun.back(), 1));
     for (size_t i = 0; i < wr.size(); ++i) std::copy(wr[i].begin(), wr[i].end(), runs.begin() + wrun[i]);
-    if (dev_build) return fused_plan_dev_finish(c, B, R, W, G, rowpair, es, nreg, maxlen, wrun, runs, t0);
+    if (dev_build) return fused_plan_dev_finish(c, B, R, W, G, rowpair ? rpmode : 0, es, nreg, maxlen, wrun, runs, t0);
     // region ray sets and every entry's slot among them (a dense map per thread)
     std::vector<std::vector<int32_t>> rrays(nreg);
     std::vector<uint16_t> lidx(std::max<int64_t>(nnz, 1) + 256, 0);
@@ -1555,7 +1656,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
         P->group = G;
         P->depth = c->num.fused_depth;
         P->pairs = c->num.fused_pairs;
-        P->rowpair = rowpair;
+        P->rowpair = rowpair ? rpmode : 0;
         P->maxr = maxr;
         P->maxlen = maxlen;
         P->nreg = nreg;
@@ -1668,7 +1769,7 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
     const int dbg = c->num.fused_dbg;
     const int am = sizeof(T) == 4 ? c->num.fused_acc32 : 0;   // accumulation mode (k_fused_rw AM)
     const bool side = fa.side_out != nullptr && (fa.xt != nullptr || fa.side_sq);
-#define HGM_RWL(AMV, WV, MRV, GV, NCV, DV, PV, DBV) HGM_RWLR(AMV, WV, MRV, GV, NCV, DV, PV, DBV, false)
+#define HGM_RWL(AMV, WV, MRV, GV, NCV, DV, PV, DBV) HGM_RWLR(AMV, WV, MRV, GV, NCV, DV, PV, DBV, 0)
 #define HGM_RWLR(AMV, WV, MRV, GV, NCV, DV, PV, DBV, RPV)                                                            \
     {                                                                                                                 \
         if (!dry)                                                                                                     \
@@ -1687,9 +1788,11 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
         }
         constexpr int AMP = sizeof(T) == 4 ? 1 : 0;
         if (am == AMP) {
-            if (MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, true)
-            if (MR == 1536) HGM_RWLR(AMP, 4, 1536, 8, 1, 2, true, 0, true)
-            if (MR == 1088) HGM_RWLR(AMP, 4, 1088, 8, 1, 2, true, 0, true)
+            if (P->rowpair == 1 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 1)
+            if (P->rowpair == 3 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 3)
+            if (P->rowpair == 2 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 2)
+            if (P->rowpair == 2 && MR == 1536) HGM_RWLR(AMP, 4, 1536, 8, 1, 2, true, 0, 2)
+            if (P->rowpair == 2 && MR == 1088) HGM_RWLR(AMP, 4, 1088, 8, 1, 2, true, 0, 2)
         }
         if (dry) return false;
         throw Error{HGM_E_ARG, "fused A*(B*q): no row-pair kernel for this plan's shape and the options"};

@@ -156,7 +156,10 @@ enum hgm_ctx_option {
                                       blocking hipStreamSynchronize / hipEventSynchronize.  PROCESS-WIDE: the
                                       last value set on any context applies to every context */,
     HGM_OPT_FUSED_ROWPAIR = 34     /* ... row-wave pass: two consecutive pixel rows per 128-entry chunk, each
-                                      row parity into a private accumulator array of the wave [0] */
+                                      row parity into a private accumulator array of the wave [0]: 1 the
+                                      second row right after the first (membership per entry), 2 the second
+                                      row from the lane after the first row's last pair, 3 as 1 with one
+                                      accumulator array (two add instructions per unit) */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for

@@ -21,10 +21,12 @@
 #   ab ROUNDS "ARGS_1" "ARGS_2" ...  alternating bench lines, one per argument set and round
 #                            -> $TAG_ab.jsonl
 #   libab OLD.so WL...       alternating library builds (HGM_LIB) on scripts/time_ops.py -> $TAG_lib_ab.jsonl
+#   shardbudget [N...]       rocprofv3 kernel trace of the C4 solve on rank 0's shard of an N-way cut
+#                            (default 2 4 8) -> $TAG_c4_shard_of<N>_kernel_stats.csv
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-TAG=${TAG:-r4}
+TAG=${TAG:-r5}
 O=gpurun_out/$TAG
 mkdir -p "$O"
 recipe=$1
@@ -47,6 +49,18 @@ case "$recipe" in
         -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > "$O/trace_default.log" 2>&1 || exit 1
     bench_line "$O/trace_default.log" > "$O/${TAG}_bench_default_c4_traced.json"
     cp "$(find "$O/trace_default" -name '*kernel_stats.csv' | head -1)" "$O/${TAG}_default_kernel_stats.csv"
+    ;;
+  shardbudget)
+    # per-rank kernel costs of the pixel-sharded C4 solve at N = 2, 4, 8 (bench.py --shard1
+    # --shard-of N: rank 0's shard on a one-rank RCCL communicator), kernel trace + stats each
+    for nn in ${@:-2 4 8}; do
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/shard_of$nn" -o trace \
+          -- python3 bench.py --workload c4 --shard1 --shard-of $nn --steps 5 --warmup 1 --no-cpu-baseline \
+          > "$O/shard_of$nn.log" 2>&1 || { tail -20 "$O/shard_of$nn.log"; exit 1; }
+      bench_line "$O/shard_of$nn.log" > "$O/${TAG}_bench_c4_shard_of$nn.json"
+      cp "$(find "$O/shard_of$nn" -name '*kernel_stats.csv' | head -1)" "$O/${TAG}_c4_shard_of${nn}_kernel_stats.csv"
+      cp "$(find "$O/shard_of$nn" -name '*kernel_trace.csv' | head -1)" "$O/c4_shard_of${nn}_kernel_trace.csv"
+    done
     ;;
   tests)
     n=$(ls "$O"/${TAG}_gpu_tests_*.log 2>/dev/null | wc -l)

@@ -472,13 +472,14 @@ def test_fused_reduce_by_band_is_bitwise(gpu_ctx, N, na, dtype):
 # bitwise repeats; GKB in its production envelope), on geometries whose pairs overflow a chunk
 # (the plan cuts those runs) and ones that never do.
 # ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("rp", [1, 2, 3])
 @pytest.mark.parametrize("N,na", [(256, 47), (512, 30), (100, 17), (200, 60)])
-def test_fused_rowpair_gmres_matches_oracle(gpu_ctx, N, na):
+def test_fused_rowpair_gmres_matches_oracle(gpu_ctx, N, na, rp):
     A, B, b, xt = _device_problem(gpu_ctx, N, na)
     k = 20
     with gpu_ctx.options(fused_ab=0):
         ref2 = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
-    with gpu_ctx.options(fused_ab=1, fused_rowpair=1):
+    with gpu_ctx.options(fused_ab=1, fused_rowpair=rp):
         info = hgmres.fused_plan_info(A, B)
         out = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
         again = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
@@ -488,7 +489,7 @@ def test_fused_rowpair_gmres_matches_oracle(gpu_ctx, N, na):
     for a_, b_ in zip(out, again):
         assert np.array_equal(np.asarray(a_), np.asarray(b_))
     dH = float(np.max(np.abs(out[-1] - ref2[-1])) / np.max(np.abs(ref2[-1])))
-    print(f"[rowpair N={N} angles={na}] slots {info['nslot']}: |dH| vs two-pass {dH:.1e}, x {rel(out[0], ref2[0]):.1e}, "
+    print(f"[rowpair {rp} N={N} angles={na}] slots {info['nslot']}: |dH| vs two-pass {dH:.1e}, x {rel(out[0], ref2[0]):.1e}, "
           f"A(Bq) vs default pass {rel(ab1, ab0):.1e}, Bq {rel(bq1, bq0):.1e}")
     assert rel(bq1, bq0) <= 1e-14 and rel(ab1, ab0) <= 1e-14
     assert dH <= TOL and rel(out[0], ref2[0]) <= TOL
@@ -498,11 +499,12 @@ def test_fused_rowpair_gmres_matches_oracle(gpu_ctx, N, na):
     assert rel(out[0], xo) <= TOL and hist_dev(out[1], eo) <= TOL and hist_dev(out[2], ro) <= TOL
 
 
+@pytest.mark.parametrize("rp", [1, 2, 3])
 @pytest.mark.parametrize("dtype", [None, "f32"])
-def test_fused_rowpair_gkb_matches_oracle(gpu_ctx, dtype):
+def test_fused_rowpair_gkb_matches_oracle(gpu_ctx, dtype, rp):
     A, At, b, xt = _gkb_pair(gpu_ctx, 256, 47, dtype=dtype)
     k = 8 if dtype is None else 4
-    with gpu_ctx.options(fused_ab=1, fused_rowpair=1):
+    with gpu_ctx.options(fused_ab=1, fused_rowpair=rp):
         hgmres.fused_plan_info(A, At)
         q1 = hgmres.lsqr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
         q1b = hgmres.lsqr_solver(A, b, xt, 0.0, k, ctx=gpu_ctx, At=At)
@@ -521,7 +523,7 @@ def test_fused_rowpair_gkb_matches_oracle(gpu_ctx, dtype):
                lsmr_res=hist_dev(m1[2], mo[2]), lsmr_ar=hist_dev(m1[3], mo[3]))
     dev0 = dict(lsqr_x=rel(q0[0], qo[0]), lsqr_res=hist_dev(q0[2], qo[2]), lsmr_x=rel(m0[0], mo[0]),
                 lsmr_res=hist_dev(m0[2], mo[2]), lsmr_ar=hist_dev(m0[3], mo[3]))
-    print(f"[rowpair gkb {dtype or 'f64'} k={k}] " + " ".join(f"{a}={v:.1e}" for a, v in dev.items()) +
+    print(f"[rowpair {rp} gkb {dtype or 'f64'} k={k}] " + " ".join(f"{a}={v:.1e}" for a, v in dev.items()) +
           " | default pass: " + " ".join(f"{a}={v:.1e}" for a, v in dev0.items()))
     bar = TOL if dtype is None else 1e-5
     for key in dev:
