@@ -94,6 +94,7 @@ struct Numerics {
     int fused_rowpair = 0;          // ... row-wave pass: units of two consecutive rows per chunk (k_fused_rw RP 1/2)
     int fused_reduce = 0;           // ... row-wave partial reduction: 0 by ray (rs_slot), 1 by ray band (runs;
                                     //     bitwise equal, measured 2-4% slower pass at C4, profiles/r4_c4_reduce_band_ab.jsonl)
+    bool lsqr_res_img = true;       // one-pass LSQR: final residual from the A*x image (no SpMV)
     int krylov_pad = -1;            // Krylov basis column padding (elements; -1 auto, kernels.hip krylov_ld)
     int fused_dbg = 0;              // ... timing experiments: skip phases (wrong results)
 };
@@ -377,6 +378,10 @@ template <typename T> void div_sqrt(hgm_ctx* c, int64_t n, const T* in, T* out, 
 // (optional: the kept A*v_k), t = av - alpha*u, *ss_out = ||t||^2 (alpha = sqrt(*ssa), device)
 template <typename T>
 void gkb_mstep(hgm_ctx* c, int64_t n, const T* w, const T* ssa, const T* u, T* t, T* av, T* ss_out);
+// (one-pass LSQR) A*x and A*w images in double (kernels.hip k_lsqr_img)
+template <typename T>
+void lsqr_img(hgm_ctx* c, int64_t m, const T* wm, const T* ssa, const T* coef, const double* st, int k, double* ax,
+              double* aw, bool init);
 template <typename T>
 void lsmr_update(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, const T* v, T c_hbar, T c_x, T c_h,
                  bool first);

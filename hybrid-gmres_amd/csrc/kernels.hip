@@ -1642,6 +1642,40 @@ template void gkb_mstep<double>(hgm_ctx*, int64_t, const double*, const double*,
                                 double*);
 template void gkb_mstep<float>(hgm_ctx*, int64_t, const float*, const float*, const float*, float*, float*, float*);
 
+// (one-pass LSQR) the images of x and w under A, in double, so the exact final residual of
+// lsqr_solver.m:52 needs no SpMV: with A*v_{k+1} = w_m / alpha_{k+1} (the pass's A*v_hat),
+// A*x += (phi/rho) A*w ; A*w = A*v_{k+1} - (theta/rho) A*w (:40-41 under A).  init: A*w = A*v_0,
+// A*x = 0.  Iterations enqueued past a device stop (st[2], as k_lsqr_step) change nothing.
+template <typename T>
+__global__ __launch_bounds__(BS) void k_lsqr_img(int64_t m, const T* __restrict__ wm, const T* ssa, const T* coef,
+                                                 const double* st, int k, double* __restrict__ ax,
+                                                 double* __restrict__ aw, int init) {
+    const double a = (double)(T)sqrt((double)*ssa);
+    const bool live = init || !(st[2] != 0.0 && st[2] < (double)(k + 1));
+    if (!live) return;
+    const double c0 = init ? 0.0 : (double)coef[0], c1 = init ? 0.0 : (double)coef[1];
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < m; i += (int64_t)gridDim.x * BS) {
+        const double av = a != 0.0 ? (double)wm[i] / a : (double)wm[i];
+        if (init) {
+            ax[i] = 0.0;
+            aw[i] = av;
+        } else {
+            ax[i] = ax[i] + c0 * aw[i];
+            aw[i] = av - c1 * aw[i];
+        }
+    }
+}
+template <typename T>
+void lsqr_img(hgm_ctx* c, int64_t m, const T* wm, const T* ssa, const T* coef, const double* st, int k, double* ax,
+              double* aw, bool init) {
+    k_lsqr_img<T><<<grid_for(m), BS, 0, c->stream>>>(m, wm, ssa, coef, st, k, ax, aw, init ? 1 : 0);
+    HGM_HIP(hipGetLastError());
+}
+template void lsqr_img<double>(hgm_ctx*, int64_t, const double*, const double*, const double*, const double*, int,
+                               double*, double*, bool);
+template void lsqr_img<float>(hgm_ctx*, int64_t, const float*, const float*, const float*, const double*, int,
+                              double*, double*, bool);
+
 // lsmr_solver.m:61-67
 template <typename T, bool FIRST>
 __global__ __launch_bounds__(BS) void k_lsmr_update(int64_t n, T* __restrict__ x, T* __restrict__ h,

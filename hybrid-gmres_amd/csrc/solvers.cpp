@@ -865,6 +865,7 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     // non-hybrid: the stop test uses phi_bar (host), so the error history (:43) stays on the
     // device and is read once after the loop instead of once per iteration
     T* errh = hybrid ? nullptr : c->buf<T>("lsqr_errh", maxit);
+    double *img_ax = nullptr, *img_aw = nullptr;   // (one-pass) A*x, A*w images for :52
     int k = 0;
     // Device-resident scalars (single rank, production kernels): beta and alpha stay on the
     // device as sums of squares, the SpMV epilogues read them there (PendNorm::asq), and the
@@ -895,6 +896,13 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         const bool host_sc = !c->num.lsqr_dev;
         const int batch = tol > 0 && !host_sc ? 8 : maxit;
         int stop = 0;
+        // the final residual (:52) from A*x kept alongside x (A*v_k is the pass's A*v_hat / alpha):
+        // no SpMV after the loop (HGM_OPT_LSQR_RES_IMG)
+        if (c->num.lsqr_res_img) {
+            img_ax = c->buf<double>("lsqr_ax", m + 1);
+            img_aw = c->buf<double>("lsqr_aw", m + 1);
+            lsqr_img<T>(c, m, wm, wm + m, coef, st, 0, img_ax, img_aw, true);
+        }
         for (k = 0; k < maxit && stop == 0;) {
             const int kend = std::min(maxit, k + batch);
             for (; k < kend; ++k) {
@@ -924,6 +932,7 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
                     lsqr_rot<T>(c, sl + S_BETA, wm + m, st, coef, phib, k, nb, tol); // :31-38, :44-46
                 }
                 lsqr_step<T>(c, n, x, w, v, wm + m, coef, st, k, xt, errh + k);     // :28, :40-41, :43
+                if (img_ax) lsqr_img<T>(c, m, wm, wm + m, coef, st, k, img_ax, img_aw, false);
                 if (dist_n(c)) allreduce(c, errh + k, 1);
                 if (stop) {
                     ++k;
@@ -1052,9 +1061,26 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         re.add(eh.data(), errh, sizeof(T) * nit);
         re.go();
         for (int i = 0; i < nit; ++i) err[i] = std::sqrt((double)eh[i]) / nxt;   // :43
-        apply_A<T>(c, A, x, t, EPI_RSUB, T(0), b);                            // :52 exact final residual
-        sumsq<T>(c, m, t, sl + S_RES);
-        res[nit - 1] = std::sqrt((double)read1<T>(c, sl + S_RES)) / nb;
+        if (img_ax) {
+            // :52 norm(b - A*x) from the kept image (replicated m-vector: no collective)
+            double* b64 = c->buf<double>("lsqr_b64", m + 1);
+            if constexpr (std::is_same_v<T, double>) {
+                HGM_HIP(hipMemcpyAsync(b64, b, sizeof(double) * m, hipMemcpyDeviceToDevice, c->stream));
+            } else {
+                convert_back<T>(c, m, b, b64);
+            }
+            double* rs = c->buf<double>("lsqr_rs", 1);
+            sumsq_diff<double>(c, m, b64, img_ax, rs);
+            double hv = 0;
+            Reader rr(c);
+            rr.add(&hv, rs, sizeof(double));
+            rr.go();
+            res[nit - 1] = std::sqrt(hv) / nb;
+        } else {
+            apply_A<T>(c, A, x, t, EPI_RSUB, T(0), b);                        // :52 exact final residual
+            sumsq<T>(c, m, t, sl + S_RES);
+            res[nit - 1] = std::sqrt((double)read1<T>(c, sl + S_RES)) / nb;
+        }
     }
     stage_out_n<T>(c, x_out, x, n, dev, po);
     if (err_out) std::memcpy(err_out, err.data(), sizeof(double) * nit);

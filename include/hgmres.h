@@ -159,7 +159,10 @@ enum hgm_ctx_option {
                                       row parity into a private accumulator array of the wave [0]: 1 the
                                       second row right after the first (membership per entry), 2 the second
                                       row from the lane after the first row's last pair, 3 as 1 with one
-                                      accumulator array (two add instructions per unit) */
+                                      accumulator array (two add instructions per unit) */,
+    HGM_OPT_LSQR_RES_IMG = 35      /* one-pass lsqr_solver: the exact final residual norm(b - A*x) of
+                                      lsqr_solver.m:52 from A*x kept in double alongside x (A*v_k is the
+                                      pass's A*v_hat / alpha) instead of one more SpMV [1] */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for
