@@ -356,6 +356,15 @@ def test_lsqr_one_pass_scalars_and_tol_stop(gpu_ctx, dtype):
                 vs_oracle=max(hist_dev(sd[1], ref[1]), hist_dev(sd[2], ref[2]), rel(sd[0], ref[0])))
     print(f"[lsqr one pass tol stop {dtype or 'f64'}] k={sd[3]} " + " ".join(f"{a}={v:.1e}" for a, v in devs.items()))
     assert devs["dev_vs_host"] <= bar
+    # the exact final residual (lsqr_solver.m:52) from the kept A*x image against one more SpMV
+    # (lsqr_res_img = 0): the same x, the last residual within the image's rounding
+    with gpu_ctx.options(fused_ab=1, lsqr_res_img=0):
+        expl = hgmres.lsqr_solver(A, b, xt, tol, 12, ctx=gpu_ctx, At=At)
+    assert np.array_equal(np.asarray(expl[0]), np.asarray(sd[0]))
+    assert np.array_equal(np.asarray(expl[2])[:-1], np.asarray(sd[2])[:-1])
+    dres = abs(expl[2][-1] - sd[2][-1]) / expl[2][-1]
+    print(f"[lsqr final residual image vs SpMV {dtype or 'f64'}] {dres:.1e}")
+    assert dres <= (1e-12 if dtype is None else 1e-4)
     # fp32: iterations 5-6 are past the fp32 envelope's 1e-5 (1e-3 from iteration 5)
     assert devs["vs_two_pass"] <= (TOL if dtype is None else 1e-3)
     assert devs["vs_oracle"] <= (TOL if dtype is None else 1e-3)
@@ -472,8 +481,8 @@ def test_fused_reduce_by_band_is_bitwise(gpu_ctx, N, na, dtype):
 # bitwise repeats; GKB in its production envelope), on geometries whose pairs overflow a chunk
 # (the plan cuts those runs) and ones that never do.
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("rp", [1, 2, 3])
-@pytest.mark.parametrize("N,na", [(256, 47), (512, 30), (100, 17), (200, 60)])
+@pytest.mark.parametrize("N,na,rp", [(256, 47, 1), (256, 47, 2), (256, 47, 3), (512, 30, 3), (100, 17, 3),
+                                     (200, 60, 3), (2048, 19, 3)])
 def test_fused_rowpair_gmres_matches_oracle(gpu_ctx, N, na, rp):
     A, B, b, xt = _device_problem(gpu_ctx, N, na)
     k = 20
@@ -486,6 +495,7 @@ def test_fused_rowpair_gmres_matches_oracle(gpu_ctx, N, na, rp):
         bq1, ab1 = hgmres.spmv_ab(A, B, b)
     with gpu_ctx.options(fused_ab=1, fused_rowpair=0):
         bq0, ab0 = hgmres.spmv_ab(A, B, b)
+
     for a_, b_ in zip(out, again):
         assert np.array_equal(np.asarray(a_), np.asarray(b_))
     dH = float(np.max(np.abs(out[-1] - ref2[-1])) / np.max(np.abs(ref2[-1])))
