@@ -581,7 +581,7 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
         case HGM_OPT_FUSED_PLAN_DEV: if (!b01) return bad("fused_plan_dev is 0 or 1"); n.fused_plan_dev = v != 0; break;
         case HGM_OPT_FUSED_REDUCE: if (!b01) return bad("fused_reduce is 0 or 1"); n.fused_reduce = (int)v; break;
         case HGM_OPT_FUSED_ROWPAIR:
-            if (!(v == 0 || v == 1 || v == 2 || v == 3)) return bad("fused_rowpair is 0, 1, 2 or 3");
+            if (!(v == 0 || v == 1 || v == 2 || v == 3 || v == 4)) return bad("fused_rowpair is 0 to 4");
             n.fused_rowpair = (int)v;
             break;
         case HGM_OPT_LSQR_RES_IMG: if (!b01) return bad("lsqr_res_img is 0 or 1"); n.lsqr_res_img = v != 0; break;

@@ -708,7 +708,7 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
             }
             return;
         }
-        if constexpr (RP == 1 || RP == 3) {
+        if constexpr (RP == 1 || RP >= 3) {
 #pragma unroll
             for (int u = 0; u < G / 2; ++u) {
                 // unit u = rows 2u, 2u+1 (a single row, or none, at the batch's end: lengths 0)
@@ -795,7 +795,7 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
         uint32_t k[G][NCH][EPL];
         bool ia[RP ? G / 2 : 1][EPL];             // (RP) entry of its unit's first row
         bool la_[RP == 2 ? G / 2 : 1];            // (RP 2) lane of its unit's first row
-        uint32_t kb[RP == 3 ? G / 2 : 1][EPL];    // (RP 3) the second row's accumulator address
+        uint32_t kb[RP >= 3 ? G / 2 : 1][EPL];    // (RP 3, 4) the second row's accumulator address
         if constexpr (RP == 2) {
 #pragma unroll
             for (int u = 0; u < G / 2; ++u) {
@@ -819,7 +819,7 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                 P[2 * u] = isA ? p : T(0);
                 P[2 * u + 1] = isA ? T(0) : p;
             }
-        } else if constexpr (RP == 1 || RP == 3) {
+        } else if constexpr (RP == 1 || RP >= 3) {
 #pragma unroll
             for (int u = 0; u < G / 2; ++u) {
                 const int la = b.len[2 * u], lab = la + b.len[2 * u + 1];
@@ -831,6 +831,21 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                     const bool in = (uint32_t)pos < (uint32_t)lab;
                     const uint32_t sl = e ? b.s[u][0] >> 16 : b.s[u][0] & 0xffffu;
                     const uint32_t dm = (uint32_t)(MAXR - 64 + ln) * (uint32_t)ES;
+                    if constexpr (RP == 4) {
+                        // RP 4 = RP 3 with the q reads through the two accumulator addresses (q = 0
+                        // at the dummies): the row split costs a second q read instead of the selects
+                        // of the products (AS == 1: the q and accumulator offsets coincide)
+                        static_assert(AS == 1, "row pairs: T accumulators");
+                        const uint32_t ka = inA ? sl : dm, kk = (in && !inA) ? sl : dm;
+                        const T qa = *reinterpret_cast<const T*>(reinterpret_cast<const char*>(qloc) + ka);
+                        const T qb = *reinterpret_cast<const T*>(reinterpret_cast<const char*>(qloc) + kk);
+                        pa = pa + b.v[u][0][e] * qa;
+                        pb = pb + b.v[u][0][e] * qb;
+                        k[u][0][e] = ka;
+                        kb[u][e] = kk;
+                        ia[u][e] = inA;
+                        continue;
+                    }
                     const uint32_t kq = in ? sl : dm;
                     const T p = b.v[u][0][e] * *reinterpret_cast<const T*>(reinterpret_cast<const char*>(qloc) + kq);
                     pa = pa + (inA ? p : T(0));
@@ -891,7 +906,7 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
         } else {
             zx = zx + zs * b.xv;
         }
-        if constexpr (RP == 3) {
+        if constexpr (RP >= 3) {
 #pragma unroll
             for (int u = 0; u < G / 2; ++u) {
                 const T za = lane_bcast(zs, 2 * u * GL), zb = lane_bcast(zs, (2 * u + 1) * GL);
@@ -1799,6 +1814,7 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
             if (MR == 1536) HGM_RWLR(AMP, 4, 1536, 8, 1, 2, true, 0, 3)
             if (MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 3)
         }
+        if (P->rowpair == 4 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 4)
         if (P->rowpair == 1 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 1)
         if (P->rowpair == 2 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 2)
         if (dry) return false;
