@@ -1576,7 +1576,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
     // (only for the shape the row-pair kernels exist for: 4 waves, 8-row batches, pairs, depth 2,
     // the production accumulation; any other options keep the plain row-wave plan)
     const int rpmode = c->num.fused_rowpair;
-    const bool rowpair = rpmode && c->num.fused_pairs && W == 4 && G == 8 && c->num.fused_depth == 2 &&
+    bool rowpair = rpmode && c->num.fused_pairs && W == 4 && G == 8 && c->num.fused_depth == 2 &&
                          c->num.fused_dbg == 0 && (es == 8 || c->num.fused_acc32 == 1) && maxlen + 1 <= 128;
     // does the unit (s, s+1) fit one chunk: mode 1 both rows contiguous from s's first pair (<= 128
     // entries), mode 2 each row from its own first pair (<= 64 lanes of pairs together)
@@ -1585,9 +1585,13 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
         const int64_t la = rp[s + 1] - rp[s] + (rp[s] & 1), lb = rp[s + 2] - rp[s + 1] + (rp[s + 1] & 1);
         return (la + 1) / 2 + (lb + 1) / 2 <= 64;
     };
+    // (rows so long that most pairs miss the chunk -- more than 64 runs in a wave after the cuts --
+    // keep the plain row-wave plan: every unit would be a single row)
     if (rowpair) {
+        std::vector<std::vector<int2>> wr1(wr.size());
+        std::atomic<bool> over{false};
         parallel_for((int64_t)wr.size(), [&](int64_t i) {
-            std::vector<int2> out;
+            std::vector<int2>& out = wr1[(size_t)i];
             for (const int2& r : wr[(size_t)i]) {
                 int s0 = r.x;
                 const int end = r.x + r.y;
@@ -1603,8 +1607,10 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
                 }
                 if (s0 < end) out.push_back(make_int2(s0, end - s0));
             }
-            wr[(size_t)i].swap(out);
+            if (out.size() > 64) over = true;
         });
+        if (over) rowpair = false;
+        else wr.swap(wr1);
     }
     std::vector<int32_t> wrun((size_t)nreg * W + 1, 0);
     for (size_t i = 0; i < wr.size(); ++i) {

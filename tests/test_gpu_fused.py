@@ -391,14 +391,16 @@ def test_fused_spmv_ab_fp32(gpu_ctx):
 
 
 def test_fused_failed_plan_is_retried_with_other_options(gpu_ctx):
-    """a refused plan (a 64 x 64 region holds more rays than four waves' LDS) is
-    remembered for THAT option tuple only; the default options then plan and run the one pass
-    on the same operator (kernel timing sees the fused class)."""
+    """a refused plan (two waves with 4-row batches: no kernel of that shape, at the
+    region and at its half) is remembered for THAT option tuple only; the default options then
+    plan and run the one pass on the same operator (kernel timing sees the fused class)."""
     A, B, b, xt = _device_problem(gpu_ctx, 256, 47)
     q = np.random.default_rng(2).standard_normal(A.shape[0])
     with gpu_ctx.options(fused_ab=0):
         _, ref = hgmres.spmv_ab(A, B, q)
-    with gpu_ctx.options(**_fused_opts(1, 64)):
+    with gpu_ctx.options(**_fused_opts(1, 32, waves=2, group=4)):
+        with pytest.raises((ValueError, hgmres.HgmError)):
+            hgmres.fused_plan_info(A, B)
         _, r64 = hgmres.spmv_ab(A, B, q)                  # refused: the two-pass product
     assert np.array_equal(r64, ref)
     gpu_ctx.kernel_timing(True)
