@@ -52,10 +52,14 @@ case "$recipe" in
     ;;
   shardbudget)
     # per-rank kernel costs of the pixel-sharded C4 solve at N = 2, 4, 8 (bench.py --shard1
-    # --shard-of N: rank 0's shard on a one-rank RCCL communicator), kernel trace + stats each
+    # --shard-of N: rank 0's shard on a one-rank RCCL communicator), kernel trace + stats each.
+    # gram_err_min=0: the error monitor keeps the Gram form on every iteration, as the global
+    # solve does (the shard's own problem would otherwise fall back to the explicit x-forming
+    # reconstruction, which runs on the step stream on a communicator)
     for nn in ${@:-2 4 8}; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/shard_of$nn" -o trace \
           -- python3 bench.py --workload c4 --shard1 --shard-of $nn --steps 5 --warmup 1 --no-cpu-baseline \
+             --opt gram_err_min=0 \
           > "$O/shard_of$nn.log" 2>&1 || { tail -20 "$O/shard_of$nn.log"; exit 1; }
       bench_line "$O/shard_of$nn.log" > "$O/${TAG}_bench_c4_shard_of$nn.json"
       cp "$(find "$O/shard_of$nn" -name '*kernel_stats.csv' | head -1)" "$O/${TAG}_c4_shard_of${nn}_kernel_stats.csv"
