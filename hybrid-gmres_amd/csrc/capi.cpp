@@ -579,7 +579,10 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             n.fused_acc32 = (int)v;
             break;
         case HGM_OPT_FUSED_PLAN_DEV: if (!b01) return bad("fused_plan_dev is 0 or 1"); n.fused_plan_dev = v != 0; break;
-        case HGM_OPT_FUSED_REDUCE: if (!b01) return bad("fused_reduce is 0 or 1"); n.fused_reduce = (int)v; break;
+        case HGM_OPT_FUSED_REDUCE:
+            if (!(v == 0 || v == 1 || v == 2 || v == 3 || v == 4)) return bad("fused_reduce is 0 to 4");
+            n.fused_reduce = (int)v;
+            break;
         case HGM_OPT_FUSED_ROWPAIR:
             if (!(v == 0 || v == 1 || v == 2 || v == 3 || v == 4)) return bad("fused_rowpair is 0 to 4");
             n.fused_rowpair = (int)v;

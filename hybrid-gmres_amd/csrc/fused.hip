@@ -344,7 +344,10 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(D <= 2 ? FB
 #endif
 // With zx_out, block 0 first adds the nzx regional shares of the side dot x_true'(B*q) (fixed
 // order) into *zx_out.
-template <int RG, typename T, typename TP = T>
+#ifndef HGM_FUSED_RB
+#define HGM_FUSED_RB 4
+#endif
+template <int RG, typename T, typename TP = T, int RB = HGM_FUSED_RB>
 __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* __restrict__ rs_ptr,
                                                      const int32_t* __restrict__ rs_slot,
                                                      const TP* __restrict__ part, T* __restrict__ w,
@@ -359,10 +362,6 @@ __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* _
         TP s = TP(0);
         const int64_t k0 = rs_ptr[i], k1 = rs_ptr[i + 1];
         int64_t k = k0 + gl;
-#ifndef HGM_FUSED_RB
-#define HGM_FUSED_RB 4
-#endif
-        constexpr int RB = HGM_FUSED_RB;
         for (; k + (RB - 1) * RG < k1; k += RB * RG) {   // RB slot reads, then RB partial reads in flight
             int32_t sl[RB];
             TP p[RB];
@@ -1954,6 +1953,19 @@ bool fused_pass(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArg
         launch(c, true, k_fused_reduce<HGM_FUSED_RG, T, double>, dim3(rgrid), dim3(BS), P->m,
                (const int64_t*)P->rs_ptr, (const int32_t*)P->rs_slot, (const double*)P->part, fa.w,
                (const T*)P->zx_part, (int)P->nreg, side ? fa.side_out : nullptr);
+    } else if (c->num.fused_reduce >= 2) {
+        // measured variants: fewer lanes per ray (the lanes of a wave then read adjacent rays' slots
+        // of one region: coalesced partial gathers), more loads in flight
+        const int rg = c->num.fused_reduce == 2 ? 1 : c->num.fused_reduce == 3 ? 2 : 4;
+        const unsigned g2 = (unsigned)std::max<int64_t>(1, (P->m * rg + BS - 1) / BS);
+#define HGM_RED(RGV, RBV)                                                                                        \
+    launch(c, true, k_fused_reduce<RGV, T, T, RBV>, dim3(g2), dim3(BS), P->m, (const int64_t*)P->rs_ptr,          \
+           (const int32_t*)P->rs_slot, (const T*)P->part, fa.w, (const T*)P->zx_part, (int)P->nreg,               \
+           side ? fa.side_out : nullptr)
+        if (rg == 1) HGM_RED(1, 8);
+        else if (rg == 2) HGM_RED(2, 8);
+        else HGM_RED(4, 4);
+#undef HGM_RED
     } else {
         launch(c, true, k_fused_reduce<HGM_FUSED_RG, T>, dim3(rgrid), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
                (const int32_t*)P->rs_slot, (const T*)P->part, fa.w, (const T*)P->zx_part, (int)P->nreg,

@@ -150,7 +150,8 @@ enum hgm_ctx_option {
                                       (an LDS bitmap per region) [1]; 0 the host build (same bytes) */
     HGM_OPT_FUSED_REDUCE = 32,     /* ... the row-wave pass's partial reduction: 1 by bands of 64 rays over
                                       runs of consecutive slots, 0 per ray through its slot list [0] (the
-                                      same sums: bitwise equal) */
+                                      same sums: bitwise equal); 2, 3, 4: per ray with 1, 2 or 4 lanes per
+                                      ray instead of 8 (another fixed order) */
     HGM_OPT_HOST_SPIN_US = 33      /* host waits (stream / event / ring polls): microseconds of pure spinning
                                       before each further poll yields the core (sched_yield) [200]; < 0: the
                                       blocking hipStreamSynchronize / hipEventSynchronize.  PROCESS-WIDE: the
