@@ -158,6 +158,39 @@ def dump_c2(name="c2_512.npz", k=20):
     print("wrote", name, "k", kk, "res", r[-1], "err", e[-1])
 
 
+def dump_c4u(name="c4u_2048.npz", k=20):
+    """The C4 unmatched line's path (bench.py --unmatched: ABgmres_nonhybrid_bounds with the
+    pixel-driven back-projector B != A', run_2D_phantom.m:13-15 / analyze_regularization.m B_pert)
+    at a quarter of C4's pixels with C4's 47 angles, so the device kernels are the ones C4 takes
+    (column-banded A, the paged streaming B kernel for its 94-entry rows over an L2-resident x):
+    2048^2, nnz(A) 2.5e8, nnz(B) 3.9e8, 20 iterations.  Operators pinned by CSR hash; b stored;
+    x as its norm plus every 997th entry."""
+    import gc
+    from oracle import parallel as OP
+    from hgmres.problems import pixel_driven_backprojector, shepp_logan, siddon_projector
+    A = siddon_projector(2048, 47)
+    hA = csr_hash(A)
+    xt = shepp_logan(2048).ravel(order="F")
+    OP.build()
+    PA = OP.ParallelCSR(A)
+    del A
+    gc.collect()
+    b_exact = PA @ xt
+    e = np.random.default_rng(0).standard_normal(PA.shape[0])
+    b = b_exact + e / np.linalg.norm(e) * 1e-2 * np.linalg.norm(b_exact)
+    B = pixel_driven_backprojector(2048, 47)
+    hB = csr_hash(B)
+    PB = OP.ParallelCSR(B)
+    del B
+    gc.collect()
+    x, err, res, kk, H = R.ABgmres_nonhybrid_bounds(PA, PB, b, xt, 0.0, k, return_H=True)
+    d = {"maxit": k, "N": 2048, "n_angles": 47, "A_sha256": hA, "B_sha256": hB, "b": b, "sample_stride": 997,
+         "abn_H": H, "abn_err": err, "abn_res": res, "abn_k": kk, "abn_xnorm": np.linalg.norm(x),
+         "abn_xs": x[::997].copy()}
+    np.savez_compressed(os.path.join(OUT, name), **d)
+    print("wrote", name, "k", kk, "res", res[-1], "err", err[-1])
+
+
 def dump_shaw_pipeline(name="shaw32_pipeline.npz"):
     """analyze_regularization.m on shaw(32) (restated, hgmres.regtools) with numpy noise and
     mismatch (MATLAB's randn stream cannot be reproduced): inputs, the oracle's outputs in the
@@ -193,6 +226,9 @@ if __name__ == "__main__":
         sys.exit(0)
     if sys.argv[1:] == ["c2"]:
         dump_c2()
+        sys.exit(0)
+    if sys.argv[1:] == ["c4u"]:
+        dump_c4u()
         sys.exit(0)
     if sys.argv[1:] == ["c4"]:
         dump_c4()

@@ -211,6 +211,40 @@ def test_c4_ab_gmres_full_size(gpu_ctx):
     gc.collect()
 
 
+def test_c4_unmatched_path_vs_oracle(gpu_ctx):
+    """The C4 unmatched line (bench.py --unmatched): AB-GMRES
+    (ABgmres_nonhybrid_bounds.m) with the pixel-driven back-projector B != A' (the reference's own
+    use case, run_2D_phantom.m:13-15), at a quarter of C4's pixels and C4's 47 angles so the device
+    takes C4's kernels (the column-banded A, the paged streaming B kernel for 94-entry rows over
+    an L2-resident x, two passes per step, the explicit n-space reconstruction), 20 iterations
+    against tests/golden/c4u_2048.npz (make_golden.py c4u) at the north_star bar."""
+    g = load_golden("c4u_2048.npz")
+    k, st = int(g["maxit"]), int(g["sample_stride"])
+    A = hgmres.SparseOperator.siddon(2048, 47, ctx=gpu_ctx)
+    B = hgmres.SparseOperator.pixel_backprojector(2048, 47, ctx=gpu_ctx)
+    assert B.nnz > 3.5e8
+    assert _csr_hash(A.to_scipy()) == str(g["A_sha256"])
+    assert _csr_hash(B.to_scipy()) == str(g["B_sha256"])
+    gc.collect()
+    b = g["b"]
+    xt = shepp_logan(2048).ravel(order="F")
+    o = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
+    x, e, r, kk, H = o[0], o[1], o[2], o[3], o[-1]
+    dH = H_rel(H, g["abn_H"])
+    print(f"[c4u 2048^2/47 unmatched k={kk}] |dH|/|H|={dH:.2e} |dx_s|={rel(x[::st], g['abn_xs']):.2e} "
+          f"res dev {float(np.max(np.abs(r - g['abn_res']) / g['abn_res'])):.2e} "
+          f"err dev {float(np.max(np.abs(e - g['abn_err']) / g['abn_err'])):.2e}")
+    assert kk == int(g["abn_k"]) == k
+    assert dH <= TOL, dH
+    hist_ok(e, g["abn_err"])
+    hist_ok(r, g["abn_res"])
+    assert abs(np.linalg.norm(x) - float(g["abn_xnorm"])) <= TOL * float(g["abn_xnorm"])
+    assert rel(x[::st], g["abn_xs"]) <= TOL
+    A.close()
+    B.close()
+    gc.collect()
+
+
 def test_c4_sharded_two_ranks_vs_oracle(tmp_path):
     """configs[3] as the N-GPU bench runs it, at full size: two pixel shards cut as bench.py
     build_shard cuts them (whole tile columns of the 4 x 4-tiled stored order, 64-column bands,
