@@ -39,7 +39,7 @@ for vname in variants:
     # | d<bits> (phase-skip timing)
     mf = re.fullmatch(r"f(\d+)(?:x(\d))?(?:r(\d+))?", vname)
     # row-wave pass: waves, region, rows per batch, ring depth, pairs
-    mw = re.fullmatch(r"w(\d)r(\d+)(?:g(\d))?(?:d(\d))?(?:p(\d))?(?:a(\d))?(?:q(\d))?", vname)
+    mw = re.fullmatch(r"w(\d)r(\d+)(?:g(\d+))?(?:d(\d))?(?:p(\d))?(?:a(\d))?(?:q(\d))?", vname)
     if vname.startswith("e"):                                   # row-wave pass, phase-skip timing
         o = dict(fused_ab=1, fused_kind=1, fused_dbg=int(vname[1:]), fused_acc32=1)
     elif mw:
