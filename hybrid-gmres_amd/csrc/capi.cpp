@@ -566,7 +566,7 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             n.fused_waves = (int)v;
             break;
         case HGM_OPT_FUSED_GROUP:
-            if (!(v == 4 || v == 8 || v == 16)) return bad("fused_group is 4, 8 or 16");
+            if (!(v == 4 || v == 8)) return bad("fused_group is 4 or 8");
             n.fused_group = (int)v;
             break;
         case HGM_OPT_FUSED_DEPTH:

@@ -497,7 +497,7 @@ __device__ __forceinline__ void swap16(float& a, float& b) {
 // a full wave reduction each (DPP tree + 8 readlanes).
 template <int G, typename T>
 __device__ __forceinline__ T rows_sum_t(T (&P)[G]) {
-    static_assert(G == 4 || G == 8 || G == 16, "rows per batch");
+    static_assert(G == 4 || G == 8, "rows per batch");
 #pragma unroll
     for (int i = 0; i < G / 2; ++i) {          // lane bit 5
         swap32(P[i], P[i + G / 2]);
@@ -508,22 +508,7 @@ __device__ __forceinline__ T rows_sum_t(T (&P)[G]) {
         swap16(P[i], P[i + G / 4]);
         P[i] = P[i] + P[i + G / 4];
     }
-    if constexpr (G == 16) {                   // lane bits 3 and 2, then the quad
-        const bool h3 = (threadIdx.x & 8) != 0, h2 = (threadIdx.x & 4) != 0;
-        T s2[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {          // bit 3: row_ror 8 (lane ^ 8 within the row)
-            const T a = h3 ? P[j + 2] : P[j];
-            const T t = h3 ? P[j] : P[j + 2];
-            s2[j] = a + dpp_mov<0x128>(t);
-        }
-        T s = h2 ? s2[1] : s2[0];              // bit 2: row_half_mirror (lane 7 - i of its half)
-        const T t = h2 ? s2[0] : s2[1];
-        s = s + dpp_mov<0x141>(t);
-        s += dpp_mov<0xB1>(s);                 // lane ^ 1
-        s += dpp_mov<0x4E>(s);                 // lane ^ 2
-        return s;
-    } else if constexpr (G == 8) {             // lane bit 3: row_ror 8 within 16-lane rows
+    if constexpr (G == 8) {                    // lane bit 3: row_ror 8 within 16-lane rows
         const bool hi = (threadIdx.x & 8) != 0;
         T s = hi ? P[1] : P[0];
         const T t = hi ? P[0] : P[1];
@@ -1590,8 +1575,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
     // (only for the shape the row-pair kernels exist for: 4 waves, 8-row batches, pairs, depth 2,
     // the production accumulation; any other options keep the plain row-wave plan)
     const int rpmode = c->num.fused_rowpair;
-    bool rowpair = rpmode && c->num.fused_pairs && W == 4 && (G == 8 || (G == 16 && rpmode == 3)) &&
-                   c->num.fused_depth == 2 &&
+    bool rowpair = rpmode && c->num.fused_pairs && W == 4 && G == 8 && c->num.fused_depth == 2 &&
                          c->num.fused_dbg == 0 && (es == 8 || c->num.fused_acc32 == 1) && maxlen + 1 <= 128;
     // does the unit (s, s+1) fit one chunk: mode 1 both rows contiguous from s's first pair (<= 128
     // entries), mode 2 each row from its own first pair (<= 64 lanes of pairs together)
@@ -1822,22 +1806,13 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
     if (P->rowpair) {
         // row pairs: the production accumulation, four waves, one chunk, 8-row batches, depth 2
         constexpr int AMP = sizeof(T) == 4 ? 1 : 0;
-        if (dbg || W != 4 || (G != 8 && G != 16) || NC != 1 || !PRm || D != 2 || am != AMP) {
+        if (dbg || W != 4 || G != 8 || NC != 1 || !PRm || D != 2 || am != AMP) {
             if (dry) return false;
             throw Error{HGM_E_ARG, "fused A*(B*q): row pairs take 4 waves, 8 rows, one chunk, pairs, depth 2, "
                                    "the production accumulation"};
         }
         // mode 3 (the default) for every four-wave shape; modes 1 and 2 (measured slower,
         // DESIGN.md §3.5) for the C4/C5 shape only
-        if (P->rowpair == 3 && G == 16) {     // 16-row batches (8 units): the C4/C5 shape, measured
-            if (MR == 2048) HGM_RWLR(AMP, 4, 2048, 16, 1, 2, true, 0, 3)
-            if (dry) return false;
-            throw Error{HGM_E_ARG, "fused A*(B*q): 16-row batches exist for the 2,048-slot shape only"};
-        }
-        if (G != 8) {
-            if (dry) return false;
-            throw Error{HGM_E_ARG, "fused A*(B*q): row pairs take 8 or 16 rows per batch"};
-        }
         if (P->rowpair == 3) {
             if (MR == 1088) HGM_RWLR(AMP, 4, 1088, 8, 1, 2, true, 0, 3)
             if (MR == 1344) HGM_RWLR(AMP, 4, 1344, 8, 1, 2, true, 0, 3)

@@ -140,8 +140,7 @@ enum hgm_ctx_option {
                                       1 row-wave pass (options 25-27) [1] */
     HGM_OPT_FUSED_WREGION = 25,    /* ... row-wave pass: pixel square (side) per workgroup [32] */
     HGM_OPT_FUSED_WAVES = 26,      /* ... row-wave pass: waves per workgroup, 1, 2 or 4 [4] */
-    HGM_OPT_FUSED_GROUP = 27,      /* ... row-wave pass: pixel rows per load batch, 4 or 8 [8]; 16 with the
-                                      row pairs (the 2,048-slot shape) */
+    HGM_OPT_FUSED_GROUP = 27,      /* ... row-wave pass: pixel rows per load batch, 4 or 8 [8] */
     HGM_OPT_FUSED_DEPTH = 28,      /* ... row-wave pass: batches in its load ring, 2..4 [2] */
     HGM_OPT_FUSED_PAIRS = 29,      /* ... row-wave pass: two entries per lane (16-byte value pairs) [1] */
     HGM_OPT_FUSED_ACC32 = 30       /* ... fp32 operators (lsqr_solver / lsmr_solver of BASELINE configs[4]): how
