@@ -1575,8 +1575,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
     // (only for the shape the row-pair kernels exist for: 4 waves, 8-row batches, pairs, depth 2,
     // the production accumulation; any other options keep the plain row-wave plan)
     const int rpmode = c->num.fused_rowpair;
-    bool rowpair = rpmode && c->num.fused_pairs && W == 4 && G == 8 &&
-                   (c->num.fused_depth == 2 || (c->num.fused_depth == 3 && rpmode >= 3)) &&
+    bool rowpair = rpmode && c->num.fused_pairs && W == 4 && G == 8 && c->num.fused_depth == 2 &&
                          c->num.fused_dbg == 0 && (es == 8 || c->num.fused_acc32 == 1) && maxlen + 1 <= 128;
     // does the unit (s, s+1) fit one chunk: mode 1 both rows contiguous from s's first pair (<= 128
     // entries), mode 2 each row from its own first pair (<= 64 lanes of pairs together)
@@ -1807,26 +1806,20 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
     if (P->rowpair) {
         // row pairs: the production accumulation, four waves, one chunk, 8-row batches, depth 2
         constexpr int AMP = sizeof(T) == 4 ? 1 : 0;
-        if (dbg || W != 4 || G != 8 || NC != 1 || !PRm || (D != 2 && D != 3) || am != AMP) {
+        if (dbg || W != 4 || G != 8 || NC != 1 || !PRm || D != 2 || am != AMP) {
             if (dry) return false;
             throw Error{HGM_E_ARG, "fused A*(B*q): row pairs take 4 waves, 8 rows, one chunk, pairs, depth 2, "
                                    "the production accumulation"};
         }
-        // mode 3 (the default) for every four-wave shape; modes 1 and 2 (measured slower,
-        // DESIGN.md §3.5) for the C4/C5 shape only
-        if (D == 3) {                        // a deeper load ring (measured variant, 2,048 slots)
-            if (P->rowpair == 3 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 3, true, 0, 3)
-            if (P->rowpair == 4 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 3, true, 0, 4)
-            if (dry) return false;
-            throw Error{HGM_E_ARG, "fused A*(B*q): row pairs with ring depth 3: modes 3 and 4, 2,048 slots only"};
+        // mode 4 (the default) for every four-wave shape; modes 1-3 (measured variants)
+        // for the C4/C5 shape only
+        if (P->rowpair == 4) {
+            if (MR == 1088) HGM_RWLR(AMP, 4, 1088, 8, 1, 2, true, 0, 4)
+            if (MR == 1344) HGM_RWLR(AMP, 4, 1344, 8, 1, 2, true, 0, 4)
+            if (MR == 1536) HGM_RWLR(AMP, 4, 1536, 8, 1, 2, true, 0, 4)
+            if (MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 4)
         }
-        if (P->rowpair == 3) {
-            if (MR == 1088) HGM_RWLR(AMP, 4, 1088, 8, 1, 2, true, 0, 3)
-            if (MR == 1344) HGM_RWLR(AMP, 4, 1344, 8, 1, 2, true, 0, 3)
-            if (MR == 1536) HGM_RWLR(AMP, 4, 1536, 8, 1, 2, true, 0, 3)
-            if (MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 3)
-        }
-        if (P->rowpair == 4 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 4)
+        if (P->rowpair == 3 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 3)
         if (P->rowpair == 1 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 1)
         if (P->rowpair == 2 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 2)
         if (dry) return false;

@@ -91,7 +91,7 @@ struct Numerics {
     bool fused_pairs = true;        // ... row-wave pass: two entries per lane
     int fused_acc32 = 1;            // ... fp32 row-wave pass: 0 ds_add_f32, 1 read-add-write, 2 fp64 accumulators
     bool fused_plan_dev = true;     // ... row-wave plan's ray sets built on the device (false: the host build)
-    int fused_rowpair = 3;          // ... row-wave pass: units of two consecutive rows per chunk (k_fused_rw RP 1/2/3)
+    int fused_rowpair = 4;          // ... row-wave pass: units of two consecutive rows per chunk (k_fused_rw RP 1-4)
     int fused_reduce = 0;           // ... row-wave partial reduction: 0 by ray (rs_slot), 1 by ray band (runs;
                                     //     bitwise equal, measured 2-4% slower pass at C4, profiles/r4_c4_reduce_band_ab.jsonl)
     bool lsqr_res_img = true;       // one-pass LSQR: final residual from the A*x image (no SpMV)

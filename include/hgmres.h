@@ -156,13 +156,13 @@ enum hgm_ctx_option {
                                       before each further poll yields the core (sched_yield) [200]; < 0: the
                                       blocking hipStreamSynchronize / hipEventSynchronize.  PROCESS-WIDE: the
                                       last value set on any context applies to every context */,
-    HGM_OPT_FUSED_ROWPAIR = 34     /* ... row-wave pass: two consecutive pixel rows per 128-entry chunk [3]:
-                                      0 one row per chunk; 3 the second row right after the first, one
-                                      accumulator array per wave, the two rows added by two instructions;
-                                      1 (as 3 with a private array per row parity), 2 (the second row
-                                      from the lane after the first row's last pair) and 4 (as 3 with the
-                                      row split on the q reads) are measured variants of the 2048-slot
-                                      shape only */,
+    HGM_OPT_FUSED_ROWPAIR = 34     /* ... row-wave pass: two consecutive pixel rows per 128-entry chunk [4]:
+                                      0 one row per chunk; 4 the second row right after the first, one
+                                      accumulator array per wave, the two rows' q reads and adds by two
+                                      instructions each (other lanes on their dummy slot); 1 (a private
+                                      array per row parity), 2 (the second row from the lane after the first
+                                      row's last pair) and 3 (the row split by selects of the products) are
+                                      measured variants of the 2048-slot shape only */,
     HGM_OPT_LSQR_RES_IMG = 35      /* one-pass lsqr_solver: the exact final residual norm(b - A*x) of
                                       lsqr_solver.m:52 from A*x kept in double alongside x (A*v_k is the
                                       pass's A*v_hat / alpha) instead of one more SpMV [1] */

@@ -483,8 +483,8 @@ def test_fused_reduce_by_band_is_bitwise(gpu_ctx, N, na, dtype):
 # bitwise repeats; GKB in its production envelope), on geometries whose pairs overflow a chunk
 # (the plan cuts those runs) and ones that never do.
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("N,na,rp", [(256, 47, 1), (256, 47, 2), (256, 47, 3), (512, 30, 3), (100, 17, 3),
-                                     (200, 60, 3), (2048, 19, 3)])
+@pytest.mark.parametrize("N,na,rp", [(256, 47, 1), (256, 47, 2), (256, 47, 3), (256, 47, 4), (512, 30, 4),
+                                     (100, 17, 4), (200, 60, 4), (2048, 19, 4)])
 def test_fused_rowpair_gmres_matches_oracle(gpu_ctx, N, na, rp):
     A, B, b, xt = _device_problem(gpu_ctx, N, na)
     k = 20
@@ -511,7 +511,7 @@ def test_fused_rowpair_gmres_matches_oracle(gpu_ctx, N, na, rp):
     assert rel(out[0], xo) <= TOL and hist_dev(out[1], eo) <= TOL and hist_dev(out[2], ro) <= TOL
 
 
-@pytest.mark.parametrize("rp", [1, 2, 3])
+@pytest.mark.parametrize("rp", [1, 2, 3, 4])
 @pytest.mark.parametrize("dtype", [None, "f32"])
 def test_fused_rowpair_gkb_matches_oracle(gpu_ctx, dtype, rp):
     A, At, b, xt = _gkb_pair(gpu_ctx, 256, 47, dtype=dtype)
