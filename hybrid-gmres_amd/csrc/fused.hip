@@ -834,14 +834,13 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                         // RP 4 = RP 3 with the q reads through the two accumulator addresses (q = 0
                         // at the dummies): the row split costs a second q read instead of the selects
                         // of the products (AS == 1: the q and accumulator offsets coincide)
-                        static_assert(AS == 1, "row pairs: T accumulators");
                         const uint32_t ka = inA ? sl : dm, kk = (in && !inA) ? sl : dm;
                         const T qa = *reinterpret_cast<const T*>(reinterpret_cast<const char*>(qloc) + ka);
                         const T qb = *reinterpret_cast<const T*>(reinterpret_cast<const char*>(qloc) + kk);
                         pa = pa + b.v[u][0][e] * qa;
                         pb = pb + b.v[u][0][e] * qb;
-                        k[u][0][e] = ka;
-                        kb[u][e] = kk;
+                        k[u][0][e] = ka * AS;              // (AS == 2: fp64 accumulators of an fp32 pass)
+                        kb[u][e] = kk * AS;
                         ia[u][e] = inA;
                         continue;
                     }
@@ -1576,7 +1575,9 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
     // the production accumulation; any other options keep the plain row-wave plan)
     const int rpmode = c->num.fused_rowpair;
     bool rowpair = rpmode && c->num.fused_pairs && W == 4 && G == 8 && c->num.fused_depth == 2 &&
-                         c->num.fused_dbg == 0 && (es == 8 || c->num.fused_acc32 == 1) && maxlen + 1 <= 128;
+                         c->num.fused_dbg == 0 &&
+                   (es == 8 || c->num.fused_acc32 == 1 || (c->num.fused_acc32 == 2 && rpmode == 4)) &&
+                   maxlen + 1 <= 128;
     // does the unit (s, s+1) fit one chunk: mode 1 both rows contiguous from s's first pair (<= 128
     // entries), mode 2 each row from its own first pair (<= 64 lanes of pairs together)
     auto fits = [&](int64_t s) {
@@ -1806,6 +1807,9 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
     if (P->rowpair) {
         // row pairs: the production accumulation, four waves, one chunk, 8-row batches, depth 2
         constexpr int AMP = sizeof(T) == 4 ? 1 : 0;
+        if constexpr (sizeof(T) == 4)            // fp64 accumulators (ds_add_f64) with mode 4: measured variant
+            if (am == 2 && P->rowpair == 4 && !dbg && W == 4 && G == 8 && NC == 1 && PRm && D == 2 && MR == 2048)
+                HGM_RWLR(2, 4, 2048, 8, 1, 2, true, 0, 4)
         if (dbg || W != 4 || G != 8 || NC != 1 || !PRm || D != 2 || am != AMP) {
             if (dry) return false;
             throw Error{HGM_E_ARG, "fused A*(B*q): row pairs take 4 waves, 8 rows, one chunk, pairs, depth 2, "
