@@ -133,7 +133,15 @@ static void ensure_stage(hgm_ctx* c, size_t bytes) {
 // hands the core to RCCL's proxy and other runnable threads; with nothing else runnable the yield
 // returns at once, so the wake-up latency stays that of the spin.  A negative value waits with the
 // blocking hipStreamSynchronize / hipEventSynchronize instead.
-std::atomic<int> g_host_spin_us{200};
+// Default: 200 us, or the blocking waits when the process may run on fewer than 4 cores (ranks
+// pinned together: 2 ranks on 2 cores ran the 2-rank C3 solve 10-17 % faster blocking,
+// profiles/r5_pinned_2rank.jsonl).
+static int host_spin_default() {
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0 && CPU_COUNT(&cs) < 4) return -1;
+    return 200;
+}
+std::atomic<int> g_host_spin_us{host_spin_default()};
 
 void HostPause::operator()() {
     if (++polls < 64) return;

@@ -153,7 +153,8 @@ enum hgm_ctx_option {
                                       same sums: bitwise equal); 2, 3, 4: per ray with 1, 2 or 4 lanes per
                                       ray instead of 8 (another fixed order) */
     HGM_OPT_HOST_SPIN_US = 33      /* host waits (stream / event / ring polls): microseconds of pure spinning
-                                      before each further poll yields the core (sched_yield) [200]; < 0: the
+                                      before each further poll yields the core (sched_yield) [200; -1 when
+                                      the process's CPU affinity holds fewer than 4 cores]; < 0: the
                                       blocking hipStreamSynchronize / hipEventSynchronize.  PROCESS-WIDE: the
                                       last value set on any context applies to every context */,
     HGM_OPT_FUSED_ROWPAIR = 34     /* ... row-wave pass: two consecutive pixel rows per 128-entry chunk [4]:

@@ -110,3 +110,22 @@ def test_empty_operator_breaks_at_once(gpu_ctx):
         _same(a, b_)
     with pytest.raises(hgmres.OutputNotAssigned):
         hgmres.hybrid_ab_gmres_rtp(A, B, b, xt, 0.0, 3, 1e-2, ctx=gpu_ctx)
+
+
+def test_host_spin_default_follows_cpu_affinity(gpu_ctx, tmp_path):
+    """ADVICE r4 (host spins): the host waits spin then yield by default, and wait blocking when
+    the process may run on fewer than 4 cores (capi.cpp host_spin_default)."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    pkg = os.path.join(ROOT, "hybrid-gmres_amd")
+    ncpu = len(os.sched_getaffinity(0))
+    assert gpu_ctx.get_option("host_spin_us") == (200 if ncpu >= 4 else -1)
+    code = (f"import os, sys; sys.path.insert(0, {pkg!r})\n"
+            "os.sched_setaffinity(0, sorted(os.sched_getaffinity(0))[:2])\n"
+            "import hgmres\n"
+            "print(int(hgmres.Context(0).get_option('host_spin_us')))\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip().splitlines()[-1] == "-1"
