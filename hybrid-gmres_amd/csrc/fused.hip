@@ -910,6 +910,20 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                 const T za = lane_bcast(zs, 2 * u * GL), zb = lane_bcast(zs, (2 * u + 1) * GL);
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {         // the unit's first row, then its second
+                    if constexpr (AM == 1 && EPL == 2) {
+                        // read-add-write of the row's two entries per lane with ONE round trip: both
+                        // reads, then both writes. Within one pixel row the slots are distinct, so
+                        // only a lane whose two entries both sit on its dummy slot reads it twice
+                        // (the dummy's value is never used): the same sums as one entry at a time.
+                        const T sj = h ? zb : za;
+                        TA* p0 = reinterpret_cast<TA*>(reinterpret_cast<char*>(ac) + (h ? kb[u][0] : k[u][0][0]));
+                        TA* p1 = reinterpret_cast<TA*>(reinterpret_cast<char*>(ac) + (h ? kb[u][1] : k[u][0][1]));
+                        const T o0 = *p0, o1 = *p1;
+                        const T t0 = b.v[u][0][0] * sj, t1 = b.v[u][0][1] * sj;
+                        *p0 = o0 + t0;
+                        *p1 = o1 + t1;
+                        continue;
+                    }
 #pragma unroll
                     for (int e = 0; e < EPL; ++e) {
                         const T sj = h ? zb : za;
