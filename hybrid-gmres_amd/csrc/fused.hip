@@ -531,6 +531,14 @@ __device__ __forceinline__ T rows_sum_t(T (&P)[G]) {
 // sums are bitwise reproducible (test_gpu_fused.py repeats every product and solve bit for bit).
 // Breaking any of (1)-(3) (shared accumulators, a second wave, duplicate slots per row) would
 // make the order depend on timing.
+// Row-pair mode 4's products and fp32 accumulator updates as fused multiply-adds (one rounding per
+// term instead of two; the library otherwise builds with -ffp-contract=off for MATLAB's epilogues).
+#ifndef HGM_FUSED_FMA
+#define HGM_FUSED_FMA 1
+#endif
+__device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
 template <typename T>
 __device__ __forceinline__ void lds_add(T* p, T t) {
     (void)__hip_atomic_fetch_add(p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -837,8 +845,13 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                         const uint32_t ka = inA ? sl : dm, kk = (in && !inA) ? sl : dm;
                         const T qa = *reinterpret_cast<const T*>(reinterpret_cast<const char*>(qloc) + ka);
                         const T qb = *reinterpret_cast<const T*>(reinterpret_cast<const char*>(qloc) + kk);
-                        pa = pa + b.v[u][0][e] * qa;
-                        pb = pb + b.v[u][0][e] * qb;
+                        if constexpr (HGM_FUSED_FMA) {   // (one rounding per term: half the VALU)
+                            pa = fma_t(b.v[u][0][e], qa, pa);
+                            pb = fma_t(b.v[u][0][e], qb, pb);
+                        } else {
+                            pa = pa + b.v[u][0][e] * qa;
+                            pb = pb + b.v[u][0][e] * qb;
+                        }
                         k[u][0][e] = ka * AS;              // (AS == 2: fp64 accumulators of an fp32 pass)
                         kb[u][e] = kk * AS;
                         ia[u][e] = inA;
@@ -919,9 +932,14 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                         TA* p0 = reinterpret_cast<TA*>(reinterpret_cast<char*>(ac) + (h ? kb[u][0] : k[u][0][0]));
                         TA* p1 = reinterpret_cast<TA*>(reinterpret_cast<char*>(ac) + (h ? kb[u][1] : k[u][0][1]));
                         const T o0 = *p0, o1 = *p1;
-                        const T t0 = b.v[u][0][0] * sj, t1 = b.v[u][0][1] * sj;
-                        *p0 = o0 + t0;
-                        *p1 = o1 + t1;
+                        if constexpr (HGM_FUSED_FMA && RP == 4) {
+                            *p0 = fma_t(b.v[u][0][0], sj, o0);
+                            *p1 = fma_t(b.v[u][0][1], sj, o1);
+                        } else {
+                            const T t0 = b.v[u][0][0] * sj, t1 = b.v[u][0][1] * sj;
+                            *p0 = o0 + t0;
+                            *p1 = o1 + t1;
+                        }
                         continue;
                     }
 #pragma unroll
