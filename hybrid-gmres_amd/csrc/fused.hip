@@ -345,7 +345,7 @@ __global__ __launch_bounds__(FBS) __attribute__((amdgpu_waves_per_eu(D <= 2 ? FB
 // With zx_out, block 0 first adds the nzx regional shares of the side dot x_true'(B*q) (fixed
 // order) into *zx_out.
 #ifndef HGM_FUSED_RB
-#define HGM_FUSED_RB 4
+#define HGM_FUSED_RB 16
 #endif
 template <int RG, typename T, typename TP = T, int RB = HGM_FUSED_RB>
 __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* __restrict__ rs_ptr,
@@ -362,7 +362,23 @@ __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* _
         TP s = TP(0);
         const int64_t k0 = rs_ptr[i], k1 = rs_ptr[i + 1];
         int64_t k = k0 + gl;
-        for (; k + (RB - 1) * RG < k1; k += RB * RG) {   // RB slot reads, then RB partial reads in flight
+        if constexpr (RB >= 8) {
+            // a ray's partials in batches of RB per lane with the batch's tail clamped to the ray's
+            // last slot (read again, not added): every slot read, then every partial read in flight
+            // (C4: ~14 partials per lane, one batch instead of three batches and a serial tail)
+            for (; k < k1; k += RB * RG) {
+                int32_t sl[RB];
+                TP p[RB];
+#pragma unroll
+                for (int u = 0; u < RB; ++u) sl[u] = rs_slot[std::min<int64_t>(k + u * RG, k1 - 1)];
+#pragma unroll
+                for (int u = 0; u < RB; ++u) p[u] = part[sl[u]];
+#pragma unroll
+                for (int u = 0; u < RB; ++u)
+                    if (k + u * RG < k1) s += p[u];
+            }
+        }
+        for (; RB < 8 && k + (RB - 1) * RG < k1; k += RB * RG) {   // RB slot reads, then RB partial reads in flight
             int32_t sl[RB];
             TP p[RB];
 #pragma unroll
