@@ -83,10 +83,11 @@ def _gkb_check(fn, A, out, seeds=tuple(range(1, 9)), k=100.0, nhist=2, label="")
     oracle `fn(A)`.  Tolerance per quantity and per history entry: max(1e-10, k x the largest
     spread of the oracle itself under the rounding-error model (8 seeds: LSQR without
     reorthogonalisation amplifies rounding chaotically)), capped at GKB_CAP = 1e-6.  Entries
-    whose envelope would exceed the cap (late iterations where any two correct fp64 summation
-    orders disagree by more than 1e-8) are not judged here: the fixed-order parity mode
-    (tests/test_gpu_parity_mode.py) holds every entry, and x, at 1e-10.  Measured deviations
-    are printed (pytest -s / -rA) so the margin is visible."""
+    whose envelope exceeds the cap (late iterations where any two correct fp64 summation orders
+    disagree by more than 1e-8) are held to the envelope alone (k x the oracle's own spread, no
+    absolute bar), and the fixed-order parity mode (tests/test_gpu_parity_mode.py) holds every
+    entry, and x, at 1e-10.  Measured deviations are printed (pytest -s / -rA) so the margin is
+    visible."""
     ref = fn(A)
     sx = 0.0
     sh = [np.zeros(np.size(r_)) for r_ in ref[1:1 + nhist]]
@@ -103,6 +104,11 @@ def _gkb_check(fn, A, out, seeds=tuple(range(1, 9)), k=100.0, nhist=2, label="")
     msg = [f"x: dev {dx:.2e} tol {min(tx, GKB_CAP):.2e}" + (" (over cap: parity mode)" if tx > GKB_CAP else "")]
     if tx <= GKB_CAP:
         assert dx <= tx, (dx, tx)
+    else:
+        #  past the cap the production x is still held to k x the oracle's own
+        # spread under the rounding model: the deviation is the recurrences' sensitivity to rounding,
+        # which any two correct fp64 summation orders show as well
+        assert dx <= tx, (dx, tx)
     for i in range(nhist):
         a_, r_ = np.asarray(out[1 + i]), np.asarray(ref[1 + i])
         assert a_.shape == r_.shape
@@ -111,8 +117,12 @@ def _gkb_check(fn, A, out, seeds=tuple(range(1, 9)), k=100.0, nhist=2, label="")
         judged = ok & (tol_v <= GKB_CAP)
         d = np.abs(a_ - r_) / np.maximum(np.abs(r_), 1e-300)
         assert np.all(d[judged] <= tol_v[judged]), (np.max(d[judged] / tol_v[judged]), i)
+        # the entries past the cap: within k x the oracle's rounding spread (no absolute bar)
+        late = ok & ~judged
+        assert np.all(d[late] <= tol_v[late]), (np.max(d[late] / tol_v[late]), i)
+        ratio = np.max(d[late] / tol_v[late] * k, initial=0.0)
         msg.append(f"hist{i}: max dev {np.max(d[judged], initial=0):.2e} over {int(judged.sum())} judged entries, "
-                   f"{int((ok & ~judged).sum())} left to parity mode")
+                   f"{int(late.sum())} past the cap at <= {ratio:.1f}x the oracle's own spread (bar {k:.0f}x)")
     print(f"[gkb {label}] " + "; ".join(msg))
     return ref
 
