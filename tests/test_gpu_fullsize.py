@@ -245,6 +245,39 @@ def test_c4_unmatched_path_vs_oracle(gpu_ctx):
     gc.collect()
 
 
+def test_c4_unmatched_full_size_vs_oracle(gpu_ctx):
+    """the C4 unmatched line itself (bench.py --workload c4 --unmatched) at full
+    size: 4096^2 / 47 angles, the pixel-driven back-projector B != A' (1.58e9 entries), 20
+    iterations of ABgmres_nonhybrid_bounds against tests/golden/c4u_4096.npz (make_c4u_4096.py: the
+    oracle restatement on both operators, pinned by CSR hash to the numpy generators) at the
+    north_star bar."""
+    g = load_golden("c4u_4096.npz")
+    k, st = int(g["maxit"]), int(g["sample_stride"])
+    A = hgmres.SparseOperator.siddon(4096, 47, ctx=gpu_ctx)
+    assert _csr_hash(A.to_scipy()) == str(g["A_sha256"])
+    gc.collect()
+    B = hgmres.SparseOperator.pixel_backprojector(4096, 47, ctx=gpu_ctx)
+    assert _csr_hash(B.to_scipy()) == str(g["B_sha256"])
+    gc.collect()
+    b = g["b"]
+    xt = shepp_logan(4096).ravel(order="F")
+    o = hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True)
+    x, e, r, kk, H = o[0], o[1], o[2], o[3], o[-1]
+    dH = H_rel(H, g["abn_H"])
+    print(f"[c4u 4096^2/47 unmatched k={kk}] |dH|/|H|={dH:.2e} |dx_s|={rel(x[::st], g['abn_xs']):.2e} "
+          f"res dev {float(np.max(np.abs(r - g['abn_res']) / g['abn_res'])):.2e} "
+          f"err dev {float(np.max(np.abs(e - g['abn_err']) / g['abn_err'])):.2e}")
+    assert kk == int(g["abn_k"]) == k
+    assert dH <= TOL, dH
+    hist_ok(e, g["abn_err"])
+    hist_ok(r, g["abn_res"])
+    assert abs(np.linalg.norm(x) - float(g["abn_xnorm"])) <= TOL * float(g["abn_xnorm"])
+    assert rel(x[::st], g["abn_xs"]) <= TOL
+    A.close()
+    B.close()
+    gc.collect()
+
+
 def test_c4_sharded_two_ranks_vs_oracle(tmp_path):
     """configs[3] as the N-GPU bench runs it, at full size: two pixel shards cut as bench.py
     build_shard cuts them (whole tile columns of the 4 x 4-tiled stored order, 64-column bands,
