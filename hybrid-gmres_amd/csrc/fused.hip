@@ -547,6 +547,11 @@ __device__ __forceinline__ T rows_sum_t(T (&P)[G]) {
 // sums are bitwise reproducible (test_gpu_fused.py repeats every product and solve bit for bit).
 // Breaking any of (1)-(3) (shared accumulators, a second wave, duplicate slots per row) would
 // make the order depend on timing.
+// cache policy of the row-wave pass's entry stream (values, slots): the default (0); nt (2) measured
+// 1.7-2.2 % slower (a unit's chunk shares its boundary lines with the next unit's)
+#ifndef HGM_RW_AUX
+#define HGM_RW_AUX 0
+#endif
 // Row-pair mode 4's products and fp32 accumulator updates as fused multiply-adds (one rounding per
 // term instead of two; the library otherwise builds with -ffp-contract=off for MATLAB's epilogues).
 #ifndef HGM_FUSED_FMA
@@ -719,15 +724,15 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                 const int base = (isA ? relA : relB) + 2 * li;      // entry index from eb
                 const int vo = in ? base * ES : (1 << 30), lo = in ? base * 2 : (1 << 30);
                 if constexpr (ES == 8) {
-                    const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, vo, 0, 2));
+                    const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, vo, 0, HGM_RW_AUX));
                     b.v[u][0][0] = t.x;
                     b.v[u][0][EPL - 1] = t.y;
                 } else {
-                    const float2 t = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rv, vo, 0, 2));
+                    const float2 t = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rv, vo, 0, HGM_RW_AUX));
                     b.v[u][0][0] = t.x;
                     b.v[u][0][EPL - 1] = t.y;
                 }
-                b.s[u][0] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, lo, 0, 2);
+                b.s[u][0] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, lo, 0, HGM_RW_AUX);
             }
             return;
         }
@@ -745,15 +750,15 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                 const bool in = 2 * ln < (int)(e2 - e0) + off;
                 const int vo = in ? 2 * ln * ES : (1 << 30), lo = in ? 2 * ln * 2 : (1 << 30);
                 if constexpr (ES == 8) {
-                    const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, vo, rel * ES, 2));
+                    const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, vo, rel * ES, HGM_RW_AUX));
                     b.v[u][0][0] = t.x;
                     b.v[u][0][EPL - 1] = t.y;
                 } else {
-                    const float2 t = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rv, vo, rel * ES, 2));
+                    const float2 t = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rv, vo, rel * ES, HGM_RW_AUX));
                     b.v[u][0][0] = t.x;
                     b.v[u][0][EPL - 1] = t.y;
                 }
-                b.s[u][0] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, lo, rel * 2, 2);
+                b.s[u][0] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, lo, rel * 2, HGM_RW_AUX);
             }
             return;
         }
@@ -777,15 +782,15 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                     const bool in = !HGM_RW_MASK_LOADS || 2 * ln + CH * c < len + off;
                     const int vo = in ? (2 * ln + CH * c) * ES : (1 << 30), lo = in ? (2 * ln + CH * c) * 2 : (1 << 30);
                     if constexpr (ES == 8) {
-                        const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, vo, rel * ES, 2));
+                        const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rv, vo, rel * ES, HGM_RW_AUX));
                         b.v[j][c][0] = t.x;
                         b.v[j][c][EPL - 1] = t.y;
                     } else {
-                        const float2 t = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rv, vo, rel * ES, 2));
+                        const float2 t = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rv, vo, rel * ES, HGM_RW_AUX));
                         b.v[j][c][0] = t.x;
                         b.v[j][c][EPL - 1] = t.y;
                     }
-                    b.s[j][c] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, lo, rel * 2, 2);
+                    b.s[j][c] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rl, lo, rel * 2, HGM_RW_AUX);
                 }
             } else {
                 const int64_t e0 = readlane64(rpv, j), e1 = readlane64(rpv, j + 1);
