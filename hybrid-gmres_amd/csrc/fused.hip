@@ -552,6 +552,11 @@ __device__ __forceinline__ T rows_sum_t(T (&P)[G]) {
 #ifndef HGM_RW_AUX
 #define HGM_RW_AUX 0
 #endif
+// the regions' partials are written once and read once, by the reduction: non-temporal stores
+// (fp64 pass + reduction 2.244 vs 2.252 ms, fp32 equal; profiles/r5_micro_part_nt_ab.txt)
+#ifndef HGM_PART_NT
+#define HGM_PART_NT 1
+#endif
 // Row-pair mode 4's products and fp32 accumulator updates as fused multiply-adds (one rounding per
 // term instead of two; the library otherwise builds with -ffp-contract=off for MATLAB's epilogues).
 #ifndef HGM_FUSED_FMA
@@ -1062,7 +1067,8 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
             t += acc[w][0][k];
             if constexpr (NA == 2) t += acc[w][1][k];
         }
-        part[pb + k] = t;
+        if constexpr (HGM_PART_NT) __builtin_nontemporal_store(t, &part[pb + k]);
+        else part[pb + k] = t;
     }
     if (zx_part) {
         __syncthreads();
