@@ -596,6 +596,7 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
             n.fused_rowpair = (int)v;
             break;
         case HGM_OPT_LSQR_RES_IMG: if (!b01) return bad("lsqr_res_img is 0 or 1"); n.lsqr_res_img = v != 0; break;
+        case HGM_OPT_LSMR_FUSE_NMON: if (!b01) return bad("lsmr_fuse_nmon is 0 or 1"); n.lsmr_fuse_nmon = v != 0; break;
         case HGM_OPT_HOST_SPIN_US:
             if (!(v == std::floor(v) && std::fabs(v) <= 1e9)) return bad("host_spin_us is an integer");
             g_host_spin_us.store((int)v);
@@ -643,6 +644,7 @@ HGM_API int hgm_ctx_get_option(const hgm_ctx* c, int option, double* v) {
         case HGM_OPT_FUSED_REDUCE: *v = n.fused_reduce; break;
         case HGM_OPT_FUSED_ROWPAIR: *v = n.fused_rowpair; break;
         case HGM_OPT_LSQR_RES_IMG: *v = n.lsqr_res_img; break;
+        case HGM_OPT_LSMR_FUSE_NMON: *v = n.lsmr_fuse_nmon; break;
         case HGM_OPT_HOST_SPIN_US: *v = g_host_spin_us.load(); break;
         default: return HGM_E_ARG;
     }

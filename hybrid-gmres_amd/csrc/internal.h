@@ -95,6 +95,7 @@ struct Numerics {
     int fused_reduce = 0;           // ... row-wave partial reduction: 0 by ray (rs_slot), 1 by ray band (runs;
                                     //     bitwise equal, measured 2-4% slower pass at C4, profiles/r4_c4_reduce_band_ab.jsonl)
     bool lsqr_res_img = true;       // one-pass LSQR: final residual from the A*x image (no SpMV)
+    bool lsmr_fuse_nmon = true;     // one-pass fp32 LSMR: the n-space step and monitor in one launch
     int krylov_pad = -1;            // Krylov basis column padding (elements; -1 auto, kernels.hip krylov_ld)
     int fused_dbg = 0;              // ... timing experiments: skip phases (wrong results)
 };
@@ -407,6 +408,12 @@ void lsmr_rot(hgm_ctx* c, const T* ssb, const T* ssa, double* st, T* coef, doubl
 template <typename T>
 void lsmr_step(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, T* v, const T* ssa, const T* coef, const double* st,
                int k, const T* xt, T* err_out);
+// lsmr_step + lsmr_monitor_r in one launch (same bits; HGM_OPT_LSMR_FUSE_NMON); false when it does
+// not apply (no x_true, a small n, unaligned vectors): the caller runs the two
+template <typename T>
+bool lsmr_step_mon(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, T* v, const T* ssa, const T* coef, const double* st,
+                   int k, const T* xt, T* err_out, const T* p1, const T* p0, T* Ih, T* Ihb, T* Ir, bool first,
+                   double* mon_out, const double* cf);
 void lsmr_stop(hgm_ctx* c, const double* rr, double nb, double tol, double* st, int k);
 template <typename T> void div_sqrt_nz(hgm_ctx* c, int64_t n, const T* in, T* out, const T* ss);
 // out[i] = epi(in[i], a, z[i]) (out may alias z): the epilogue of an SpMV applied to its raw product

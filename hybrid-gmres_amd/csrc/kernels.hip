@@ -1960,6 +1960,125 @@ void lsmr_monitor_r(hgm_ctx* c, int64_t n, const T* p1, const T* p0, T* Ih, T* I
     HGM_HIP(hipGetLastError());
 }
 
+// k_lsmr_step and k_lsmr_mon_r in one pass over the n-space (the fp32 one-pass LSMR with x_true):
+// the two kernels walk the same elements in the same grid (parts_for(n) blocks, grid_elems) and
+// touch disjoint vectors, so each of the two block sums -- and every element -- has the bits of
+// the two separate launches; one launch boundary and one sweep of the grid instead of two.
+template <typename T, bool FIRST>
+__global__ __launch_bounds__(BS) void k_lsmr_step_mon(int64_t n, T* __restrict__ x, T* __restrict__ h,
+                                                      T* __restrict__ hbar, T* __restrict__ v, const T* ssa,
+                                                      const T* coef, const double* st, int k, const T* __restrict__ xt,
+                                                      T* __restrict__ parts_e, const T* __restrict__ p1,
+                                                      const T* __restrict__ p0, T* __restrict__ Ih, T* __restrict__ Ihb,
+                                                      T* __restrict__ Ir, double* __restrict__ parts_m,
+                                                      const double* __restrict__ cf) {
+    __shared__ T sh[4];
+    __shared__ double shm[4];
+    const T alpha = (T)sqrt((double)*ssa);
+    const bool live = !(st[8] != 0.0 && st[8] < (double)(k + 1));
+    const T c_hbar = coef[0], c_x = coef[1], c_h = coef[2];
+    const double c1 = cf[0], c0 = cf[1], f = cf[2], e = cf[3], cx = cf[4];
+    T acc = 0;
+    double accm = 0;
+    grid_elems<T, true>(n, [&](int64_t i, auto wc) {
+        constexpr int W = decltype(wc)::value;
+        {   // k_lsmr_step's element body
+            T vv[W], xx[W], hh[W], hb[W], tt[W];
+            vload<W>(v, i, vv);
+            vload<W>(x, i, xx);
+            if (live) {
+                vload<W>(h, i, hh);
+                if (!FIRST) vload<W>(hbar, i, hb);
+            }
+            vload<W>(xt, i, tt);
+#pragma unroll
+            for (int u = 0; u < W; ++u) {
+                if (alpha > T(0)) vv[u] = vv[u] / alpha;
+                if (live) {
+                    if (FIRST) hb[u] = hh[u];
+                    else { const T p = c_hbar * hb[u]; hb[u] = hh[u] - p; }
+                    const T q = c_x * hb[u];
+                    xx[u] = xx[u] + q;
+                    const T r = c_h * hh[u];
+                    hh[u] = vv[u] - r;
+                }
+                const T d = xx[u] - tt[u];
+                acc += d * d;
+            }
+            if (alpha > T(0)) vstore<W>(v, i, vv);
+            if (live) {
+                vstore<W>(hbar, i, hb);
+                vstore<W>(x, i, xx);
+                vstore<W>(h, i, hh);
+            }
+        }
+        {   // k_lsmr_mon_r's element body
+            T a[W], b[W], hm[W], hbm[W], r[W];
+            vload<W>(p1, i, a);
+            vload<W>(p0, i, b);
+            if (!FIRST) {
+                vload<W>(Ih, i, hm);
+                vload<W>(Ihb, i, hbm);
+            }
+            vload<W>(Ir, i, r);
+#pragma unroll
+            for (int u = 0; u < W; ++u) {
+                const double x1 = c1 * (double)a[u], x0 = c0 * (double)b[u];
+                const double iv = x1 + x0;
+                double ih, ihb;
+                if (FIRST) { ih = iv; ihb = ih; }
+                else {
+                    const double q = f * (double)hm[u];
+                    ih = iv - q;
+                    const double w = e * (double)hbm[u];
+                    ihb = ih - w;
+                }
+                const double s_ = cx * ihb;
+                const double ir = (double)r[u] - s_;
+                hm[u] = (T)ih;
+                hbm[u] = (T)ihb;
+                r[u] = (T)ir;
+                const double rr = (double)r[u];
+                accm += rr * rr;
+            }
+            vstore<W>(Ih, i, hm);
+            vstore<W>(Ihb, i, hbm);
+            vstore<W>(Ir, i, r);
+        }
+    });
+    const T tot = block_sum_all(acc, sh);
+    const double totm = block_sum_all(accm, shm);
+    if (threadIdx.x == 0) {
+        parts_e[blockIdx.x] = tot;
+        parts_m[blockIdx.x] = totm;
+    }
+}
+
+// The fused pair when it gives the separate launches' bits (x_true given, the partial-sum grid,
+// 16-byte aligned vectors); false: the caller runs lsmr_step and lsmr_monitor_r.
+template <typename T>
+bool lsmr_step_mon(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, T* v, const T* ssa, const T* coef, const double* st,
+                   int k, const T* xt, T* err_out, const T* p1, const T* p0, T* Ih, T* Ihb, T* Ir, bool first,
+                   double* mon_out, const double* cf) {
+    if (!c->num.lsmr_fuse_nmon || !xt || n <= SINGLE_MAX) return false;
+    if (!(al16(x) && al16(h) && al16(hbar) && al16(v) && al16(xt) && al16(p1) && al16(p0) && al16(Ih) && al16(Ihb) &&
+          al16(Ir)))
+        return false;
+    const int np = parts_for(n);
+    T* parts_e = c->buf<T>("red_parts", MAX_PARTS);
+    double* parts_m = c->buf<double>("lsmr_mon_parts", MAX_PARTS);
+    if (first)
+        k_lsmr_step_mon<T, true><<<np, BS, 0, c->stream>>>(n, x, h, hbar, v, ssa, coef, st, k, xt, parts_e, p1, p0, Ih,
+                                                           Ihb, Ir, parts_m, cf);
+    else
+        k_lsmr_step_mon<T, false><<<np, BS, 0, c->stream>>>(n, x, h, hbar, v, ssa, coef, st, k, xt, parts_e, p1, p0, Ih,
+                                                            Ihb, Ir, parts_m, cf);
+    k_finalize<T><<<1, BS, 0, c->stream>>>(parts_e, np, err_out);
+    k_finalize<double><<<1, BS, 0, c->stream>>>(parts_m, np, mon_out);
+    HGM_HIP(hipGetLastError());
+    return true;
+}
+
 template <typename T>
 void lsmr_monitor(hgm_ctx* c, int64_t n, const T* p1, const T* p0, double c1, double c0, double* Ih, double* Ihb,
                   double* Ix, const T* rhs, double f, double e, double cx, bool first, double* out, const double* cf) {
@@ -2055,6 +2174,8 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
                                     const double*);                                            \
     template void lsmr_step<T>(hgm_ctx*, int64_t, T*, T*, T*, T*, const T*, const T*, const double*, int, \
                                const T*, T*);                                                  \
+    template bool lsmr_step_mon<T>(hgm_ctx*, int64_t, T*, T*, T*, T*, const T*, const T*, const double*, int, \
+                                   const T*, T*, const T*, const T*, T*, T*, T*, bool, double*, const double*); \
     template void div_sqrt_nz<T>(hgm_ctx*, int64_t, const T*, T*, const T*);                  \
     template void fill<T>(hgm_ctx*, int64_t, T*, T);                                           \
     template void scale<T>(hgm_ctx*, int64_t, const T*, T*, T);                                \

@@ -1254,12 +1254,16 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
                 fused_pass<T>(c, At, fp, fa);                                     // :38-39 (+ A*v_hat)
                 if (dist_n(c)) allreduce(c, wm, m + 1);
                 lsmr_rot<T>(c, sl + S_BETA, wm + m, st, coef, cfm, cfn);          // :42-67 scalars
-                lsmr_step<T>(c, n, x, h, hbar, v, wm + m, coef, st, k, xt, xt ? errh + k : nullptr);   // :40, :61-67, :72
-                if (xt && dist_n(c)) allreduce(c, errh + k, 1);
                 double* dm = dmonh + 2 * (size_t)k;
+                // (fp32: the n-space step and the n-space monitor in one launch when it applies)
+                const bool nmon = img_t && lsmr_step_mon<T>(c, n, x, h, hbar, v, wm + m, coef, st, k, xt,
+                                                            xt ? errh + k : nullptr, Atu1, Atu0, Ihn_t, Ihbn_t,
+                                                            Irn_t, k == 0, dm + 1, cfn);
+                if (!nmon) lsmr_step<T>(c, n, x, h, hbar, v, wm + m, coef, st, k, xt, xt ? errh + k : nullptr);   // :40, :61-67, :72
+                if (xt && dist_n(c)) allreduce(c, errh + k, 1);
                 lsmr_monitor<T>(c, m, Av, nullptr, 0, 0, Ihm, Ihbm, Ixm, b, 0, 0, 0, k == 0, dm, cfm);
-                if (img_t) lsmr_monitor_r<T>(c, n, Atu1, Atu0, Ihn_t, Ihbn_t, Irn_t, k == 0, dm + 1, cfn);
-                else lsmr_monitor<T>(c, n, Atu1, Atu0, 0, 0, Ihn, Ihbn, Ixn, Atb, 0, 0, 0, k == 0, dm + 1, cfn);
+                if (!nmon && img_t) lsmr_monitor_r<T>(c, n, Atu1, Atu0, Ihn_t, Ihbn_t, Irn_t, k == 0, dm + 1, cfn);
+                else if (!nmon) lsmr_monitor<T>(c, n, Atu1, Atu0, 0, 0, Ihn, Ihbn, Ixn, Atb, 0, 0, 0, k == 0, dm + 1, cfn);
                 if (dist_n(c)) allreduce(c, dm + 1, 1);
                 std::swap(Atu0, Atu1);
                 if (tol > 0) lsmr_stop(c, dm, nb, tol, st, k);                   // :76

@@ -27,7 +27,7 @@ OPTIONS = {"parity": 1, "mgs_form": 2, "mgs_single": 3, "gram_err": 4, "gram_err
            "krylov_pad": 23, "fused_kind": 24, "fused_wregion": 25, "fused_waves": 26, "fused_group": 27,
            "fused_depth": 28, "fused_pairs": 29, "fused_acc32": 30, "fused_plan_dev": 31, "fused_reduce": 32,
            "host_spin_us": 33, "fused_rowpair": 34,
-           "lsqr_res_img": 35}
+           "lsqr_res_img": 35, "lsmr_fuse_nmon": 36}
 HGM_MGS, HGM_CGS2 = 0, 1
 HGM_SIDE_AB, HGM_SIDE_BA = 0, 1
 HGM_DEVICE_PTRS = 1

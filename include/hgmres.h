@@ -166,7 +166,10 @@ enum hgm_ctx_option {
                                       measured variants of the 2048-slot shape only */,
     HGM_OPT_LSQR_RES_IMG = 35      /* one-pass lsqr_solver: the exact final residual norm(b - A*x) of
                                       lsqr_solver.m:52 from A*x kept in double alongside x (A*v_k is the
-                                      pass's A*v_hat / alpha) instead of one more SpMV [1] */
+                                      pass's A*v_hat / alpha) instead of one more SpMV [1] */,
+    HGM_OPT_LSMR_FUSE_NMON = 36    /* one-pass lsmr_solver with x_true: the n-space step (:40, :61-67, :72)
+                                      and the n-space monitor (:71's A'r image) in one launch [1] (the
+                                      same bits as two) */
 };
 
 /* Host all-reduce hook (sum, in place, host memory) used instead of RCCL for

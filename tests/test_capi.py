@@ -120,7 +120,7 @@ def test_ctx_option_api_without_gpu():
     v = ctypes.c_double()
     assert lib.hgm_ctx_set_option(None, 1, 1.0) == L.HGM_E_ARG
     assert lib.hgm_ctx_get_option(None, 1, ctypes.byref(v)) == L.HGM_E_ARG
-    assert set(L.OPTIONS.values()) == set(range(1, 36))
+    assert set(L.OPTIONS.values()) == set(range(1, 37))
     txt = open(os.path.join(ROOT, "include", "hgmres.h")).read()
     for name, val in L.OPTIONS.items():   # the Python names mirror the header's enum
         assert re.search(rf"HGM_OPT_{name.upper()}\s*=\s*{val}\b", txt), name

@@ -610,3 +610,15 @@ def test_fp32_one_pass_within_fp32_oracle_envelope(gpu_ctx, solver):
                                      for a, f_, m_ in ratios))
     assert dx <= max(1e-6, kfac * sx), (dx, sx)
     Ar.close()
+
+
+def test_lsmr_fused_step_monitor_is_bitwise(gpu_ctx):
+    """HGM_OPT_LSMR_FUSE_NMON: the fp32 one-pass LSMR's n-space step and n-space monitor in one
+    launch give the two launches' bits (x and every history)."""
+    A, At, b, xt = _gkb_pair(gpu_ctx, 512, 47, dtype="f32")
+    outs = {}
+    for f in (0, 1):
+        with gpu_ctx.options(fused_ab=1, lsmr_fuse_nmon=f):
+            outs[f] = hgmres.lsmr_solver(A, b, xt, 0.0, 10, ctx=gpu_ctx, At=At)
+    for a_, b_ in zip(outs[0], outs[1]):
+        assert np.array_equal(np.asarray(a_), np.asarray(b_))
