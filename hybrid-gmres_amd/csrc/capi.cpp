@@ -666,6 +666,16 @@ HGM_API int hgm_ctx_rank(const hgm_ctx* c, int* rank, int* world) {
     return HGM_OK;
 }
 
+HGM_API int hgm_ctx_solve_path(const hgm_ctx* c, int what, int* out, int cap, int* n) {
+    if (!c || (what != 0 && what != 1) || cap < 0 || (cap > 0 && !out)) return HGM_E_ARG;
+    std::vector<int> v;
+    if (what == 0) v = c->path_mon;
+    else if (c->path_onepass >= 0) v.push_back(c->path_onepass);
+    for (int i = 0; i < cap && i < (int)v.size(); ++i) out[i] = v[i];
+    if (n) *n = (int)v.size();
+    return HGM_OK;
+}
+
 // ---- matrices ----------------------------------------------------------------
 HGM_API int hgm_mat_create_csr(hgm_ctx* c, int64_t rows, int64_t cols, int64_t nnz, const int64_t* row_ptr,
                                const int32_t* col_idx, const double* val, int dtype, hgm_mat** out) {

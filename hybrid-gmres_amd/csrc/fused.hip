@@ -1488,6 +1488,12 @@ static void plan_bands(FusedPlan* P, const std::vector<int32_t>& ray_tab, const 
     P->band_run = upload(run);
 }
 
+// The one refusal a smaller region can cure (fused_ab_plan retries it with half the side); every
+// other refusal of a plan (option shapes without a kernel, index ranges) goes straight to the
+// two-pass path.
+static const char* const kLdsCapacityMsg =
+    "fused A*(B*q): a region is crossed by more rays than the LDS of its waves holds";
+
 // The device part of the row-wave plan: ray sets, slots (lidx) and ray_tab by k_plan_count /
 // k_plan_fill, then the ray-major reduction index by a counting sort of ray_tab on the host
 // (slots in increasing order = regions in order, as the host build).
@@ -1529,7 +1535,7 @@ static FusedPlan* fused_plan_dev_finish(hgm_ctx* c, const hgm_mat* B, int R, int
     if (W == WV && worst <= MRV - 64 && (maxr == 0 || MRV < maxr)) maxr = MRV;
         HGM_RW_SHAPES(HGM_RW_PICK)
 #undef HGM_RW_PICK
-        HGM_REQUIRE(maxr > 0, "fused A*(B*q): a region is crossed by more rays than the LDS of its waves holds");
+        HGM_REQUIRE(maxr > 0, kLdsCapacityMsg);
         P->maxr = maxr;
         std::vector<int64_t> reg_base(nreg + 1, 0);
         for (int64_t g = 0; g < nreg; ++g) reg_base[g + 1] = reg_base[g] + cnt[g];
@@ -1712,7 +1718,7 @@ FusedPlan* fused_plan_build_rw(hgm_ctx* c, const hgm_mat* B, int R, int W, int G
     if (W == WV && worst.load() <= MRV - 64 && (maxr == 0 || MRV < maxr)) maxr = MRV;
     HGM_RW_SHAPES(HGM_RW_PICK)
 #undef HGM_RW_PICK
-    HGM_REQUIRE(maxr > 0, "fused A*(B*q): a region is crossed by more rays than the LDS of its waves holds");
+    HGM_REQUIRE(maxr > 0, kLdsCapacityMsg);
     std::vector<int64_t> reg_base(nreg + 1, 0);
     for (int64_t g = 0; g < nreg; ++g) reg_base[g + 1] = reg_base[g] + (int64_t)rrays[g].size();
     const int64_t nslot = reg_base[nreg];
@@ -1818,7 +1824,7 @@ const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B) {
                         Bm->fused = fused_plan_build_rw(c, B, R, nu.fused_waves, nu.fused_group);
                         break;
                     } catch (const Error& e) {
-                        if (e.code != HGM_E_ARG || R / 2 < 16 || R % 2) throw;
+                        if (e.code != HGM_E_ARG || e.msg != kLdsCapacityMsg || R / 2 < 16 || R % 2) throw;
                     }
                 }
             } else {

@@ -140,6 +140,11 @@ struct hgm_ctx {
     // packets (hipExtLaunchKernelGGL), so they bracket kernel execution only
     hipEvent_t arm_start = nullptr, arm_stop = nullptr, cur_stop = nullptr;
     hgm::Timing timing;
+    // path decisions of the last solve (hgm_ctx_solve_path): per GMRES iteration, whether the error
+    // monitor came from the Gram form (1) or x was formed (0); whether the last Golub-Kahan solve
+    // took the one-pass path.  On a communicator both decide the collective sequence.
+    std::vector<int> path_mon;
+    int path_onepass = -1;
 
     template <typename T>
     T* buf(const std::string& name, size_t count) {

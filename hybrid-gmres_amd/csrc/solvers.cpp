@@ -84,6 +84,26 @@ T read1(hgm_ctx* c, const T* dev) {
     return v;
 }
 
+// The Golub-Kahan solvers' one-pass plan, agreed over the ranks.  The one-pass path all-reduces
+// [A*v_hat | alpha^2] (m + 1 values) per iteration and the two-pass path A*v (m) plus n-space
+// norms, so on a communicator every rank must take the same one: each rank plans its own shard
+// (a plan can be refused on some shards only, e.g. the centre tile columns of a fan-beam cut),
+// the refusals are summed over the ranks, and the pass runs only if no rank refused.
+template <typename T>
+const FusedPlan* agreed_gk_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* At, bool allowed) {
+    const FusedPlan* fp = allowed ? fused_ab_plan(c, A, At) : nullptr;
+    if (fp && !fused_gk_ok(c, At, fp)) fp = nullptr;
+    if (dist_n(c)) {
+        double* f = reinterpret_cast<double*>(c->dscal) + 96;
+        const double refused = fp ? 0.0 : 1.0;
+        h2d(c, f, &refused, sizeof(double));
+        allreduce(c, f, 1);
+        if (read1<double>(c, f) != 0.0) fp = nullptr;
+    }
+    c->path_onepass = fp ? 1 : 0;
+    return fp;
+}
+
 // Input vector hand-over: device pointer (HGM_DEVICE_PTRS) or host buffer.
 template <typename T>
 const T* stage_in(hgm_ctx* c, const char* name, const double* p, int64_t n, bool dev) {
@@ -241,6 +261,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     const double wait0 = c->wait_s;
     const long waits0 = c->waits;
     HGM_REQUIRE(maxit >= 1, "maxit must be >= 1");
+    c->path_mon.clear();
     using T = double;
     const bool dev = o && (o->flags & HGM_DEVICE_PTRS);
     const int orth = o ? o->orth : HGM_MGS;
@@ -742,6 +763,7 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
                 want_x = false;
             }
         }
+        c->path_mon.push_back(want_x ? 0 : 1);
         enqueue_recon(k, want_x);
         x_assigned = true;
         if (k + L + 1 < maxit) enqueue_step(k + L + 1);  // speculative, see above
@@ -836,8 +858,7 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     // At (fused.hip, row epilogue), alpha^2 = ||v_hat||^2 as its side sum, and the next step's
     // A*v_{k+1} (:22) is (A*v_hat) / alpha: an m-vector operation instead of a second pass.
     // wm = [A*v_hat | alpha^2] (m + 1: alpha^2 rides the m-vector all-reduce on a communicator).
-    const FusedPlan* fp = (!hybrid && !parity) ? fused_ab_plan(c, A, At) : nullptr;
-    if (fp && !fused_gk_ok(c, At, fp)) fp = nullptr;
+    const FusedPlan* fp = agreed_gk_plan<T>(c, A, At, !hybrid && !parity);
     T* wm = fp ? c->buf<T>("gkb_wm", m + 2) : nullptr;
     // beta = norm(b) (lsqr_solver.m:7; hybrid: norm([b;0]) = norm(b), hybrid_lsqr_solver.m:9)
     double beta = nb;
@@ -1170,8 +1191,7 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     }
     // One pass over the operator per iteration (as lsqr_t): the step :38-39 and
     // A*v_hat in one pass over At, A*v_{k+1} (:34, the kept A*v) = (A*v_hat) / alpha.
-    const FusedPlan* fp = !parity ? fused_ab_plan(c, A, At) : nullptr;
-    if (fp && !fused_gk_ok(c, At, fp)) fp = nullptr;
+    const FusedPlan* fp = agreed_gk_plan<T>(c, A, At, !parity);
     T* wm = fp ? c->buf<T>("gkb_wm", m + 2) : nullptr;                         // [A*v_hat | alpha^2]
     HGM_HIP(hipMemcpyAsync(u, b, sizeof(T) * m, hipMemcpyDeviceToDevice, c->stream));   // :10
     double beta = nb;                                                          // :11

@@ -88,6 +88,20 @@ class Context:
         _check(L.load().hgm_ctx_rank(self._h, C.byref(r), C.byref(w)), self)
         return r.value, w.value
 
+    def solve_path(self):
+        """Path decisions of the last solve on this context (``hgm_ctx_solve_path``):
+        ``{"gram_monitor": [0/1 per GMRES iteration], "one_pass": 0/1 or None}``."""
+        lib = L.load()
+        out = {}
+        for what, key in ((0, "gram_monitor"), (1, "one_pass")):
+            n = C.c_int()
+            _check(lib.hgm_ctx_solve_path(self._h, what, None, 0, C.byref(n)), self)
+            buf = (C.c_int * max(n.value, 1))()
+            _check(lib.hgm_ctx_solve_path(self._h, what, buf, n.value, C.byref(n)), self)
+            out[key] = list(buf[:n.value])
+        out["one_pass"] = out["one_pass"][0] if out["one_pass"] else None
+        return out
+
     def set_option(self, name, value):
         """Per-context numerics option (``hgm_ctx_set_option``; names in ``_lib.OPTIONS``),
         e.g. ``ctx.set_option("parity", 1)``.  Returns the previous value."""

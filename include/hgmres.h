@@ -11,7 +11,7 @@
  *   hgm_hybrid_ba_gmres_rtp  <- hybrid_ba_gmres_rtp.m:1   [x,error_norm,residual_norm,niters]
  *   hgm_gmres_bounds         <- ABgmres_hybrid_bounds.m:1-2, ABgmres_nonhybrid_bounds.m:1-2,
  *                               BAgmres_hybrid_bounds.m:1-2, BAgmres_nonhybrid_bounds.m:1-2
- *                               (outputs 1-4; the dense spectral-bound outputs 5-8 are out of scope)
+ *                               (outputs 1-4; outputs 5-8: hgm_gmres_bounds_filter below)
  *   hgm_lsqr_solver          <- lsqr_solver.m:1           [x,error_norm,residual_norm,niters]
  *   hgm_lsmr_solver          <- lsmr_solver.m:1           [x,err_hist,res_hist,ar_hist,iters]
  *   hgm_hybrid_lsqr_solver   <- hybrid_lsqr_solver.m:1
@@ -197,6 +197,13 @@ HGM_API const char* hgm_last_error(const hgm_ctx* ctx);
 HGM_API int hgm_ctx_synchronize(hgm_ctx* ctx);
 HGM_API void* hgm_ctx_stream(hgm_ctx* ctx);
 HGM_API int hgm_ctx_rank(const hgm_ctx* ctx, int* rank, int* world);
+/* Path decisions of the context's last solve (test hook: on a communicator every rank must issue
+ * the same collective sequence, so these must agree across the ranks).  what = 0: one entry per
+ * iteration of the last GMRES-family solve, 1 when that iteration's error monitor came from the
+ * Gram form (no x formed, no collective) and 0 when x was formed (an all-reduced error sum);
+ * what = 1: one entry, 1 when the last lsqr_solver / lsmr_solver took the one-pass path (agreed
+ * over the ranks).  *n = entries available, at most cap written. */
+HGM_API int hgm_ctx_solve_path(const hgm_ctx* ctx, int what, int* out, int cap, int* n);
 /* Set / read one hgm_ctx_option (HGM_E_ARG for an unknown option or a value out of range). */
 HGM_API int hgm_ctx_set_option(hgm_ctx* ctx, int option, double value);
 HGM_API int hgm_ctx_get_option(const hgm_ctx* ctx, int option, double* value);

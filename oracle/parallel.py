@@ -47,6 +47,9 @@ def load():
         lib.oracle_csr_matvec_f32.argtypes = [C.c_int64, P(C.c_int64), P(C.c_int32), P(C.c_float), P(C.c_float),
                                               P(C.c_float)]
         lib.oracle_csr_matvec_f32.restype = None
+        lib.oracle_csr_matvec_f32_order.argtypes = [C.c_int64, P(C.c_int64), P(C.c_int32), P(C.c_float),
+                                                    P(C.c_float), P(C.c_float), C.c_int, C.c_int]
+        lib.oracle_csr_matvec_f32_order.restype = None
         lib.oracle_num_threads.restype = C.c_int
         _lib = lib
     return _lib
@@ -98,6 +101,18 @@ class ParallelCSR:
         load().oracle_csr_matvec(self.shape[0], self.rp.ctypes.data_as(C.POINTER(C.c_int64)),
                                  self.ci.ctypes.data_as(C.POINTER(C.c_int32)), self.val.ctypes.data_as(dp),
                                  v.ctypes.data_as(dp), y.ctypes.data_as(dp))
+        return y
+
+    def matvec_f32_order(self, v, ways, rev):
+        """fp32 product in another summation order (spmv_omp.c oracle_csr_matvec_f32_order)."""
+        assert self.dtype == np.float32
+        v = np.ascontiguousarray(v, dtype=np.float32)
+        y = np.empty(self.shape[0], dtype=np.float32)
+        fp = C.POINTER(C.c_float)
+        load().oracle_csr_matvec_f32_order(self.shape[0], self.rp.ctypes.data_as(C.POINTER(C.c_int64)),
+                                           self.ci.ctypes.data_as(C.POINTER(C.c_int32)),
+                                           self.val.ctypes.data_as(fp), v.ctypes.data_as(fp),
+                                           y.ctypes.data_as(fp), int(ways), int(rev))
         return y
 
     def __matmul__(self, v):

@@ -35,4 +35,28 @@ void oracle_csr_matvec_f32(int64_t rows, const int64_t* rp, const int32_t* ci, c
     }
 }
 
+/* fp32 in ANOTHER summation order (test infrastructure: the fp32 oracle's own rounding spread,
+   tests/golden/make_golden.py dump_c5).  Row entries are visited forward (rev = 0) or backward
+   (rev = 1) and dealt round-robin over `ways` accumulators (1..128), which are then combined by
+   a pairwise tree -- the shape of a lane-parallel GPU row sum.  Each order is a correct fp32 sum
+   of the same products; ways = 1, rev = 0 is oracle_csr_matvec_f32. */
+void oracle_csr_matvec_f32_order(int64_t rows, const int64_t* rp, const int32_t* ci, const float* val,
+                                 const float* x, float* y, int ways, int rev) {
+    if (ways < 1) ways = 1;
+    if (ways > 128) ways = 128;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < rows; ++i) {
+        float acc[128];
+        for (int w = 0; w < ways; ++w) acc[w] = 0.0f;
+        const int64_t a = rp[i], len = rp[i + 1] - rp[i];
+        for (int64_t t = 0; t < len; ++t) {
+            const int64_t j = rev ? a + len - 1 - t : a + t;
+            acc[t % ways] += val[j] * x[ci[j]];
+        }
+        for (int h = 1; h < ways; h *= 2)
+            for (int w = 0; w + h < ways; w += 2 * h) acc[w] += acc[w + h];
+        y[i] = acc[0];
+    }
+}
+
 int oracle_num_threads(void) { return omp_get_max_threads(); }

@@ -1,10 +1,12 @@
-"""Worker for test_gpu_parity.py::test_shard_emulation_two_ranks (and, through
-solve_all, test_gpu_rccl.py's one-rank RCCL run).
+"""Worker for the multi-rank tests: test_gpu_parity.py::test_shard_emulation_two_ranks,
+test_gpu_fullsize.py::test_c4_c5_sharded_vs_oracle (world 2, 4, 8) and, through solve_all,
+test_gpu_rccl.py's one-rank RCCL run.
 
 Runs the pixel-sharded solvers as ``world`` processes on ONE device with the
 cross-rank sums routed through the library's host all-reduce hook (a fixed-order
-two-party sum over a local socket), i.e. the same C++ code path as RCCL mode
-with a different transport.  usage: _shard_worker.py RANK WORLD PORT OUTDIR
+sum over local sockets: rank 0 adds the ranks' arrays in rank order and sends the
+sum back), i.e. the same C++ code path as RCCL mode with a different transport.
+usage: _shard_worker.py RANK WORLD PORT OUTDIR [c4]
 """
 import os
 import sys
@@ -20,39 +22,72 @@ from hgmres.dist import plan_pixel_shards, shard_operators  # noqa: E402
 from hgmres.problems import tomo_problem  # noqa: E402
 
 
-def main():
-    rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
-    ctx = hgmres.Context(0)
-    conn = None
-    if world > 1:
+class Hub:
+    """Fixed-order all-reduce of ``world`` processes over local sockets.  Rank 0 listens and
+    accepts the other ranks (each announces its rank); a sum is ((r0 + r1) + r2) + ... in rank
+    order, formed on rank 0 and sent back to every rank, so every rank gets the same bits (as
+    RCCL's all-reduce gives every rank the same result)."""
+
+    def __init__(self, rank, world, port):
         from multiprocessing.connection import Client, Listener
+        self.rank, self.world, self.conns = rank, world, {}
+        if world == 1:
+            return
         if rank == 0:
-            lst = Listener(("127.0.0.1", port), authkey=b"hgm")
-            conn = lst.accept()
+            lst = Listener(("127.0.0.1", port), authkey=b"hgm", backlog=world)
+            for _ in range(world - 1):
+                c = lst.accept()
+                self.conns[int(c.recv())] = c
+            lst.close()
         else:
-            for _ in range(600):
+            c = None
+            for _ in range(1200):
                 try:
-                    conn = Client(("127.0.0.1", port), authkey=b"hgm")
+                    c = Client(("127.0.0.1", port), authkey=b"hgm")
                     break
                 except (ConnectionRefusedError, OSError):
                     time.sleep(0.1)
-            assert conn is not None
+            assert c is not None, "no hub"
+            c.send(rank)
+            self.conns[0] = c
 
-        def allreduce(arr):
-            if rank == 0:
-                other = conn.recv()
-                s = arr + other          # fixed order: rank 0 + rank 1
-                conn.send(s)
-                arr[:] = s
-            else:
-                conn.send(arr.copy())
-                arr[:] = conn.recv()
+    def allreduce(self, arr):
+        if self.world == 1:
+            return
+        if self.rank == 0:
+            s = np.array(arr, dtype=arr.dtype, copy=True)
+            for r in range(1, self.world):
+                other = self.conns[r].recv()
+                if other.shape != s.shape:    # a collective-sequence mismatch between ranks: fail loudly
+                    raise RuntimeError(f"rank {r} sent {other.shape} while rank 0 reduces {s.shape}")
+                s = s + other
+            for r in range(1, self.world):
+                self.conns[r].send(s)
+            arr[:] = s
+        else:
+            self.conns[0].send(np.array(arr, copy=True))
+            arr[:] = self.conns[0].recv()
 
-        ctx.set_host_allreduce(rank, world, allreduce)
-    res = solve_c4(ctx, rank, world) if len(sys.argv) > 5 and sys.argv[5] == "c4" else solve_all(ctx, rank, world)
+    def barrier(self):
+        self.allreduce(np.zeros(1))
+
+    def close(self):
+        for c in self.conns.values():
+            c.close()
+
+
+def main():
+    rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    ctx = hgmres.Context(0)
+    hub = Hub(rank, world, port)
+    if world > 1:
+        ctx.set_host_allreduce(rank, world, hub.allreduce)
+    if len(sys.argv) > 5 and sys.argv[5] == "c4":
+        res = solve_c4(ctx, rank, world, hub)
+    else:
+        res = solve_all(ctx, rank, world)
     np.savez(os.path.join(out, f"rank{rank}_of{world}.npz"), **res)
-    if conn is not None:
-        conn.close()
+    hub.close()
     ctx.close()
 
 
@@ -146,39 +181,66 @@ def solve_all(ctx, rank, world):
     A32s = B32s.T
     x, e, r, k = hgmres.lsqr_solver(A32s, P.b, xs[tlo:thi], 0.0, 6, ctx=ctx, At=B32s)
     res.update(tlsqr32_x=x, tlsqr32_res=r, tlsqr32_err=e)
+    res.update(tlsqr32_path=ctx.solve_path()["one_pass"])
     x, e, r, a, k = hgmres.lsmr_solver(A32s, P.b, xs[tlo:thi], 0.0, 6, ctx=ctx, At=B32s)
-    res.update(tlsmr32_x=x, tlsmr32_res=r, tlsmr32_err=e, tlsmr32_ar=a)
+    res.update(tlsmr32_x=x, tlsmr32_res=r, tlsmr32_err=e, tlsmr32_ar=a, tlsmr32_path=ctx.solve_path()["one_pass"])
+    # a one-pass plan refused on ONE rank only (HGM_OPT_FUSED_AB off on the last rank;
+    # a fan-beam cut can refuse the centre shards' plans alone): the ranks agree on the two-pass
+    # path (solvers.cpp agreed_gk_plan) instead of issuing different collective sequences, so the
+    # solve equals the one with the pass off on every rank, bit for bit
+    for tag, off in (("tmix", rank == world - 1), ("toff", True)):
+        with ctx.options(fused_ab=0 if off else 1):
+            x, e, r, k = hgmres.lsqr_solver(A32s, P.b, xs[tlo:thi], 0.0, 6, ctx=ctx, At=B32s)
+            pq = ctx.solve_path()["one_pass"]
+            xm_, em_, rm_, am_, km_ = hgmres.lsmr_solver(A32s, P.b, xs[tlo:thi], 0.0, 6, ctx=ctx, At=B32s)
+            pm = ctx.solve_path()["one_pass"]
+        res.update({f"{tag}q_x": x, f"{tag}q_res": r, f"{tag}q_err": e, f"{tag}q_path": pq,
+                    f"{tag}m_x": xm_, f"{tag}m_res": rm_, f"{tag}m_ar": am_, f"{tag}m_path": pm})
     res.update(lo=lo, hi=hi, tlo=tlo, thi=thi)
     return res
 
 
-def solve_c4(ctx, rank, world):
+def solve_c4(ctx, rank, world, hub):
     """BASELINE configs[3] and [4] at full size, cut exactly as bench.py build_shard cuts them
-    (device-generated 4096^2 / 47-angle operator, 4 x 4-tiled, whole tile columns of stored
-    pixels, B_g = row slice of A', A_g its transpose, 64-column bands), with the fixture's b
-    (tests/golden/c4_4096.npz) in place of the device-formed one:
+    for --gpus `world` (device-generated 4096^2 / 47-angle operator, 4 x 4-tiled, whole tile
+    columns of stored pixels, B_g = row slice of A', A_g its transpose, 64-column bands), with the
+    fixture's b (tests/golden/c4_4096.npz) in place of the device-formed one.  The ranks build
+    their shards one after the other (each build holds the full operator, its transpose and the
+    sort's scratch for a moment), so the peak HBM of `world` ranks on one device is one build plus
+    the shards:
     * ABgmres_nonhybrid_bounds, 20 iterations, fp64 (the one pass per shard + the m-vector
-      all-reduce; test_gpu_fullsize.py::test_c4_sharded_two_ranks_vs_oracle);
-    * lsqr_solver / lsmr_solver on the fp32 shards, 5 iterations."""
+      all-reduce), with the per-iteration monitor path (Gram form or x formed) of every rank;
+    * lsqr_solver / lsmr_solver on the fp32 shards, the bench's 20 iterations, with the path."""
     import bench
     from conftest import load_golden
     g = load_golden("c4_4096.npz")
     b = np.ascontiguousarray(g["b"])
     res = {}
     for wl, tag in (("c4", "abn"), ("c5", "f32")):
-        A_g, B_g, _, xs, (lo, hi), full = bench.build_shard(ctx, bench.WORKLOADS[wl], rank, world)
+        for turn in range(world):
+            if turn == rank:
+                t0 = time.time()
+                A_g, B_g, _, xs, (lo, hi), full = bench.build_shard(ctx, bench.WORKLOADS[wl], rank, world)
+                ctx.synchronize()
+                print(f"[rank {rank}/{world}] {wl} shard [{lo}, {hi}) built in {time.time() - t0:.1f} s", flush=True)
+            hub.barrier()
         xt = np.ascontiguousarray(xs[lo:hi])
+        t0 = time.time()
         if tag == "abn":
             out_ = hgmres.ABgmres_nonhybrid_bounds(A_g, B_g, b, xt, 0.0, 20, ctx=ctx, return_H=True)
-            res.update(abn_x=out_[0], abn_err=out_[1], abn_res=out_[2], abn_k=out_[3], abn_H=out_[-1])
+            res.update(abn_x=out_[0], abn_err=out_[1], abn_res=out_[2], abn_k=out_[3], abn_H=out_[-1],
+                       abn_path=np.array(ctx.solve_path()["gram_monitor"]), abn_xt_zero=bool(np.all(xt == 0)))
         else:
-            x, e, r, k = hgmres.lsqr_solver(A_g, b, xt, 0.0, 5, ctx=ctx, At=B_g)
-            res.update(lsqr32_x=x, lsqr32_err=e, lsqr32_res=r, lsqr32_k=k)
-            x, e, r, a, k = hgmres.lsmr_solver(A_g, b, xt, 0.0, 5, ctx=ctx, At=B_g)
-            res.update(lsmr32_x=x, lsmr32_err=e, lsmr32_res=r, lsmr32_ar=a, lsmr32_k=k)
+            x, e, r, k = hgmres.lsqr_solver(A_g, b, xt, 0.0, 20, ctx=ctx, At=B_g)
+            res.update(lsqr32_x=x, lsqr32_err=e, lsqr32_res=r, lsqr32_k=k, lsqr32_path=ctx.solve_path()["one_pass"])
+            x, e, r, a, k = hgmres.lsmr_solver(A_g, b, xt, 0.0, 20, ctx=ctx, At=B_g)
+            res.update(lsmr32_x=x, lsmr32_err=e, lsmr32_res=r, lsmr32_ar=a, lsmr32_k=k,
+                       lsmr32_path=ctx.solve_path()["one_pass"])
+        print(f"[rank {rank}/{world}] {wl} solves {time.time() - t0:.1f} s", flush=True)
         res.update({f"{tag}_lo": lo, f"{tag}_hi": hi})
         A_g.close()
         B_g.close()
+        hub.barrier()
     return res
 
 

@@ -137,6 +137,101 @@ def dump_c4(name="c4_4096.npz", k=20):
     print("wrote", name, "k", kk, "res", res[-1], "err", err[-1])
 
 
+class _Ordered32:
+    """The fp32 operator with every product summed in ANOTHER fixed order (oracle/spmv_omp.c
+    oracle_csr_matvec_f32_order: row entries forward or backward over `ways` round-robin
+    accumulators combined by a pairwise tree -- the shape of a lane-parallel GPU row sum).  Each is
+    a correct fp32 implementation of the same products; the spread of the solves over such orders
+    is the fp32 oracle's own rounding envelope."""
+    dtype = np.float32
+
+    def __init__(self, PM, ways, rev):
+        self.PM, self.ways, self.rev = PM, ways, rev
+        self.shape = PM.shape
+
+    def __matmul__(self, v):
+        return self.PM.matvec_f32_order(v, self.ways, self.rev)
+
+    @property
+    def T(self):
+        return _Ordered32(self.PM.T, self.ways, self.rev)
+
+    @property
+    def val(self):
+        return self.PM.val
+
+
+# the alternative orders of dump_c5: (accumulators, reversed)
+C5_ORDERS = ((1, 1), (2, 0), (4, 1), (8, 0), (16, 1), (32, 0), (64, 1), (128, 0))
+
+
+def csr_hash32(M):
+    """sha256 of the fp32 operator: indptr (int64), indices (int32), data (float32)."""
+    h = hashlib.sha256()
+    for a, dt in ((M.indptr, np.int64), (M.indices, np.int32), (M.data, np.float32)):
+        a = np.ascontiguousarray(a, dtype=dt).reshape(-1)
+        for i in range(0, a.size, 1 << 24):
+            h.update(memoryview(a[i:i + (1 << 24)]))
+    return h.hexdigest()
+
+
+def dump_c5(name="c5_4096.npz", k=20, stride=197):
+    """BASELINE configs[4] at full size: lsqr_solver / lsmr_solver on the 4096^2 / 47-angle operator
+    in fp32 (the restatement's lsqr_solver_f32 / lsmr_solver_f32: float32 operator, vectors and
+    fixed-order sums), all 20 iterations of the bench, with the fixture's b (c4_4096.npz, the
+    fp64 operator's A x_true + 1 % noise).  Plus the oracle's OWN fp32 rounding spread: the same
+    solves with every SpMV summed in each of the 8 other orders of C5_ORDERS (_Ordered32); per
+    history entry the largest relative deviation from the sequential-order run, and for x the
+    largest normwise deviation over the samples x[::stride].  The production test holds the device within 100 x
+    that spread at every iteration (VERDICT r5 "Next" #2).  The fp32 operator is pinned by the
+    sha256 of (indptr, indices, float32 data) in reference pixel order.  ~40 GB, ~40 min on 8 cores."""
+    import gc
+    import time
+    import scipy.sparse as sp
+    from oracle import parallel as OP
+    from hgmres.problems import siddon_projector, shepp_logan
+    g = np.load(os.path.join(OUT, "c4_4096.npz"))
+    b = np.ascontiguousarray(g["b"])
+    A = siddon_projector(4096, 47)
+    h64 = csr_hash(A)
+    assert h64 == str(g["A_sha256"]), "generator drifted from the C4 fixture's operator"
+    A32 = sp.csr_matrix((A.data.astype(np.float32), A.indices, A.indptr), shape=A.shape)
+    del A
+    gc.collect()
+    h32 = csr_hash32(A32)
+    xt = shepp_logan(4096).ravel(order="F")
+    OP.build()
+    PA = OP.ParallelCSR(A32)
+    del A32
+    gc.collect()
+    PA.T                                           # formed once, shared by every run
+    d = {"maxit": k, "N": 4096, "n_angles": 47, "A_sha256": h64, "A32_sha256": h32, "sample_stride": stride,
+         "orders": np.array(C5_ORDERS)}
+    for tag, fn, nh in (("lsqr", R.lsqr_solver_f32, 2), ("lsmr", R.lsmr_solver_f32, 3)):
+        t0 = time.time()
+        ref = fn(PA, b, xt, 0.0, k)
+        print(f"{tag} fixed order: {time.time() - t0:.0f} s, res {ref[2][-1]:.6e}", flush=True)
+        xs = ref[0][::stride].astype(np.float64)
+        sx, sh = 0.0, [np.zeros(k) for _ in range(nh)]
+        for ways, rev in C5_ORDERS:
+            t0 = time.time()
+            p = fn(_Ordered32(PA, ways, rev), b, xt, 0.0, k)
+            ps = p[0][::stride].astype(np.float64)
+            sx = max(sx, float(np.linalg.norm(ps - xs) / np.linalg.norm(xs)))
+            for i in range(nh):
+                sh[i] = np.maximum(sh[i], np.abs(p[1 + i] - ref[1 + i]) / np.abs(ref[1 + i]))
+            print(f"  order {ways}/{rev}: {time.time() - t0:.0f} s, spread x {sx:.2e} hist "
+                  + " ".join(f"{float(np.max(s)):.1e}" for s in sh), flush=True)
+        hn = ["err", "res", "ar"][:nh]
+        d.update({f"{tag}_k": int(ref[-1]), f"{tag}_xs": ref[0][::stride].copy(), f"{tag}_xnorm":
+                  float(np.linalg.norm(ref[0].astype(np.float64))), f"{tag}_spread_xs": sx})
+        for i, nm in enumerate(hn):
+            d[f"{tag}_{nm}"] = np.asarray(ref[1 + i], dtype=np.float64)
+            d[f"{tag}_spread_{nm}"] = sh[i]
+        np.savez_compressed(os.path.join(OUT, name), **d)     # partial file after LSQR
+    print("wrote", name)
+
+
 def dump_c2(name="c2_512.npz", k=20):
     """BASELINE configs[1] at full size and at the bench's count (bench.py WORKLOADS["c2"]):
     hybrid_ab_gmres_rtp (hybrid_ab_gmres_rtp.m:1-43), 512^2, 30 angles, nnz 1.0e7, lambda 1e-2,
@@ -232,6 +327,9 @@ if __name__ == "__main__":
         sys.exit(0)
     if sys.argv[1:] == ["c4"]:
         dump_c4()
+        sys.exit(0)
+    if sys.argv[1:] == ["c5"]:
+        dump_c5()
         sys.exit(0)
     if sys.argv[1:] == ["shaw"]:
         dump_shaw_pipeline()

@@ -1043,3 +1043,13 @@ def test_shard_emulation_two_ranks(tmp_path):
         assert np.array_equal(o[0][f"{tag}_res"], o[1][f"{tag}_res"])
         # (fp32 Golub-Kahan envelope, DESIGN.md §6: 1e-5 through iteration 4, 1e-3 from 5 on)
         assert d["res"] <= 1e-3 and d["err"] <= 1e-3 and d["x"] <= 5e-3 and d["vs_1rank"] <= 1e-3, tag
+    # the one-pass plan is agreed over the ranks: with the pass allowed on every rank
+    # both take it; refused on the last rank only, both take the two-pass path and the solve is
+    # bitwise the one with the pass off everywhere (no mismatched collective sequence, no hang)
+    for r in range(2):
+        assert int(o[r]["tlsqr32_path"]) == 1 and int(o[r]["tlsmr32_path"]) == 1, r
+        for sv in ("q", "m"):
+            assert int(o[r][f"tmix{sv}_path"]) == 0 and int(o[r][f"toff{sv}_path"]) == 0, (r, sv)
+            for k_ in ("x", "res"):
+                assert np.array_equal(o[r][f"tmix{sv}_{k_}"], o[r][f"toff{sv}_{k_}"]), (r, sv, k_)
+    assert np.array_equal(o[0]["tmixm_ar"], o[1]["tmixm_ar"])
