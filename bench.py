@@ -39,20 +39,21 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
-# cpu_iters: iterations of the oracle timed for cpu_baseline (a bounded 10-30 s sample)
+# cpu_iters: iterations of the oracle timed for cpu_baseline (a bounded 10-30 s sample: the full maxit
+# where the per-iteration cost grows with k, a few iterations where the SpMVs dominate)
 WORKLOADS = {
     "c2": dict(N=512, angles=30, solver="hybrid_ab_gmres_rtp", maxit=20, lam=1e-2, cpu_iters=20),
-    "c3": dict(N=2048, angles=19, solver="hybrid_ba_gmres_rtp", maxit=20, lam=1e-2, cpu_iters=3),
+    "c3": dict(N=2048, angles=19, solver="hybrid_ba_gmres_rtp", maxit=20, lam=1e-2, cpu_iters=20),
     # BASELINE configs[2]: GCV lambda selection (k_gcv Arnoldi steps once, fminbnd on the
     # cached H: analyze_regularization.m:39-46) + the BA-GMRES solve at the chosen lambda
-    "c3gcv": dict(N=2048, angles=19, solver="hybrid_ba_gmres_rtp", maxit=20, lam=1e-2, cpu_iters=3,
+    "c3gcv": dict(N=2048, angles=19, solver="hybrid_ba_gmres_rtp", maxit=20, lam=1e-2, cpu_iters=20,
                   gcv=dict(k=20, lo=1e-8, hi=1.0, tolx=1e-10)),
-    "c4": dict(N=4096, angles=47, solver="ABgmres_nonhybrid_bounds", maxit=20, lam=0.0, cpu_iters=2,
+    "c4": dict(N=4096, angles=47, solver="ABgmres_nonhybrid_bounds", maxit=20, lam=0.0, cpu_iters=4,
                cpu_iters_single=1),
     # BASELINE configs[4]: the Golub-Kahan path on the 4096^2 operator in fp32
-    "c5": dict(N=4096, angles=47, solver="lsqr_solver", maxit=20, lam=0.0, f32=True, cpu_iters=2,
+    "c5": dict(N=4096, angles=47, solver="lsqr_solver", maxit=20, lam=0.0, f32=True, cpu_iters=4,
                cpu_iters_single=1),
-    "c5m": dict(N=4096, angles=47, solver="lsmr_solver", maxit=20, lam=0.0, f32=True, cpu_iters=2,
+    "c5m": dict(N=4096, angles=47, solver="lsmr_solver", maxit=20, lam=0.0, f32=True, cpu_iters=4,
                 cpu_iters_single=1),
 }
 UNITS = {"lsqr_solver": "LSQR iters/s", "lsmr_solver": "LSMR iters/s"}
@@ -485,10 +486,17 @@ def _host_cores():
 
 def cpu_baseline(A, B, b, x_true, wl, iters, iters_single):
     """The oracle restatement (the reference algorithm) on the same operator, timed on the
-    host: the process's OMP_NUM_THREADS cores (oracle/spmv_omp.c row-block SpMV, BLAS unrestricted; the products are
-    bitwise those of the one-core scipy leg) and, if iters_single > 0, one core (scipy CSR
-    SpMV, BLAS limited to one thread).  A timed solve includes the reference's setup
-    (r0, norms), so iters/s understates the CPU's steady rate by that share (stated)."""
+    host: the process's OMP_NUM_THREADS cores (oracle/spmv_omp.c row-block SpMV, BLAS
+    unrestricted; the products are bitwise those of the one-core scipy leg) and, if
+    iters_single > 0, one core (scipy CSR SpMV, BLAS limited to one thread).  fp32 workloads run
+    the fp32 restatement (lsqr_solver_f32 / lsmr_solver_f32: float32 operator and vectors, the
+    GPU's arithmetic type).  The restatement's iteration clock (oracle/restatement.py
+    iteration_clock) splits each timed solve into its setup (r0, norms: before the first
+    iteration) and its iterations; `value` is iterations / iteration time, the setup is stated
+    apart.  GMRES samples run the workload's full maxit where the per-iteration cost grows with k
+    (the MGS sweep, hybrid_ab_gmres_rtp's A*Qk), a few iterations where the SpMVs dominate (C4's
+    m-space basis is 2.2 MB a column)."""
+    import scipy.sparse as sp
     from oracle import parallel as OP
     from oracle import restatement as R
     try:
@@ -496,41 +504,60 @@ def cpu_baseline(A, B, b, x_true, wl, iters, iters_single):
     except ImportError:   # pragma: no cover
         threadpool_limits = None
     import contextlib
-    fn = getattr(R, wl["solver"])
+    f32 = bool(wl.get("f32"))
+    fn = getattr(R, wl["solver"] + ("_f32" if f32 else ""))
     gkb = wl["solver"] in UNITS
+    gcv = wl.get("gcv")
     unit = UNITS.get(wl["solver"], "GMRES iters/s")
-    As, Bs = A.to_scipy(), B.to_scipy()     # fp64 arithmetic on the fp32-rounded values for C5
+    As, Bs = A.to_scipy(), B.to_scipy()
+    if f32:
+        As = sp.csr_matrix((As.data.astype(np.float32), As.indices, As.indptr), shape=As.shape)
+        Bs = sp.csr_matrix((Bs.data.astype(np.float32), Bs.indices, Bs.indptr), shape=Bs.shape)
 
     def run(Aop, Bop, k):
-        if gkb:   # the restatement applies A' itself (lsqr_solver.m:10); here B = A' (device transpose)
-            args = (Aop, b, x_true, 0.0, k)
-        else:
-            args = (Aop, Bop, b, x_true, 0.0, k) + ((wl["lam"],) if wl["solver"] != "ABgmres_nonhybrid_bounds" else ())
+        """(iterations, setup s, iteration s) of one timed step of the workload on the oracle."""
+        n = Aop.shape[1]
         t0 = time.perf_counter()
-        out = fn(*args)
-        dt = time.perf_counter() - t0
+        with R.iteration_clock() as clk:
+            lam = wl["lam"]
+            if gcv:   # the c3gcv step: GCV on one Arnoldi, fminbnd, the solve at that lambda
+                import scipy.optimize as so
+                Hg, beta = R.arnoldi(Aop, Bop, b, gcv["k"], "ba")
+                lam = float(so.fminbound(lambda l_: R.gcv_from_H(Hg, beta, l_, n), gcv["lo"], gcv["hi"],
+                                         xtol=gcv["tolx"]))
+            if gkb:   # the restatement applies A' itself (lsqr_solver.m:10); here B = A' (device transpose)
+                args = (Aop, b, x_true, 0.0, k)
+            else:
+                args = (Aop, Bop, b, x_true, 0.0, k) + ((lam,) if wl["solver"] != "ABgmres_nonhybrid_bounds" else ())
+            out = fn(*args)
+            t1 = time.perf_counter()
+            ticks = list(clk)
         kk = out[-1] if wl["solver"] == "lsmr_solver" else out[3]
-        return kk, dt
+        # (c3gcv: the setup is the GCV Arnoldi's r0; the solve's own setup counts as step work)
+        return kk, ticks[0] - t0, t1 - ticks[0]
 
     OP.build()
     threads = OP.num_threads()
     PB = OP.ParallelCSR(Bs)
     PA = OP.ParallelCSR(As, T=PB if gkb else None)
-    k_all, dt_all = run(PA, PB, iters)
-    res = {"value": round(k_all / dt_all, 4), "unit": unit, "cores": threads, "kind": "port",
+    k_all, su, it_s = run(PA, PB, iters)
+    what = (f"one c3gcv step (the {gcv['k']}-step GCV Arnoldi, fminbnd, and a {k_all}-iteration solve)" if gcv else
+            f"a {k_all}-iteration solve" + (" (the workload's full maxit)" if k_all == wl["maxit"] else ""))
+    res = {"value": round(k_all / it_s, 4), "unit": unit, "cores": threads, "kind": "port",
+           "setup_s": round(su, 2), "iteration_s": round(it_s, 2),
            "nproc": _host_cores(), "cpu_model": _cpu_model(),
            "cores_reason": f"OpenMP threads = OMP_NUM_THREADS ({os.environ.get('OMP_NUM_THREADS', 'unset')}): the "
                            "host-core share of this process (the 1-GPU box grants 16 cores; nproc counts the whole "
                            "machine's CPUs, which other boxes' jobs use)",
-           "sample": f"oracle/restatement.py {wl['solver']} on the same {wl['N']}^2 operator, one complete "
-                     f"{k_all}-iteration solve incl. its setup ({dt_all:.1f} s), CSR SpMV on {threads} OpenMP "
-                     f"threads (oracle/spmv_omp.c, bitwise = scipy), numpy BLAS unrestricted"}
+           "sample": f"oracle/restatement.py {fn.__name__} on the same {wl['N']}^2 operator, {what}: setup "
+                     f"{su:.1f} s (before the first iteration, not in value) + iterations {it_s:.1f} s; CSR SpMV on "
+                     f"{threads} OpenMP threads (oracle/spmv_omp.c, bitwise = scipy), numpy BLAS unrestricted"}
     if iters_single > 0:
         with (threadpool_limits(limits=1) if threadpool_limits else contextlib.nullcontext()):
-            k1, dt1 = run(As, Bs, iters_single)
-        res["single_core"] = {"value": round(k1 / dt1, 4), "unit": unit, "cores": 1,
-                              "sample": f"same solver, {k1}-iteration solve incl. setup ({dt1:.1f} s), "
-                                        f"scipy CSR SpMV + numpy on 1 thread"}
+            k1, su1, it1 = run(As, Bs, iters_single)
+        res["single_core"] = {"value": round(k1 / it1, 4), "unit": unit, "cores": 1, "setup_s": round(su1, 2),
+                              "sample": f"same solver, {k1}-iteration solve: setup {su1:.1f} s apart, iterations "
+                                        f"{it1:.1f} s; scipy CSR SpMV + numpy on 1 thread"}
     return res
 
 

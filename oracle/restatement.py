@@ -42,6 +42,7 @@ orders on the GPU, so the two agree to the last bit on the Krylov recurrences.
 from __future__ import annotations
 
 import contextlib
+import time
 
 import numpy as np
 import scipy.linalg as sla
@@ -54,6 +55,27 @@ _FIX_CH = 64        # chunk length of _fsum (kernels.hip FIX_CH)
 
 class OutputNotAssigned(RuntimeError):
     """MATLAB: 'Output argument "x" not assigned during call'."""
+
+
+# Iteration clock (bench.py cpu_baseline): while `iteration_clock()` is active, every solver loop
+# appends time.perf_counter() at the top of each iteration, so the caller can time the setup
+# (before the first tick) apart from the iterations.  No effect on any result.
+_CLOCK = None
+
+
+def _tick():
+    if _CLOCK is not None:
+        _CLOCK.append(time.perf_counter())
+
+
+@contextlib.contextmanager
+def iteration_clock():
+    global _CLOCK
+    prev, _CLOCK = _CLOCK, []
+    try:
+        yield _CLOCK
+    finally:
+        _CLOCK = prev
 
 
 @contextlib.contextmanager
@@ -376,6 +398,7 @@ def hybrid_ba_gmres_rtp(A, B, b, x_true, tol, maxit, lam, return_H=False, orth="
     nb, nxt = _norm(b), _norm(x_true)
     k = 0
     for k in range(maxit):                       # :18
+        _tick()
         v = M_reg(Q[:, k])                       # :19
         if _arnoldi_step(Q, H, k, v, orth=orth): # :20-26
             break
@@ -410,6 +433,7 @@ def hybrid_ab_gmres_rtp(A, B, b, x_true, tol, maxit, lam, return_H=False):
     x = None
     k = 0
     for k in range(maxit):                       # :18
+        _tick()
         v = M_reg_op(Q[:, k])                    # :19
         if _mgs_arnoldi_step(Q, H, k, v):        # :20-26
             break
@@ -446,6 +470,7 @@ def lsqr_solver(A, b, x_true, tol, maxit):
     nb, nxt = _norm(b), _norm(x_true)
     k = 0
     for k in range(maxit):                       # :20
+        _tick()
         u_hat = A @ v - alpha * u                # :22
         beta = _norm(u_hat)                      # :23
         u = u_hat / beta                         # :24
@@ -507,6 +532,7 @@ def lsmr_solver(A, b, x_true=None, tol=None, maxit=None):
         normA = float(sp.linalg.norm(A, "fro")) if sp.issparse(A) else float(np.linalg.norm(A, "fro"))
     k = 0
     for k in range(maxit):                       # :32
+        _tick()
         u = A @ v - alpha * u                    # :34
         beta = _norm(u)                          # :35
         if beta > 0:
@@ -742,6 +768,7 @@ def _gmres_ptr(A, B, b, x_true, tol, maxit, lam, side, hybrid, explicit_BA=False
     xk = None
     k = 0
     for k in range(maxit):                       # :24
+        _tick()
         v = op(Q[:, k])                          # :25
         if _mgs_arnoldi_step(Q, H, k, v):        # :26-32
             break
@@ -823,6 +850,7 @@ def arnoldi(A, B, b, k_gcv, gcv_type, breakdown_tol=1e-12, orth="mgs"):
     H = np.zeros((k_gcv + 1, k_gcv))             # :14
     Q[:, 0] = r0 / beta                          # :15
     for k in range(k_gcv):                       # :18
+        _tick()
         v = op(Q[:, k])
         if _arnoldi_step(Q, H, k, v, breakdown_tol=breakdown_tol, orth=orth):   # :25-31
             break
@@ -930,6 +958,7 @@ def lsqr_solver_f32(A, b, x_true, tol, maxit):
     residual_norm = np.zeros(maxit)
     k = 0
     for k in range(maxit):                       # :20
+        _tick()
         u_hat = _mv32(A, v) - f32(alpha) * u     # :22
         beta = _nrm32(u_hat)                     # :23
         u = u_hat / f32(beta)                    # :24
@@ -991,6 +1020,7 @@ def lsmr_solver_f32(A, b, x_true=None, tol=None, maxit=None):
     ar_hist = np.zeros(maxit)                    # :30
     k = 0
     for k in range(maxit):                       # :32
+        _tick()
         u = _mv32(A, v) - f32(alpha) * u         # :34
         beta = _nrm32(u)                         # :35
         if beta > 0:
