@@ -409,6 +409,8 @@ extern "C" {
 
 HGM_API int hgm_version(void) { return HGM_VERSION; }
 
+HGM_API int hgm_experiments(void) { return HGM_EXPERIMENTS; }
+
 HGM_API int hgm_runtime_check(char* msg, int len) {
     const std::set<std::string> names = hip_runtimes();
     if (msg && len > 0) {
@@ -519,6 +521,26 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
         c->err = std::string("hgm_ctx_set_option: ") + what;
         return HGM_E_ARG;
     };
+    if (!HGM_EXPERIMENTS) {
+        // measured variants of the one-pass kernel: compiled into the experiments build only
+        bool variant = false;
+        switch (option) {
+            case HGM_OPT_FUSED_REGION: variant = v != 64; break;
+            case HGM_OPT_FUSED_BS: variant = v != 1024; break;
+            case HGM_OPT_FUSED_DBG: variant = v != 0; break;
+            case HGM_OPT_FUSED_PF: variant = v != 2; break;
+            case HGM_OPT_FUSED_KIND: variant = v != 1; break;
+            case HGM_OPT_FUSED_WAVES: variant = v != 4; break;
+            case HGM_OPT_FUSED_GROUP: variant = v != 8; break;
+            case HGM_OPT_FUSED_DEPTH: variant = v != 2; break;
+            case HGM_OPT_FUSED_PAIRS: variant = v != 1; break;
+            case HGM_OPT_FUSED_ACC32: variant = v != 1; break;
+            case HGM_OPT_FUSED_REDUCE: variant = !(v == 0 || v == 1); break;
+            case HGM_OPT_FUSED_ROWPAIR: variant = !(v == 0 || v == 4); break;
+            default: break;
+        }
+        if (variant) return bad("a measured variant of the one-pass kernel: experiments build only (HGM_EXPERIMENTS=1)");
+    }
     switch (option) {
         case HGM_OPT_PARITY: if (!b01) return bad("parity is 0 or 1"); n.parity = v != 0; break;
         case HGM_OPT_MGS_FORM: if (!b01) return bad("mgs form is 0 or 1"); n.mgs_form = (int)v; break;

@@ -1338,8 +1338,12 @@ FusedPlan* fused_plan_build(hgm_ctx* c, const hgm_mat* B, int R) {
 namespace {
 // (waves, LDS ray slots) of the instantiated kernels, 64 slots of each being the lanes' dummies;
 // the plan takes the fewest slots that hold its regions' rays (more workgroups per CU)
+#if HGM_EXPERIMENTS
 #define HGM_RW_SHAPES(X) X(1, 1088) X(1, 2048) X(1, 4096) X(2, 1088) X(2, 1536) X(2, 2048) X(2, 4096) \
     X(4, 1088) X(4, 1344) X(4, 1536) X(4, 2048)
+#else
+#define HGM_RW_SHAPES(X) X(4, 1088) X(4, 1344) X(4, 1536) X(4, 2048)
+#endif
 constexpr int RW_SLOTS_MAX = 4096;
 constexpr int RW_ROW_MAX = 255;                   // entries per pixel row (two chunks of 128, pairs)
 }  // namespace
@@ -1872,9 +1876,11 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
     if (P->rowpair) {
         // row pairs: the production accumulation, four waves, one chunk, 8-row batches, depth 2
         constexpr int AMP = sizeof(T) == 4 ? 1 : 0;
+#if HGM_EXPERIMENTS
         if constexpr (sizeof(T) == 4)            // fp64 accumulators (ds_add_f64) with mode 4: measured variant
             if (am == 2 && P->rowpair == 4 && !dbg && W == 4 && G == 8 && NC == 1 && PRm && D == 2 && MR == 2048)
                 HGM_RWLR(2, 4, 2048, 8, 1, 2, true, 0, 4)
+#endif
         if (dbg || W != 4 || G != 8 || NC != 1 || !PRm || D != 2 || am != AMP) {
             if (dry) return false;
             throw Error{HGM_E_ARG, "fused A*(B*q): row pairs take 4 waves, 8 rows, one chunk, pairs, depth 2, "
@@ -1888,9 +1894,11 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
             if (MR == 1536) HGM_RWLR(AMP, 4, 1536, 8, 1, 2, true, 0, 4)
             if (MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 4)
         }
+#if HGM_EXPERIMENTS
         if (P->rowpair == 3 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 3)
         if (P->rowpair == 1 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 1)
         if (P->rowpair == 2 && MR == 2048) HGM_RWLR(AMP, 4, 2048, 8, 1, 2, true, 0, 2)
+#endif
         if (dry) return false;
         throw Error{HGM_E_ARG, "fused A*(B*q): no row-pair kernel for this plan's shape and the options"};
     }
@@ -1898,18 +1906,23 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
         constexpr int AMP = sizeof(T) == 4 ? 1 : 0;    // the production accumulation of this T
         const bool dshape = W == 4 && MR == 2048 && G == 8 && NC == 1 && PRm && D == 2;
         if (dbg) {   // timing experiments (hgm_spmv_ab only): the default shape
+#if HGM_EXPERIMENTS
             if (dshape && am == AMP) {
 #define HGM_RWD(DV) if (dbg == DV) HGM_RWL(AMP, 4, 2048, 8, 1, 2, true, DV)
                 HGM_RWD(1) HGM_RWD(2) HGM_RWD(4) HGM_RWD(7)
 #undef HGM_RWD
             }
+#endif
             if (dry) return false;
             throw Error{HGM_E_ARG, "fused_dbg (Golub-Kahan / fp32 pass): waves 4, 2048 slots, 8 rows, pairs, depth 2, one chunk; 1, 2, 4 or 7"};
         }
+#if HGM_EXPERIMENTS
         if constexpr (sizeof(T) == 4) {   // the other fp32 accumulations: the default shape (measurements)
             if (dshape && am == 0) HGM_RWL(0, 4, 2048, 8, 1, 2, true, 0)
             if (dshape && am == 2) HGM_RWL(2, 4, 2048, 8, 1, 2, true, 0)
         }
+#endif
+        (void)dshape;
         if (am == AMP) {
 #define HGM_RW(WV, MRV)                                                                                              \
     if (W == WV && MR == MRV && G == 8 && PRm && D == 2) {                                                           \
@@ -1921,11 +1934,13 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
         }
     } else {
         if (dbg) {   // timing experiments: the default shape only
+#if HGM_EXPERIMENTS
             if (W == 4 && MR == 2048 && G == 8 && NC == 1 && PRm && D == 2) {
 #define HGM_RWD(DV) if (dbg == DV) HGM_RWL(0, 4, 2048, 8, 1, 2, true, DV)
                 HGM_RWD(1) HGM_RWD(2) HGM_RWD(3) HGM_RWD(4) HGM_RWD(5) HGM_RWD(6) HGM_RWD(7)
 #undef HGM_RWD
             }
+#endif
             if (dry) return false;
             throw Error{HGM_E_ARG, "fused_dbg with the row-wave pass: waves 4, 2048 slots, 8 rows, pairs, depth 2, one chunk"};
         }
@@ -1938,6 +1953,7 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
     }
         HGM_RW_SHAPES(HGM_RW)
 #undef HGM_RW
+#if HGM_EXPERIMENTS
         if (W == 4 && MR == 2048 && NC == 1 && PRm) {
             if (G == 8 && D == 3) HGM_RWL(0, 4, 2048, 8, 1, 3, true, 0)
             if (G == 4 && D == 2) HGM_RWL(0, 4, 2048, 4, 1, 2, true, 0)
@@ -1947,6 +1963,7 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
             if (G == 8) HGM_RWL(0, 4, 2048, 8, 2, 2, false, 0)
             if (G == 4) HGM_RWL(0, 4, 2048, 4, 2, 2, false, 0)
         }
+#endif
     }
 #undef HGM_RWL
 #undef HGM_RWLR
@@ -1983,6 +2000,9 @@ bool fused_pass(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArg
         else if constexpr (sizeof(T) == 8) fused_rw_launch<T, false>(c, B, P, fa, false);
     } else {
         HGM_REQUIRE(!gk && sizeof(T) == 8, "fused pass: the sub-chunk kernel is fp64 without epilogues");
+#if !HGM_EXPERIMENTS
+        HGM_REQUIRE(false, "fused pass: the sub-chunk kernel (kind 0) is in the experiments build only");
+#else
         if constexpr (sizeof(T) == 8) {
 #define HGM_FUSED_LAUNCH(FB, FGV, PFV)                                                                          \
     launch(c, false, k_fused_ab<FB, FGV, PFV>, dim3((unsigned)P->nreg), dim3(FB), (const FusedSub*)P->subs,      \
@@ -2004,6 +2024,7 @@ bool fused_pass(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArg
             }
 #undef HGM_FUSED_LAUNCH
         }
+#endif
     }
     // one lane group per ray, no grid-stride cap (C4: 8,508 blocks; the 4,096 cap measured 5 us slower)
     const unsigned rgrid = (unsigned)std::max<int64_t>(1, (P->m * HGM_FUSED_RG + BS - 1) / BS);
@@ -2018,6 +2039,7 @@ bool fused_pass(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArg
             launch(c, true, k_fused_reduce_band<T, T>, dim3(bgrid), dim3(BS), P->m, P->nband,
                    (const int32_t*)P->band_ptr, (const int4*)P->band_run, (const T*)P->part, fa.w,
                    (const T*)P->zx_part, (int)P->nreg, side ? fa.side_out : nullptr);
+#if HGM_EXPERIMENTS
     } else if (f64p) {
         launch(c, true, k_fused_reduce<HGM_FUSED_RG, T, double>, dim3(rgrid), dim3(BS), P->m,
                (const int64_t*)P->rs_ptr, (const int32_t*)P->rs_slot, (const double*)P->part, fa.w,
@@ -2035,6 +2057,7 @@ bool fused_pass(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArg
         else if (rg == 2) HGM_RED(2, 8);
         else HGM_RED(4, 4);
 #undef HGM_RED
+#endif
     } else {
         launch(c, true, k_fused_reduce<HGM_FUSED_RG, T>, dim3(rgrid), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
                (const int32_t*)P->rs_slot, (const T*)P->part, fa.w, (const T*)P->zx_part, (int)P->nreg,

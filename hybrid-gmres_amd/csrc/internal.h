@@ -14,6 +14,15 @@
 
 #include "hgmres.h"
 
+// Measured variants of the one-pass kernel (the kind-0 sub-chunk pass, row-pair modes 1-3, other
+// wave / batch / depth / pairing shapes, other fp32 accumulations and reductions, the phase-skipping
+// timing bits) are compiled only into an experiments build (make EXTRA=-DHGM_EXPERIMENTS=1, used by
+// scripts/fused_micro.py); the default library carries the production kernels alone and refuses
+// those option values (hgm_ctx_set_option, hgm_experiments()).
+#ifndef HGM_EXPERIMENTS
+#define HGM_EXPERIMENTS 0
+#endif
+
 namespace hgm {
 
 struct Error {

@@ -130,14 +130,18 @@ def siddon_projector(N: int, n_angles: int, chunk_elems: int = 1 << 24) -> sp.cs
     return A
 
 
-FAN_R = 2.0          # source-to-centre distance in units of N (AIR Tools II fanbeamtomo's default R)
+FAN_R = 2.0          # source-to-centre distance in units of N (this repository's choice; see fan_geometry)
 
 
 def fan_geometry(N: int, n_angles: int, R: float = FAN_R, span: float | None = None,
                  det_offset: float = DETECTOR_OFFSET):
-    """Fan-beam, curved (equiangular) detector geometry -- the CTtype 'fancurved' of
-    run_2D_phantom.m:12-13 (PRtomo_mismatched, not vendored by the reference: its exact
-    parameters are unknown, so this follows the published AIR Tools II fanbeamtomo conventions):
+    """Fan-beam, curved (equiangular) detector geometry standing in for the CTtype 'fancurved' of
+    run_2D_phantom.m:12-13.  PRtomo_mismatched is not vendored by the reference and no fixture of
+    it exists, so this geometry is the repository's OWN choice, modelled on a curved-detector fan
+    beam; parity with PRtomo_mismatched / AIR Tools II fanbeamtomo is UNPINNED.  Its
+    departures from fanbeamtomo as commonly documented (unverifiable offline): p = ceil(sqrt(2) N)
+    rays per source (fanbeamtomo reportedly rounds), a fan span fitted to the circumscribed circle
+    rather than a user angle, and source angles equispaced over a full turn.  The geometry:
     * source angles beta_a = a * 2 pi / n_angles (a full turn), the source at distance D = R N
       from the centre, S_a = D (cos beta_a, sin beta_a);
     * p = ceil(sqrt(2) N) rays per source position at fan angles

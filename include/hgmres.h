@@ -128,30 +128,34 @@ enum hgm_ctx_option {
                                       of one: on a communicator every rank runs it on its shard, followed by
                                       the m-vector all-reduce) [1]: the kept B*q and A*(B*q) come out of one
                                       kernel (plan built on first use) */
-    HGM_OPT_FUSED_REGION = 19,     /* ... pixel square (side) per workgroup of that pass [64] */
-    HGM_OPT_FUSED_BS = 20,         /* ... threads per workgroup: 512 or 1024 [1024] (same summation order) */
-    HGM_OPT_FUSED_DBG = 21,        /* ... timing experiments only: bits skip its phases, results WRONG [0] */
-    HGM_OPT_FUSED_PF = 22,         /* ... pipeline depth: sub-chunk batches in registers, 1..4
-                                      (0 = 1: no prefetch) [2] */
+    /* [experiments] options 19-22, 24, 26-30 and the marked values of 32 and 34 select measured
+     * variants of the one-pass kernel (DESIGN.md §3.5 records each measurement): only an experiments
+     * build (hgm_experiments() == 1) has their kernels; the default library accepts only the
+     * production value in brackets. */
+    HGM_OPT_FUSED_REGION = 19,     /* [experiments] kind-0 pass: pixel square per workgroup [64] */
+    HGM_OPT_FUSED_BS = 20,         /* [experiments] kind-0 pass: 512 or 1024 threads [1024] */
+    HGM_OPT_FUSED_DBG = 21,        /* [experiments] timing only: bits skip the pass's phases, results WRONG;
+                                      hgm_spmv_ab only, every solver refuses it [0] */
+    HGM_OPT_FUSED_PF = 22,         /* [experiments] kind-0 pass: sub-chunk batches in registers 1..4 [2] */
     HGM_OPT_KRYLOV_PAD = 23        /* elements added to the Krylov basis' leading dimension when it
                                       is a multiple of 4096 (a power-of-two column stride sends
                                       every column's element i to the same HBM channel) [-1 = auto] */,
-    HGM_OPT_FUSED_KIND = 24,       /* ... kernel of the one-pass A*(B*q): 0 sub-chunk pass (options 19-22),
-                                      1 row-wave pass (options 25-27) [1] */
+    HGM_OPT_FUSED_KIND = 24,       /* [experiments] kernel of the one-pass A*(B*q): 0 the sub-chunk pass
+                                      (options 19-22), 1 the row-wave pass [1] */
     HGM_OPT_FUSED_WREGION = 25,    /* ... row-wave pass: pixel square (side) per workgroup [32] */
-    HGM_OPT_FUSED_WAVES = 26,      /* ... row-wave pass: waves per workgroup, 1, 2 or 4 [4] */
-    HGM_OPT_FUSED_GROUP = 27,      /* ... row-wave pass: pixel rows per load batch, 4 or 8 [8] */
-    HGM_OPT_FUSED_DEPTH = 28,      /* ... row-wave pass: batches in its load ring, 2..4 [2] */
-    HGM_OPT_FUSED_PAIRS = 29,      /* ... row-wave pass: two entries per lane (16-byte value pairs) [1] */
-    HGM_OPT_FUSED_ACC32 = 30       /* ... fp32 operators (lsqr_solver / lsmr_solver of BASELINE configs[4]): how
-                                      the pass accumulates a region's rays: 0 ds_add_f32, 1 fp32
-                                      read-add-write, 2 fp64 accumulators and partials (ds_add_f64) [1] */,
+    HGM_OPT_FUSED_WAVES = 26,      /* [experiments] row-wave pass: waves per workgroup, 1, 2 or 4 [4] */
+    HGM_OPT_FUSED_GROUP = 27,      /* [experiments] row-wave pass: pixel rows per load batch, 4 or 8 [8] */
+    HGM_OPT_FUSED_DEPTH = 28,      /* [experiments] row-wave pass: batches in its load ring, 2..4 [2] */
+    HGM_OPT_FUSED_PAIRS = 29,      /* [experiments] row-wave pass: two entries per lane [1] */
+    HGM_OPT_FUSED_ACC32 = 30       /* [experiments] fp32 pass (lsqr_solver / lsmr_solver of configs[4]): how a
+                                      region's rays accumulate: 0 ds_add_f32, 1 fp32 read-add-write,
+                                      2 fp64 accumulators and partials [1] */,
     HGM_OPT_FUSED_PLAN_DEV = 31,   /* ... the row-wave plan's region ray sets and slots built on the device
                                       (an LDS bitmap per region) [1]; 0 the host build (same bytes) */
     HGM_OPT_FUSED_REDUCE = 32,     /* ... the row-wave pass's partial reduction: 1 by bands of 64 rays over
                                       runs of consecutive slots, 0 per ray through its slot list [0] (the
-                                      same sums: bitwise equal); 2, 3, 4: per ray with 1, 2 or 4 lanes per
-                                      ray instead of 8 (another fixed order) */
+                                      same sums: bitwise equal); [experiments] 2, 3, 4: per ray with 1, 2
+                                      or 4 lanes per ray instead of 8 (another fixed order) */
     HGM_OPT_HOST_SPIN_US = 33      /* host waits (stream / event / ring polls): microseconds of pure spinning
                                       before each further poll yields the core (sched_yield) [200; -1 when
                                       the process's CPU affinity holds fewer than 4 cores]; < 0: the
@@ -160,10 +164,10 @@ enum hgm_ctx_option {
     HGM_OPT_FUSED_ROWPAIR = 34     /* ... row-wave pass: two consecutive pixel rows per 128-entry chunk [4]:
                                       0 one row per chunk; 4 the second row right after the first, one
                                       accumulator array per wave, the two rows' q reads and adds by two
-                                      instructions each (other lanes on their dummy slot); 1 (a private
-                                      array per row parity), 2 (the second row from the lane after the first
-                                      row's last pair) and 3 (the row split by selects of the products) are
-                                      measured variants of the 2048-slot shape only */,
+                                      instructions each (other lanes on their dummy slot); [experiments]
+                                      1 (a private array per row parity), 2 (the second row from the lane
+                                      after the first row's last pair), 3 (the row split by selects of the
+                                      products): the 2048-slot shape only */,
     HGM_OPT_LSQR_RES_IMG = 35      /* one-pass lsqr_solver: the exact final residual norm(b - A*x) of
                                       lsqr_solver.m:52 from A*x kept in double alongside x (A*v_k is the
                                       pass's A*v_hat / alpha) instead of one more SpMV [1] */,
@@ -178,6 +182,10 @@ typedef int (*hgm_allreduce_fn)(double* buf, int64_t count, void* user);
 
 /* ---- context ---------------------------------------------------------- */
 HGM_API int hgm_version(void);
+/* 1 for an experiments build (make EXTRA=-DHGM_EXPERIMENTS=1), which also carries the measured
+ * variants of the one-pass kernel that the options marked [experiments] below select; the default
+ * library (0) has the production kernels only and refuses those values with HGM_E_ARG. */
+HGM_API int hgm_experiments(void);
 /* Number of distinct HIP runtime files (libamdhip64*) mapped into the process, their paths
  * ';'-separated in msg.  More than one (e.g. PyTorch's bundled copy loaded AFTER this library
  * pulled /opt/rocm's) is refused: hgm_ctx_create then fails with HGM_E_HIP.  Load PyTorch
@@ -242,10 +250,11 @@ HGM_API int hgm_mat_create_siddon(hgm_ctx* ctx, int N, int n_angles, double det_
  * tile must divide N (and super); super must divide N. */
 HGM_API int hgm_mat_create_siddon_ordered(hgm_ctx* ctx, int N, int n_angles, double det_offset,
                                           int dtype, int tile, int super_block, hgm_mat** out);
-/* Fan-beam projector with a curved (equiangular) detector generated on the device -- the CTtype
- * 'fancurved' of run_2D_phantom.m:12-13 (PRtomo_mismatched is not vendored by the reference; the
- * geometry follows AIR Tools II fanbeamtomo's published conventions, hgmres.problems.fan_geometry,
- * bit-identical to hgmres.problems.fanbeam_projector): n_angles source positions over a full turn
+/* Fan-beam projector with a curved (equiangular) detector generated on the device, standing in
+ * for the CTtype 'fancurved' of run_2D_phantom.m:12-13.  PRtomo_mismatched is not vendored by the
+ * reference, so the geometry is this library's own choice (hgmres.problems.fan_geometry lists its
+ * departures from AIR Tools II fanbeamtomo; parity with either is unpinned), bit-identical to
+ * hgmres.problems.fanbeam_projector: n_angles source positions over a full turn
  * at distance R*N from the centre (R > 1/sqrt(2)), p = ceil(sqrt(2) N) rays per source at
  * equiangular fan angles ((d - (p-1)/2) + det_offset) * span / p; span <= 0 selects the fan that
  * covers the image's circumscribed circle, 2 asin(1 / (sqrt(2) R)).  Rows a*p + d; tile /
