@@ -1,5 +1,6 @@
-"""BASELINE configs[2]-[4] at full size on one MI355X ("configs untested").
+"""BASELINE configs[1]-[4] at full size on one MI355X.
 
+* C2 (512^2, 30 angles): hybrid_ab_gmres_rtp at the bench's 20 iterations vs tests/golden/c2_512.npz.
 * C3 (2048^2, 19 angles, nnz 1.01e8) at the bench's iteration counts: the 20-step GCV Arnoldi,
   fminbnd on it with the bench's bounds, and 20-iteration BA-GMRES at lambda 1e-2 and at the GCV
   lambda, MGS and CGS2, against the committed oracle fixture tests/golden/c3_2048.npz (operator
@@ -9,14 +10,14 @@
   difference at k = 20 is 9.0e-12 (make_golden.py prints it).
 * C4 (4096^2, 47 angles, nnz 1.0e9): ABgmres_nonhybrid_bounds (the configs[3] AB-GMRES)
   through the bench's 20 iterations against the oracle fixture tests/golden/c4_4096.npz (H, x,
-  histories at 1e-10; operator pinned by CSR hash), plus size-independent properties
-  (Hessenberg structure, monitors consistent with the returned x).
-* C5 (configs[4], fp32 operator at 4096^2): LSQR / LSMR through 20 iterations, properties,
-  and agreement with the fp64 solve at k = 4 (fp32 Golub-Kahan departs from fp64 after a few
-  steps, as a numpy float32 emulation does too; tests/test_gpu_parity.py::test_lsqr_fp32).
-  Against the fp32 oracle (oracle/restatement.py lsqr_solver_f32 / lsmr_solver_f32, the
-  reference's loops in fp32, fixed order) on the downloaded operator: parity mode bit-identical
-  through 8 iterations, and the production kernels within the stated envelope.
+  histories at 1e-10; operator pinned by CSR hash), on one GPU and as 2, 4 and 8 pixel shards
+  (one process per shard on this GPU, the host all-reduce hook), plus size-independent
+  properties (Hessenberg structure, monitors consistent with the returned x).
+* C5 (configs[4], fp32 operator at 4096^2): LSQR / LSMR through the bench's 20 iterations against
+  the fp32 oracle (tests/golden/c5_4096.npz: oracle/restatement.py lsqr_solver_f32 /
+  lsmr_solver_f32 on the same fp32 operator, pinned by hash): parity mode bit-identical, and the
+  production kernels -- one GPU and 2, 4, 8 shards -- within 100 x the oracle's own spread over
+  8 other fp32 summation orders at every iteration.
 """
 import gc
 
@@ -301,19 +302,21 @@ def _run_ranks(tmp_path, world, mode):
 
 def _c5_envelope_check(label, hists, x_s, g, tag, nh):
     """Every history entry (k = 1..20) and the sampled x of a production fp32 Golub-Kahan solve
-    within max(1e-6, 100 x) the fp32 oracle's own spread over 8 other summation orders
-    (tests/golden/c5_4096.npz, make_golden.py dump_c5; VERDICT r5 "Next" #2)."""
+    within max(1e-5, 100 x) the fp32 oracle's own spread over 8 other summation orders of its
+    SpMVs (tests/golden/c5_4096.npz, make_golden.py dump_c5; VERDICT r5 "Next" #2).  The floor:
+    where every order gives the same entry, the device still sums its fp32 norms (16.7M and 272k
+    terms) in another order than the oracle; 1e-5 is ~100 x fp32's unit roundoff (6e-8)."""
     names = ["err", "res", "ar"][:nh]
     worst = []
     for i, nm in enumerate(names):
         ref, spr = g[f"{tag}_{nm}"], g[f"{tag}_spread_{nm}"]
         d = np.abs(np.asarray(hists[i]) - ref) / np.abs(ref)
-        bar = np.maximum(1e-6, 100.0 * spr)
+        bar = np.maximum(1e-5, 100.0 * spr)
         worst.append((nm, float(np.max(d)), float(np.max(d / bar))))
         assert np.all(d <= bar), (label, nm, int(np.argmax(d / bar)) + 1, float(np.max(d / bar)))
     xs = g[f"{tag}_xs"].astype(np.float64)
     dx = float(np.linalg.norm(np.asarray(x_s) - xs) / np.linalg.norm(xs))
-    xbar = max(1e-6, 100.0 * float(g[f"{tag}_spread_xs"]))
+    xbar = max(1e-5, 100.0 * float(g[f"{tag}_spread_xs"]))
     print(f"[{label}] vs fp32 oracle over 20 iterations: " +
           "; ".join(f"{nm} max dev {a:.1e} = {f_:.3f} of the bar" for nm, a, f_ in worst) +
           f"; x dev {dx:.1e} = {dx / xbar:.3f} of the bar (oracle spread {float(g[f'{tag}_spread_xs']):.1e})")
