@@ -900,17 +900,36 @@ def gcv_function(lam, A, B, b, m, k_gcv, gcv_type):
 f32 = np.float32
 
 
+_F32_SUM = (64, False)   # (chunk, reversed) of _fsum32: (64, False) is the documented fixed order
+
+
+@contextlib.contextmanager
+def fsum32_order(chunk, reverse):
+    """_fsum32 in ANOTHER fixed order (chunk length, terms reversed) -- test infrastructure: the
+    fp32 oracle's own rounding spread over correct fp32 orders (tests/golden/make_golden.py
+    dump_c5).  Never used by the parity checks."""
+    global _F32_SUM
+    prev, _F32_SUM = _F32_SUM, (int(chunk), bool(reverse))
+    try:
+        yield
+    finally:
+        _F32_SUM = prev
+
+
 def _fsum32(p):
     """_fsum's order (64-term chunks, then 64-value chunks of those, then left to right) with
     every partial sum rounded to float32 (np.cumsum accumulates in the array's dtype)."""
     p = np.ascontiguousarray(p, dtype=np.float32).ravel()
     if p.size == 0:
         return f32(0.0)
+    ch, rev = _F32_SUM
+    if rev:
+        p = p[::-1]
     for _ in range(2):
-        r = (-p.size) % _FIX_CH
+        r = (-p.size) % ch
         if r:
             p = np.concatenate([p, np.zeros(r, dtype=np.float32)])
-        p = np.cumsum(p.reshape(-1, _FIX_CH), axis=1, dtype=np.float32)[:, -1]
+        p = np.cumsum(p.reshape(-1, ch), axis=1, dtype=np.float32)[:, -1]
     return f32(np.cumsum(p, dtype=np.float32)[-1])
 
 

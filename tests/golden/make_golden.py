@@ -161,8 +161,10 @@ class _Ordered32:
         return self.PM.val
 
 
-# the alternative orders of dump_c5: (accumulators, reversed)
-C5_ORDERS = ((1, 1), (2, 0), (4, 1), (8, 0), (16, 1), (32, 0), (64, 1), (128, 0))
+# the alternative orders of dump_c5: SpMV rows (accumulators, reversed) and the fp32 sums of
+# squares (chunk, reversed; restatement.fsum32_order) -- the device sums both in other orders
+C5_ORDERS = ((1, 1, 16, 1), (2, 0, 32, 0), (4, 1, 128, 1), (8, 0, 256, 0), (16, 1, 16, 0), (32, 0, 512, 1),
+             (64, 1, 64, 1), (128, 0, 32, 1))
 
 
 def csr_hash32(M):
@@ -180,9 +182,10 @@ def dump_c5(name="c5_4096.npz", k=20, stride=197):
     in fp32 (the restatement's lsqr_solver_f32 / lsmr_solver_f32: float32 operator, vectors and
     fixed-order sums), all 20 iterations of the bench, with the fixture's b (c4_4096.npz, the
     fp64 operator's A x_true + 1 % noise).  Plus the oracle's OWN fp32 rounding spread: the same
-    solves with every SpMV summed in each of the 8 other orders of C5_ORDERS (_Ordered32); per
-    history entry the largest relative deviation from the sequential-order run, and for x the
-    largest normwise deviation over the samples x[::stride].  The production test holds the device within 100 x
+    solves with every SpMV and every fp32 sum of squares summed in each of the 8 other orders of
+    C5_ORDERS (_Ordered32, restatement.fsum32_order); per history entry the largest relative
+    deviation from the documented-order run, and for x the largest normwise deviation over the
+    samples x[::stride].  The production test holds the device within 100 x
     that spread at every iteration (VERDICT r5 "Next" #2).  The fp32 operator is pinned by the
     sha256 of (indptr, indices, float32 data) in reference pixel order.  ~40 GB, ~40 min on 8 cores."""
     import gc
@@ -213,14 +216,15 @@ def dump_c5(name="c5_4096.npz", k=20, stride=197):
         print(f"{tag} fixed order: {time.time() - t0:.0f} s, res {ref[2][-1]:.6e}", flush=True)
         xs = ref[0][::stride].astype(np.float64)
         sx, sh = 0.0, [np.zeros(k) for _ in range(nh)]
-        for ways, rev in C5_ORDERS:
+        for ways, rev, ch, nrev in C5_ORDERS:
             t0 = time.time()
-            p = fn(_Ordered32(PA, ways, rev), b, xt, 0.0, k)
+            with R.fsum32_order(ch, nrev):
+                p = fn(_Ordered32(PA, ways, rev), b, xt, 0.0, k)
             ps = p[0][::stride].astype(np.float64)
             sx = max(sx, float(np.linalg.norm(ps - xs) / np.linalg.norm(xs)))
             for i in range(nh):
                 sh[i] = np.maximum(sh[i], np.abs(p[1 + i] - ref[1 + i]) / np.abs(ref[1 + i]))
-            print(f"  order {ways}/{rev}: {time.time() - t0:.0f} s, spread x {sx:.2e} hist "
+            print(f"  order {ways}/{rev}/{ch}/{nrev}: {time.time() - t0:.0f} s, spread x {sx:.2e} hist "
                   + " ".join(f"{float(np.max(s)):.1e}" for s in sh), flush=True)
         hn = ["err", "res", "ar"][:nh]
         d.update({f"{tag}_k": int(ref[-1]), f"{tag}_xs": ref[0][::stride].copy(), f"{tag}_xnorm":
