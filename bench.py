@@ -86,6 +86,10 @@ def parse():
     ap.add_argument("--shard-of", type=int, default=1, metavar="N",
                     help="with --shard1: solve rank 0's pixel shard of an N-way cut (per-rank kernel costs at "
                          "N GPUs, without the transport; the solve is then of that shard alone)")
+    ap.add_argument("--shard-rank", type=int, default=0, metavar="R",
+                    help="with --shard1 --shard-of N: solve rank R's shard instead of rank 0's (rank 0's shard of "
+                         "an 8-way C4 cut is all background, x_true = 0 there, which sends the shard's own error "
+                         "monitor to the x-forming reconstruction on the step stream: not the global solve's path)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="experiment: per-context numerics option (hgm_ctx_set_option), e.g. mgs_fused=0")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -251,7 +255,7 @@ def main():
         else:
             ctx = init_context(local, rank, world, one_rank_comm=args.shard1)
         cut = args.shard_of if args.shard1 else world
-        A, B, b, x_true, (lo, hi), full = build_shard(ctx, wl, rank, cut)
+        A, B, b, x_true, (lo, hi), full = build_shard(ctx, wl, args.shard_rank if args.shard1 else rank, cut)
     else:
         ctx = hgmres.Context(local)
         A, B, b, x_true = build_problem(ctx, wl, seed=rank)
@@ -443,7 +447,7 @@ def main():
                             f"tol=0, lambda={lam}, orth={args.orth}, "
                             f"residual={'explicit A*x' if args.explicit_residual else '(A*Q)*y'}",
                 "global_batch": 1 if shard else world,
-                "parallelism": (f"rank 0's shard of a {args.shard_of}-way pixel cut on a one-rank communicator "
+                "parallelism": (f"rank {args.shard_rank}'s shard of a {args.shard_of}-way pixel cut on a one-rank communicator "
                                 f"(per-rank kernel costs; not a global solve)" if args.shard1 and args.shard_of > 1 else
                                 f"pixel-sharded over {world} ranks ({args.comm} all-reduce of the m-vector)"
                                 if shard else

@@ -874,8 +874,11 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
             for (int p = 0; p < P; ++p) q[p] = buf_load2<T2>(rc, (ok[p] ? ix[p] : lim) * (int)sizeof(T2));
         };
-        // CU columns' loads in flight together (P * CU = 8 pairs a lane for short tiles)
-        constexpr int CU = P >= 4 ? 2 : 8 / P;
+        // CU columns' loads in flight together (P * CU = HGM_MGS1_LD pairs a lane)
+#ifndef HGM_MGS1_LD
+#define HGM_MGS1_LD 8
+#endif
+        constexpr int CU = HGM_MGS1_LD / P >= 2 ? HGM_MGS1_LD / P : 2;
         int c = 0;
 #pragma unroll 1
         for (; c + CU <= kk + 1; c += CU) {

@@ -26,7 +26,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-TAG=${TAG:-r5}
+TAG=${TAG:-r6}
 O=gpurun_out/$TAG
 mkdir -p "$O"
 recipe=$1
@@ -56,10 +56,12 @@ case "$recipe" in
     # gram_err_min=0: the error monitor keeps the Gram form on every iteration, as the global
     # solve does (the shard's own problem would otherwise fall back to the explicit x-forming
     # reconstruction, which runs on the step stream on a communicator)
+    # (SHARD_RANK: which rank's shard; rank 0's shard of the 8-way cut is all background, x_true = 0,
+    # so its own error monitor cannot take the Gram form; the global solve's does)
     for nn in ${@:-2 4 8}; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/shard_of$nn" -o trace \
-          -- python3 bench.py --workload c4 --shard1 --shard-of $nn --steps 5 --warmup 1 --no-cpu-baseline \
-             --opt gram_err_min=0 \
+          -- python3 bench.py --workload c4 --shard1 --shard-of $nn --shard-rank $(( ${SHARD_RANK:-0} % nn )) \
+             --steps 5 --warmup 1 --no-cpu-baseline --opt gram_err_min=0 \
           > "$O/shard_of$nn.log" 2>&1 || { tail -20 "$O/shard_of$nn.log"; exit 1; }
       bench_line "$O/shard_of$nn.log" > "$O/${TAG}_bench_c4_shard_of$nn.json"
       cp "$(find "$O/shard_of$nn" -name '*kernel_stats.csv' | head -1)" "$O/${TAG}_c4_shard_of${nn}_kernel_stats.csv"

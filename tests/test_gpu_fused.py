@@ -653,3 +653,28 @@ def test_lsmr_fused_step_monitor_is_bitwise(gpu_ctx):
             outs[f] = hgmres.lsmr_solver(A, b, xt, 0.0, 10, ctx=gpu_ctx, At=At)
     for a_, b_ in zip(outs[0], outs[1]):
         assert np.array_equal(np.asarray(a_), np.asarray(b_))
+
+
+@pytest.mark.parametrize("maxit", [20, 100, 200])
+def test_lsqr_res_img_fp32_long_runs(gpu_ctx, maxit):
+    """HGM_OPT_LSQR_RES_IMG (on by default) replaces lsqr_solver.m:52's exact final
+    residual norm(b - A*x) by the norm of b minus a double-precision image of A*x kept alongside
+    the fp32 x.  Held at the bench's 20 iterations and far past them (100, 200) on the fp32
+    one-pass path: the image's value against the true residual of the RETURNED x (b - A*x in
+    float64 over the fp32 operator's values, on the host) within 1e-4 relative, and no worse than
+    1.5 x the explicit fp32 evaluation (lsqr_res_img = 0: one fp32 SpMV of x, whose own rounding
+    in the cancellation b - A*x is ~ eps32 ||b|| / ||r||).  The iterates are the same bits
+    either way."""
+    A, At, b, xt = _gkb_pair(gpu_ctx, 512, 47, dtype="f32")
+    with gpu_ctx.options(fused_ab=1, lsqr_res_img=1):
+        xi, ei, ri, ki = hgmres.lsqr_solver(A, b, xt, 0.0, maxit, ctx=gpu_ctx, At=At)
+        assert gpu_ctx.solve_path()["one_pass"] == 1
+    with gpu_ctx.options(fused_ab=1, lsqr_res_img=0):
+        xe, ee, re, ke = hgmres.lsqr_solver(A, b, xt, 0.0, maxit, ctx=gpu_ctx, At=At)
+    assert np.array_equal(xi, xe) and np.array_equal(ri[:-1], re[:-1]) and np.array_equal(ei, ee)
+    As = A.to_scipy()                                   # fp32 values, held in float64
+    true = float(np.linalg.norm(b - As @ xi) / np.linalg.norm(b))
+    d_img, d_exp = abs(ri[-1] - true) / true, abs(re[-1] - true) / true
+    print(f"[lsqr res img fp32 k={maxit}] true {true:.9e}: image {ri[-1]:.9e} (dev {d_img:.1e}), "
+          f"explicit fp32 {re[-1]:.9e} (dev {d_exp:.1e})")
+    assert d_img <= 1e-4 and d_img <= max(1.5 * d_exp, 1e-6), (d_img, d_exp)
