@@ -10,6 +10,7 @@ usage: _shard_worker.py RANK WORLD PORT OUTDIR [c4]
 """
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -38,6 +39,7 @@ class Hub:
             for _ in range(world - 1):
                 c = lst.accept()
                 self.conns[int(c.recv())] = c
+            print(f"[hub] rank 0 connected to {sorted(self.conns)}", flush=True)
             lst.close()
         else:
             c = None
@@ -78,6 +80,13 @@ class Hub:
 
 def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    # a stuck rank reports where it is (every 60 s) and exits after 10 minutes instead of hanging
+    # the test run: the parent kills the others and fails the test
+    import faulthandler
+    faulthandler.dump_traceback_later(60, repeat=True)
+    watchdog = threading.Timer(600.0, lambda: os._exit(3))
+    watchdog.daemon = True
+    watchdog.start()
     ctx = hgmres.Context(0)
     hub = Hub(rank, world, port)
     if world > 1:
@@ -219,6 +228,7 @@ def solve_c4(ctx, rank, world, hub):
     for wl, tag in (("c4", "abn"), ("c5", "f32")):
         for turn in range(world):
             if turn == rank:
+                print(f"[rank {rank}/{world}] {wl} shard: building", flush=True)
                 t0 = time.time()
                 A_g, B_g, _, xs, (lo, hi), full = bench.build_shard(ctx, bench.WORKLOADS[wl], rank, world)
                 ctx.synchronize()

@@ -1,13 +1,15 @@
-"""Multi-rank path on the CPU (no GPU): the pixel-sharded decomposition of DESIGN.md §5,
-exercised with world_size 2 over torch.distributed gloo.
+"""Multi-rank DECOMPOSITION on the CPU (no GPU), world_size 2 over torch.distributed gloo.
 
+What this checks is the arithmetic of the pixel sharding of DESIGN.md §5, re-derived in numpy:
+it does NOT call libhgmres (no GPU here; the library's own multi-rank code runs on the GPU box
+in tests/test_gpu_parity.py::test_shard_emulation_two_ranks and, at full size as 2, 4 and 8 ranks,
+tests/test_gpu_fullsize.py::test_c4_c5_sharded_vs_oracle).
 * the shard plan and the shard operators (hgmres.dist) are exact slices whose partial
   products sum to the full ones;
-* a sharded BA-RTP GMRES written with the library's exchange pattern (one all-reduce of the
-  m-vector partial A_g q_g per operator application, one scalar all-reduce per MGS inner
+* a sharded BA-RTP GMRES written in numpy with the library's exchange pattern (one all-reduce of
+  the m-vector partial A_g q_g per operator application, one scalar all-reduce per MGS inner
   product, nothing else) reproduces the single-process oracle (oracle/restatement.py,
-  hybrid_ba_gmres_rtp.m) to 1e-10 — the decomposition the C++ path implements (its own
-  two-process run is tests/test_gpu_parity.py::test_shard_emulation_two_ranks).
+  hybrid_ba_gmres_rtp.m) to 1e-10.
 """
 import os
 import socket
