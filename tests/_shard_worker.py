@@ -80,11 +80,11 @@ class Hub:
 
 def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
-    # a stuck rank reports where it is (every 60 s) and exits after 10 minutes instead of hanging
-    # the test run: the parent kills the others and fails the test
+    # a stuck rank reports where it is (every 60 s) and exits after 5 minutes instead of hanging
+    # the test run (a world-8 C4/C5 run takes ~1 minute): the parent kills the others and fails
     import faulthandler
     faulthandler.dump_traceback_later(60, repeat=True)
-    watchdog = threading.Timer(600.0, lambda: os._exit(3))
+    watchdog = threading.Timer(300.0, lambda: os._exit(3))
     watchdog.daemon = True
     watchdog.start()
     ctx = hgmres.Context(0)

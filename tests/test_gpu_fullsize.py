@@ -291,7 +291,7 @@ def _run_ranks(tmp_path, world, mode):
     procs = [subprocess.Popen([sys.executable, "-u", worker, str(r), str(world), str(port), str(tmp_path), mode])
              for r in range(world)]
     try:
-        rcs = [p.wait(timeout=900) for p in procs]
+        rcs = [p.wait(timeout=420) for p in procs]
     finally:
         for p in procs:
             if p.poll() is None:
