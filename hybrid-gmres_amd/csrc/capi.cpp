@@ -688,6 +688,29 @@ HGM_API int hgm_ctx_rank(const hgm_ctx* c, int* rank, int* world) {
     return HGM_OK;
 }
 
+HGM_API int hgm_ctx_release_workspace(hgm_ctx* c, int64_t* bytes_freed) {
+    if (!c) return HGM_E_ARG;
+    HGM_TRY(c, {
+        HGM_HIP(hipSetDevice(c->device));
+        HGM_HIP(hipStreamSynchronize(c->stream));
+        if (c->aux) HGM_HIP(hipStreamSynchronize(c->aux));
+        int64_t b = 0;
+        for (auto& kv : c->ws) b += (int64_t)kv.second.bytes;
+        c->ws.clear();   // DevBuf destructors free the device memory
+        if (bytes_freed) *bytes_freed = b;
+    });
+    return HGM_OK;
+}
+
+HGM_API int hgm_mem_info(hgm_ctx* c, int64_t* free_bytes, int64_t* total_bytes) {
+    if (!c) return HGM_E_ARG;
+    size_t f = 0, t = 0;
+    if (hipSetDevice(c->device) != hipSuccess || hipMemGetInfo(&f, &t) != hipSuccess) return HGM_E_HIP;
+    if (free_bytes) *free_bytes = (int64_t)f;
+    if (total_bytes) *total_bytes = (int64_t)t;
+    return HGM_OK;
+}
+
 HGM_API int hgm_ctx_solve_path(const hgm_ctx* c, int what, int* out, int cap, int* n) {
     if (!c || (what != 0 && what != 1) || cap < 0 || (cap > 0 && !out)) return HGM_E_ARG;
     std::vector<int> v;

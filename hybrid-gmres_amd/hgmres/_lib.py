@@ -64,6 +64,8 @@ _SIGS = {
     "hgm_ctx_stream": (c_void_p, [c_void_p]),
     "hgm_ctx_rank": (c_int, [c_void_p, P(c_int), P(c_int)]),
     "hgm_experiments": (c_int, []),
+    "hgm_ctx_release_workspace": (c_int, [c_void_p, P(c_int64)]),
+    "hgm_mem_info": (c_int, [c_void_p, P(c_int64), P(c_int64)]),
     "hgm_ctx_solve_path": (c_int, [c_void_p, c_int, P(c_int), c_int, P(c_int)]),
     "hgm_mat_create_csr": (c_int, [c_void_p, c_int64, c_int64, c_int64, ip64, ip32, dp, c_int, P(c_void_p)]),
     "hgm_mat_create_csc": (c_int, [c_void_p, c_int64, c_int64, c_int64, ip64, ip64, dp, c_int, P(c_void_p)]),

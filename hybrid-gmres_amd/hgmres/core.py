@@ -88,6 +88,18 @@ class Context:
         _check(L.load().hgm_ctx_rank(self._h, C.byref(r), C.byref(w)), self)
         return r.value, w.value
 
+    def release_workspace(self):
+        """Free this context's device workspace (hgm_ctx_release_workspace); returns the bytes freed."""
+        b = C.c_int64()
+        _check(L.load().hgm_ctx_release_workspace(self._h, C.byref(b)), self)
+        return b.value
+
+    def mem_info(self):
+        """(free, total) bytes of device memory on this context's GPU (all processes)."""
+        f, t = C.c_int64(), C.c_int64()
+        _check(L.load().hgm_mem_info(self._h, C.byref(f), C.byref(t)), self)
+        return f.value, t.value
+
     def solve_path(self):
         """Path decisions of the last solve on this context (``hgm_ctx_solve_path``):
         ``{"gram_monitor": [0/1 per GMRES iteration], "one_pass": 0/1 or None}``."""

@@ -205,6 +205,12 @@ HGM_API const char* hgm_last_error(const hgm_ctx* ctx);
 HGM_API int hgm_ctx_synchronize(hgm_ctx* ctx);
 HGM_API void* hgm_ctx_stream(hgm_ctx* ctx);
 HGM_API int hgm_ctx_rank(const hgm_ctx* ctx, int* rank, int* world);
+/* Free the context's device workspace (the scratch and Krylov buffers its solves grow and keep for
+ * reuse; operators are untouched), after the context's streams are idle; *bytes_freed (optional).
+ * The next solve allocates again.  For long-lived contexts that share one GPU with other work. */
+HGM_API int hgm_ctx_release_workspace(hgm_ctx* ctx, int64_t* bytes_freed);
+/* Free and total device memory of the context's GPU (hipMemGetInfo: device-wide, all processes). */
+HGM_API int hgm_mem_info(hgm_ctx* ctx, int64_t* free_bytes, int64_t* total_bytes);
 /* Path decisions of the context's last solve (test hook: on a communicator every rank must issue
  * the same collective sequence, so these must agree across the ranks).  what = 0: one entry per
  * iteration of the last GMRES-family solve, 1 when that iteration's error monitor came from the

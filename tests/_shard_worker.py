@@ -228,7 +228,9 @@ def solve_c4(ctx, rank, world, hub):
     for wl, tag in (("c4", "abn"), ("c5", "f32")):
         for turn in range(world):
             if turn == rank:
-                print(f"[rank {rank}/{world}] {wl} shard: building", flush=True)
+                fr, tot = ctx.mem_info()
+                print(f"[rank {rank}/{world}] {wl} shard: building ({fr / 2**30:.0f} of {tot / 2**30:.0f} GiB free)",
+                      flush=True)
                 t0 = time.time()
                 A_g, B_g, _, xs, (lo, hi), full = bench.build_shard(ctx, bench.WORKLOADS[wl], rank, world)
                 ctx.synchronize()

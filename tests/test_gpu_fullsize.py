@@ -324,7 +324,7 @@ def _c5_envelope_check(label, hists, x_s, g, tag, nh):
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_c4_c5_sharded_vs_oracle(tmp_path, world):
+def test_c4_c5_sharded_vs_oracle(tmp_path, world, gpu_ctx):
     """configs[3] and configs[4] as the N-GPU bench runs them (bench.py --gpus N), at full size:
     `world` pixel shards cut as bench.py build_shard cuts them (whole tile columns of the 4 x 4-
     tiled stored order, 64-column bands, the one pass A_g*(B_g*q) per shard with its own plan, one
@@ -341,6 +341,13 @@ def test_c4_c5_sharded_vs_oracle(tmp_path, world):
       iterations, every history entry and x within 100 x the fp32 oracle's own spread
       (tests/golden/c5_4096.npz); the one-pass plan agreed on every rank."""
     from hgmres.core import auto_pixel_order, stored_pixel_index
+    # the ranks share this GPU with the test process: hand back the session context's workspace
+    # first (the earlier full-size solves grew it), so the ranks' operator builds never push HBM
+    # into eviction (a build that must evict other processes' buffers crawls: 70 s instead of 3)
+    freed = gpu_ctx.release_workspace()
+    fr, tot = gpu_ctx.mem_info()
+    print(f"[c4 sharded {world} ranks] released {freed / 2**30:.1f} GiB of workspace; {fr / 2**30:.0f} of "
+          f"{tot / 2**30:.0f} GiB free before the ranks start")
     o = _run_ranks(tmp_path, world, "c4")
     g = load_golden("c4_4096.npz")
     st = int(g["sample_stride"])
