@@ -36,6 +36,7 @@ class Hub:
             return
         if rank == 0:
             lst = Listener(("127.0.0.1", port), authkey=b"hgm", backlog=world)
+            lst._listener._socket.settimeout(240.0)      # (a rank that never starts fails the test)
             for _ in range(world - 1):
                 c = lst.accept()
                 self.conns[int(c.recv())] = c
@@ -59,7 +60,7 @@ class Hub:
         if self.rank == 0:
             s = np.array(arr, dtype=arr.dtype, copy=True)
             for r in range(1, self.world):
-                other = self.conns[r].recv()
+                other = self._recv(r)
                 if other.shape != s.shape:    # a collective-sequence mismatch between ranks: fail loudly
                     raise RuntimeError(f"rank {r} sent {other.shape} while rank 0 reduces {s.shape}")
                 s = s + other
@@ -68,7 +69,13 @@ class Hub:
             arr[:] = s
         else:
             self.conns[0].send(np.array(arr, copy=True))
-            arr[:] = self.conns[0].recv()
+            arr[:] = self._recv(0)
+
+    def _recv(self, r, timeout=240.0):
+        # (a rank that died or stalls fails the collective instead of blocking the others forever)
+        if not self.conns[r].poll(timeout):
+            raise TimeoutError(f"rank {self.rank}: nothing from rank {r} for {timeout:.0f} s")
+        return self.conns[r].recv()
 
     def barrier(self):
         self.allreduce(np.zeros(1))
@@ -76,6 +83,20 @@ class Hub:
     def close(self):
         for c in self.conns.values():
             c.close()
+
+
+def run_rank(rank, world, port, out, mode):
+    """One rank: its own context on device 0, the hub, the solves, rank{r}_of{world}.npz."""
+    ctx = hgmres.Context(0)
+    hub = Hub(rank, world, port)
+    try:
+        if world > 1:
+            ctx.set_host_allreduce(rank, world, hub.allreduce)
+        res = solve_c4(ctx, rank, world, hub) if mode == "c4" else solve_all(ctx, rank, world)
+        np.savez(os.path.join(out, f"rank{rank}_of{world}.npz"), **res)
+    finally:
+        hub.close()
+        ctx.close()
 
 
 def main():
@@ -87,17 +108,7 @@ def main():
     watchdog = threading.Timer(300.0, lambda: os._exit(3))
     watchdog.daemon = True
     watchdog.start()
-    ctx = hgmres.Context(0)
-    hub = Hub(rank, world, port)
-    if world > 1:
-        ctx.set_host_allreduce(rank, world, hub.allreduce)
-    if len(sys.argv) > 5 and sys.argv[5] == "c4":
-        res = solve_c4(ctx, rank, world, hub)
-    else:
-        res = solve_all(ctx, rank, world)
-    np.savez(os.path.join(out, f"rank{rank}_of{world}.npz"), **res)
-    hub.close()
-    ctx.close()
+    run_rank(rank, world, port, out, sys.argv[5] if len(sys.argv) > 5 else "all")
 
 
 def _abn_device(ctx, A_g, B_g, b, xt, maxit):
