@@ -255,7 +255,16 @@ def main():
         else:
             ctx = init_context(local, rank, world, one_rank_comm=args.shard1)
         cut = args.shard_of if args.shard1 else world
-        A, B, b, x_true, (lo, hi), full = build_shard(ctx, wl, args.shard_rank if args.shard1 else rank, cut)
+        if args.same_device and world > 1:
+            # shard emulation on one GPU: the ranks build one after the other (each build holds the
+            # full operator, its transpose and the sort scratch for a moment: ~50 GB at C4)
+            for turn in range(world):
+                if turn == rank:
+                    A, B, b, x_true, (lo, hi), full = build_shard(ctx, wl, rank, cut)
+                    torch.cuda.synchronize()
+                dist.barrier()
+        else:
+            A, B, b, x_true, (lo, hi), full = build_shard(ctx, wl, args.shard_rank if args.shard1 else rank, cut)
     else:
         ctx = hgmres.Context(local)
         A, B, b, x_true = build_problem(ctx, wl, seed=rank)
