@@ -124,3 +124,26 @@ def test_ctx_option_api_without_gpu():
     txt = open(os.path.join(ROOT, "include", "hgmres.h")).read()
     for name, val in L.OPTIONS.items():   # the Python names mirror the header's enum
         assert re.search(rf"HGM_OPT_{name.upper()}\s*=\s*{val}\b", txt), name
+
+
+def test_default_build_is_not_the_experiments_build():
+    """the default library carries the production one-pass kernels only; the
+    measured variants live in an experiments build (hgm_experiments() == 1, make
+    EXTRA=-DHGM_EXPERIMENTS=1).  The header marks their option values [experiments]."""
+    lib = hgmres.load_library()
+    if os.environ.get("HGM_LIB"):
+        pytest.skip("HGM_LIB selects another build")
+    assert lib.hgm_experiments() == 0
+    txt = open(os.path.join(ROOT, "include", "hgmres.h")).read()
+    for opt in ("HGM_OPT_FUSED_DBG", "HGM_OPT_FUSED_KIND", "HGM_OPT_FUSED_WAVES", "HGM_OPT_FUSED_ACC32"):
+        line = [l for l in txt.splitlines() if opt + " =" in l][0]
+        assert "[experiments]" in line, opt
+
+
+def test_new_ctx_calls_reject_null_without_gpu():
+    """hgm_ctx_solve_path / hgm_ctx_release_workspace / hgm_mem_info on a NULL context: HGM_E_ARG."""
+    lib = hgmres.load_library()
+    n = ctypes.c_int()
+    assert lib.hgm_ctx_solve_path(None, 0, None, 0, ctypes.byref(n)) == L.HGM_E_ARG
+    assert lib.hgm_ctx_release_workspace(None, None) == L.HGM_E_ARG
+    assert lib.hgm_mem_info(None, None, None) == L.HGM_E_ARG
