@@ -382,9 +382,22 @@ template <typename T> void lsqr_update(hgm_ctx* c, int64_t n, T* x, T* w, const 
 // (beta^2) and *ssa (alpha^2) in one thread (st = [rho_bar, phi_bar, stop]); the step
 // v /= alpha, x += coef0 w, w = v - coef1 w (skipped after the stop), with ||x - x_true||^2 fused
 // into err_out when xt != NULL; out = in / sqrt(*ss).
+// Scalars that rode an m-vector all-reduce (multi-GPU Golub-Kahan solves: the previous iteration's
+// ||x - x_true||^2 and ||A'r||^2 partials summed as trailing elements of [A*v_hat | alpha^2]),
+// copied to their history slots by the rotation kernel that runs right after that all-reduce.
+template <typename T>
+struct ScalarCopy {
+    const T* src = nullptr;
+    T* dst = nullptr;
+    const double* dsrc = nullptr;
+    double* ddst = nullptr;
+};
 template <typename T>
 void lsqr_rot(hgm_ctx* c, const T* ssb, const T* ssa, double* st, T* coef, double* phib_hist, int k, double nb,
-              double tol);
+              double tol, const ScalarCopy<T>& cp = ScalarCopy<T>{});
+// the copies of cp alone (one thread), on the context stream
+template <typename T>
+void copy_scalars(hgm_ctx* c, const ScalarCopy<T>& cp);
 template <typename T>
 void lsqr_step(hgm_ctx* c, int64_t n, T* x, T* w, T* v, const T* ssa, const T* coef, const double* st, int k,
                const T* xt, T* err_out);
@@ -418,7 +431,8 @@ void lsmr_monitor_r(hgm_ctx* c, int64_t n, const T* p1, const T* p0, T* Ih, T* I
 // into err_out when xt != NULL; the stop test :76 on the m-space monitor; out = in / sqrt(*ss)
 // unless the sum is zero.
 template <typename T>
-void lsmr_rot(hgm_ctx* c, const T* ssb, const T* ssa, double* st, T* coef, double* cfm, double* cfn);
+void lsmr_rot(hgm_ctx* c, const T* ssb, const T* ssa, double* st, T* coef, double* cfm, double* cfn,
+              const ScalarCopy<T>& cp = ScalarCopy<T>{});
 template <typename T>
 void lsmr_step(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, T* v, const T* ssa, const T* coef, const double* st,
                int k, const T* xt, T* err_out);

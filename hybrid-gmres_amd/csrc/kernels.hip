@@ -1493,9 +1493,27 @@ template <typename T> void lsqr_update(hgm_ctx* c, int64_t n, T* x, T* w, const 
 // st: [rho_bar, phi_bar, stop] (stop = iteration+1 of the first res <= tol, 0 while running).
 // ------------------------------------------------------------------------------
 template <typename T>
+__device__ __forceinline__ void scalar_copies(const ScalarCopy<T>& cp) {
+    if (cp.dst) *cp.dst = *cp.src;
+    if (cp.ddst) *cp.ddst = *cp.dsrc;
+}
+template <typename T>
+__global__ void k_copy_scalars(ScalarCopy<T> cp) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) scalar_copies(cp);
+}
+template <typename T>
+void copy_scalars(hgm_ctx* c, const ScalarCopy<T>& cp) {
+    k_copy_scalars<T><<<1, 64, 0, c->stream>>>(cp);
+    HGM_HIP(hipGetLastError());
+}
+template void copy_scalars<double>(hgm_ctx*, const ScalarCopy<double>&);
+template void copy_scalars<float>(hgm_ctx*, const ScalarCopy<float>&);
+
+template <typename T>
 __global__ void k_lsqr_rot(const T* ssb, const T* ssa, double* st, T* coef, double* phib_hist, int k, double nb,
-                           double tol) {
+                           double tol, ScalarCopy<T> cp) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    scalar_copies(cp);
     const double beta = sqrt((double)*ssb);                  // :23
     const double alpha = sqrt((double)*ssa);                 // :27
     const double rho_bar = st[0], phi_bar = st[1];
@@ -1567,8 +1585,8 @@ __global__ __launch_bounds__(BS) void k_div_sqrt(int64_t n, const T* __restrict_
 
 template <typename T>
 void lsqr_rot(hgm_ctx* c, const T* ssb, const T* ssa, double* st, T* coef, double* phib_hist, int k, double nb,
-              double tol) {
-    k_lsqr_rot<T><<<1, 64, 0, c->stream>>>(ssb, ssa, st, coef, phib_hist, k, nb, tol);
+              double tol, const ScalarCopy<T>& cp) {
+    k_lsqr_rot<T><<<1, 64, 0, c->stream>>>(ssb, ssa, st, coef, phib_hist, k, nb, tol, cp);
     HGM_HIP(hipGetLastError());
 }
 
@@ -1709,8 +1727,10 @@ void lsmr_update(hgm_ctx* c, int64_t n, T* x, T* h, T* hbar, const T* v, T c_hba
 // n-space update; cfm / cfn = the monitors' coefficients [c1, c0, f, e, cx] (m-space: image of
 // v = A*v_k; n-space: beta A'u_{k+1} + alpha_k A'u_k).
 template <typename T>
-__global__ void k_lsmr_rot(const T* ssb, const T* ssa, double* st, T* coef, double* cfm, double* cfn) {
+__global__ void k_lsmr_rot(const T* ssb, const T* ssa, double* st, T* coef, double* cfm, double* cfn,
+                           ScalarCopy<T> cp) {
     if (threadIdx.x != 0) return;
+    scalar_copies(cp);
     const double alpha_k = st[0];
     const double beta = sqrt((double)*ssb), alpha = sqrt((double)*ssa);   // :35, :39
     const double alphahat = st[1];                                        // :42
@@ -1815,8 +1835,9 @@ __global__ __launch_bounds__(BS) void k_div_sqrt_nz(int64_t n, const T* __restri
 }
 
 template <typename T>
-void lsmr_rot(hgm_ctx* c, const T* ssb, const T* ssa, double* st, T* coef, double* cfm, double* cfn) {
-    k_lsmr_rot<T><<<1, 64, 0, c->stream>>>(ssb, ssa, st, coef, cfm, cfn);
+void lsmr_rot(hgm_ctx* c, const T* ssb, const T* ssa, double* st, T* coef, double* cfm, double* cfn,
+              const ScalarCopy<T>& cp) {
+    k_lsmr_rot<T><<<1, 64, 0, c->stream>>>(ssb, ssa, st, coef, cfm, cfn, cp);
     HGM_HIP(hipGetLastError());
 }
 
@@ -2166,13 +2187,15 @@ template <typename T> void convert_back(hgm_ctx* c, int64_t n, const T* in, doub
     template void gemv<T>(hgm_ctx*, int64_t, int, const T*, int64_t, const T*, T*, int);       \
     template void div_scalar<T>(hgm_ctx*, int64_t, const T*, T*, T);                           \
     template void lsqr_update<T>(hgm_ctx*, int64_t, T*, T*, const T*, T, T);                   \
-    template void lsqr_rot<T>(hgm_ctx*, const T*, const T*, double*, T*, double*, int, double, double); \
+    template void lsqr_rot<T>(hgm_ctx*, const T*, const T*, double*, T*, double*, int, double, double,   \
+                              const ScalarCopy<T>&);                                            \
     template void lsqr_step<T>(hgm_ctx*, int64_t, T*, T*, T*, const T*, const T*, const double*, int, const T*, T*); \
     template void div_sqrt<T>(hgm_ctx*, int64_t, const T*, T*, const T*);                     \
     template void lsmr_update<T>(hgm_ctx*, int64_t, T*, T*, T*, const T*, T, T, T, bool);      \
     template void lsmr_monitor<T>(hgm_ctx*, int64_t, const T*, const T*, double, double, double*, double*, \
                                   double*, const T*, double, double, double, bool, double*, const double*); \
-    template void lsmr_rot<T>(hgm_ctx*, const T*, const T*, double*, T*, double*, double*);   \
+    template void lsmr_rot<T>(hgm_ctx*, const T*, const T*, double*, T*, double*, double*,         \
+                              const ScalarCopy<T>&);                                            \
     template void lsmr_monitor_r<T>(hgm_ctx*, int64_t, const T*, const T*, T*, T*, T*, bool, double*, \
                                     const double*);                                            \
     template void lsmr_step<T>(hgm_ctx*, int64_t, T*, T*, T*, T*, const T*, const T*, const double*, int, \

@@ -859,7 +859,7 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     // A*v_{k+1} (:22) is (A*v_hat) / alpha: an m-vector operation instead of a second pass.
     // wm = [A*v_hat | alpha^2] (m + 1: alpha^2 rides the m-vector all-reduce on a communicator).
     const FusedPlan* fp = agreed_gk_plan<T>(c, A, At, !hybrid && !parity);
-    T* wm = fp ? c->buf<T>("gkb_wm", m + 2) : nullptr;
+    T* wm = fp ? c->buf<T>("gkb_wm", m + 3) : nullptr;        // (+ the partials riding the all-reduce)
     // beta = norm(b) (lsqr_solver.m:7; hybrid: norm([b;0]) = norm(b), hybrid_lsqr_solver.m:9)
     double beta = nb;
     div_scalar<T>(c, m, b, u, (T)beta);                                        // :8  u = b / beta
@@ -917,6 +917,15 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         const bool host_sc = !c->num.lsqr_dev;
         const int batch = tol > 0 && !host_sc ? 8 : maxit;
         int stop = 0;
+        // On a communicator the error partial ||x - x_true||^2 (:43, summed over the pixel shards)
+        // rides the NEXT iteration's m-vector all-reduce as element m+1, and the rotation kernel after
+        // that all-reduce copies the sum into the history: one collective per iteration instead of
+        // two (the stop test uses phi_bar, replicated).  The last iteration's partial is summed after
+        // the loop.
+        const bool ride = dist_n(c) && !host_sc;
+        T* ride_e = ride ? wm + m + 1 : nullptr;
+        if (ride) HGM_HIP(hipMemsetAsync(ride_e, 0, sizeof(T), c->stream));
+        int last = -1;
         // the final residual (:52) from A*x kept alongside x (A*v_k is the pass's A*v_hat / alpha):
         // no SpMV after the loop (HGM_OPT_LSQR_RES_IMG)
         if (c->num.lsqr_res_img) {
@@ -930,7 +939,7 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
                 gkb_mstep<T>(c, m, wm, wm + m, u, t, nullptr, sl + S_BETA);          // :22-23 A*v - alpha*u
                 div_sqrt<T>(c, m, t, u, sl + S_BETA);                                // :24
                 fused_pass<T>(c, At, fp, fa);                                        // :26-27 (+ A*v_hat)
-                if (dist_n(c)) allreduce(c, wm, m + 1);
+                if (dist_n(c)) allreduce(c, wm, (ride && k > 0) ? m + 2 : m + 1);
                 if (host_sc) {
                     T ss[2] = {T(0), T(0)};
                     Reader rr(c);
@@ -950,11 +959,17 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
                     res[k] = std::fabs(phi_bar) / nb;                                // :44
                     if (res[k] <= tol) stop = k + 1;                                 // :46 (<=)
                 } else {
-                    lsqr_rot<T>(c, sl + S_BETA, wm + m, st, coef, phib, k, nb, tol); // :31-38, :44-46
+                    ScalarCopy<T> cp;
+                    if (ride && k > 0) {
+                        cp.src = ride_e;
+                        cp.dst = errh + k - 1;
+                    }
+                    lsqr_rot<T>(c, sl + S_BETA, wm + m, st, coef, phib, k, nb, tol, cp);   // :31-38, :44-46
                 }
-                lsqr_step<T>(c, n, x, w, v, wm + m, coef, st, k, xt, errh + k);     // :28, :40-41, :43
+                lsqr_step<T>(c, n, x, w, v, wm + m, coef, st, k, xt, ride ? ride_e : errh + k);   // :28, :40-41, :43
+                last = k;
                 if (img_ax) lsqr_img<T>(c, m, wm, wm + m, coef, st, k, img_ax, img_aw, false);
-                if (dist_n(c)) allreduce(c, errh + k, 1);
+                if (dist_n(c) && !ride) allreduce(c, errh + k, 1);
                 if (stop) {
                     ++k;
                     break;
@@ -966,6 +981,13 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
             rs.add(&sv, st + 2, sizeof(double));
             rs.go();
             stop = (int)sv;
+        }
+        if (ride && last >= 0) {                       // the last iteration's error partial
+            allreduce(c, ride_e, 1);
+            ScalarCopy<T> cp;
+            cp.src = ride_e;
+            cp.dst = errh + last;
+            copy_scalars<T>(c, cp);
         }
         k = stop > 0 ? stop - 1 : maxit;
         if (!host_sc) {
@@ -1192,7 +1214,7 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
     // One pass over the operator per iteration (as lsqr_t): the step :38-39 and
     // A*v_hat in one pass over At, A*v_{k+1} (:34, the kept A*v) = (A*v_hat) / alpha.
     const FusedPlan* fp = agreed_gk_plan<T>(c, A, At, !parity);
-    T* wm = fp ? c->buf<T>("gkb_wm", m + 2) : nullptr;                         // [A*v_hat | alpha^2]
+    T* wm = fp ? c->buf<T>("gkb_wm", m + 3) : nullptr;                         // [A*v_hat | alpha^2 | ridden]
     HGM_HIP(hipMemcpyAsync(u, b, sizeof(T) * m, hipMemcpyDeviceToDevice, c->stream));   // :10
     double beta = nb;                                                          // :11
     if (beta > 0) div_scalar<T>(c, m, u, u, (T)beta);                          // :12
@@ -1265,6 +1287,21 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         fa.side_out = wm + m;
         const int batch = tol > 0 ? 8 : maxit;
         int stop = 0;
+        // On a communicator the n-space partials of iteration k -- ||x - x_true||^2 (:72) and, in
+        // fp64, ||A'r||^2 (:71) -- ride iteration k+1's m-vector all-reduce as elements m+1, m+2, and
+        // the rotation kernel copies the sums into the histories: one collective per iteration
+        // instead of three (fp32: two; its ||A'r||^2 is a double sum that a float element cannot
+        // carry).  The stop test (:76) reads only the replicated m-space residual.  The last
+        // iteration's partials are summed after the loop.
+        constexpr bool ride_d_ok = std::is_same_v<T, double>;
+        const bool ride = dist_n(c);
+        T* ride_e = (ride && xt) ? wm + m + 1 : nullptr;
+        double* ride_d = nullptr;
+        if constexpr (ride_d_ok)
+            if (ride) ride_d = reinterpret_cast<double*>(wm + m + 2);
+        const int64_t ride_n = ride_d ? 2 : 1;       // trailing elements past alpha^2
+        if (ride) HGM_HIP(hipMemsetAsync(wm + m + 1, 0, sizeof(T) * ride_n, c->stream));
+        int last = -1;
         for (k = 0; k < maxit && stop == 0;) {
             const int kend = std::min(maxit, k + batch);
             for (; k < kend; ++k) {
@@ -1272,19 +1309,32 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
                 div_sqrt_nz<T>(c, m, r, u, sl + S_BETA);                          // :36
                 fa.zraw = Atu1;                                                   // A'*u_{k+1} (kept)
                 fused_pass<T>(c, At, fp, fa);                                     // :38-39 (+ A*v_hat)
-                if (dist_n(c)) allreduce(c, wm, m + 1);
-                lsmr_rot<T>(c, sl + S_BETA, wm + m, st, coef, cfm, cfn);          // :42-67 scalars
+                if (dist_n(c)) allreduce(c, wm, (ride && k > 0) ? m + 1 + ride_n : m + 1);
+                ScalarCopy<T> cp;
+                if (ride && k > 0) {
+                    if (ride_e) {
+                        cp.src = ride_e;
+                        cp.dst = errh + k - 1;
+                    }
+                    if (ride_d) {
+                        cp.dsrc = ride_d;
+                        cp.ddst = dmonh + 2 * (size_t)(k - 1) + 1;
+                    }
+                }
+                lsmr_rot<T>(c, sl + S_BETA, wm + m, st, coef, cfm, cfn, cp);      // :42-67 scalars
                 double* dm = dmonh + 2 * (size_t)k;
+                T* e_out = xt ? (ride_e ? ride_e : errh + k) : nullptr;
+                double* d_out = ride_d ? ride_d : dm + 1;
                 // (fp32: the n-space step and the n-space monitor in one launch when it applies)
-                const bool nmon = img_t && lsmr_step_mon<T>(c, n, x, h, hbar, v, wm + m, coef, st, k, xt,
-                                                            xt ? errh + k : nullptr, Atu1, Atu0, Ihn_t, Ihbn_t,
-                                                            Irn_t, k == 0, dm + 1, cfn);
-                if (!nmon) lsmr_step<T>(c, n, x, h, hbar, v, wm + m, coef, st, k, xt, xt ? errh + k : nullptr);   // :40, :61-67, :72
-                if (xt && dist_n(c)) allreduce(c, errh + k, 1);
+                const bool nmon = img_t && lsmr_step_mon<T>(c, n, x, h, hbar, v, wm + m, coef, st, k, xt, e_out,
+                                                            Atu1, Atu0, Ihn_t, Ihbn_t, Irn_t, k == 0, d_out, cfn);
+                if (!nmon) lsmr_step<T>(c, n, x, h, hbar, v, wm + m, coef, st, k, xt, e_out);   // :40, :61-67, :72
+                last = k;
+                if (xt && dist_n(c) && !ride_e) allreduce(c, errh + k, 1);
                 lsmr_monitor<T>(c, m, Av, nullptr, 0, 0, Ihm, Ihbm, Ixm, b, 0, 0, 0, k == 0, dm, cfm);
-                if (!nmon && img_t) lsmr_monitor_r<T>(c, n, Atu1, Atu0, Ihn_t, Ihbn_t, Irn_t, k == 0, dm + 1, cfn);
-                else if (!nmon) lsmr_monitor<T>(c, n, Atu1, Atu0, 0, 0, Ihn, Ihbn, Ixn, Atb, 0, 0, 0, k == 0, dm + 1, cfn);
-                if (dist_n(c)) allreduce(c, dm + 1, 1);
+                if (!nmon && img_t) lsmr_monitor_r<T>(c, n, Atu1, Atu0, Ihn_t, Ihbn_t, Irn_t, k == 0, d_out, cfn);
+                else if (!nmon) lsmr_monitor<T>(c, n, Atu1, Atu0, 0, 0, Ihn, Ihbn, Ixn, Atb, 0, 0, 0, k == 0, d_out, cfn);
+                if (dist_n(c) && !ride_d) allreduce(c, dm + 1, 1);
                 std::swap(Atu0, Atu1);
                 if (tol > 0) lsmr_stop(c, dm, nb, tol, st, k);                   // :76
             }
@@ -1295,6 +1345,19 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
                 rs.go();
                 stop = (int)sv;
             }
+        }
+        if (ride && last >= 0) {                       // the last iteration's ridden partials
+            allreduce(c, wm + m + 1, ride_n);
+            ScalarCopy<T> cp;
+            if (ride_e) {
+                cp.src = ride_e;
+                cp.dst = errh + last;
+            }
+            if (ride_d) {
+                cp.dsrc = ride_d;
+                cp.ddst = dmonh + 2 * (size_t)last + 1;
+            }
+            copy_scalars<T>(c, cp);
         }
         k = stop > 0 ? stop - 1 : maxit;
     }
