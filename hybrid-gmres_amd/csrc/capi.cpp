@@ -548,7 +548,10 @@ HGM_API int hgm_ctx_set_option(hgm_ctx* c, int option, double v) {
         case HGM_OPT_GRAM_ERR: if (!b01) return bad("gram err is 0 or 1"); n.gram_err = v != 0; break;
         case HGM_OPT_GRAM_ERR_MIN: if (!(v >= 0.0)) return bad("gram err min >= 0"); n.gram_err_min = v; break;
         case HGM_OPT_RING_POLL: if (!b01) return bad("ring poll is 0 or 1"); n.ring_poll = v != 0; break;
-        case HGM_OPT_PEND_NORM: if (!b01) return bad("pend norm is 0 or 1"); n.pend_norm = v != 0; break;
+        case HGM_OPT_PEND_NORM:
+            if (!(v == 0.0 || v == 1.0 || v == 2.0)) return bad("pend norm is 0, 1 or 2");
+            n.pend_norm = (int)v;
+            break;
         case HGM_OPT_RECON_SERIAL:
             if (v != -1.0 && !b01) return bad("recon serial is -1, 0 or 1");
             n.recon_serial = (int)v;

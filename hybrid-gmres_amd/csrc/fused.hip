@@ -362,10 +362,13 @@ __global__ __launch_bounds__(BS) void k_fused_reduce(int64_t m, const int64_t* _
         TP s = TP(0);
         const int64_t k0 = rs_ptr[i], k1 = rs_ptr[i + 1];
         int64_t k = k0 + gl;
-        if constexpr (RB >= 8) {
+        if constexpr (RB >= 2) {
             // a ray's partials in batches of RB per lane with the batch's tail clamped to the ray's
             // last slot (read again, not added): every slot read, then every partial read in flight
-            // (C4: ~14 partials per lane, one batch instead of three batches and a serial tail)
+            // (C4: ~14 partials per lane, one batch instead of three batches and a serial tail).  The
+            // lane adds its partials in slot order whatever RB is, so every RB gives the same bits;
+            // the host sizes RB to the partials per lane (fused_reduce_rb: a pixel shard's rays
+            // cross few of its regions)
             for (; k < k1; k += RB * RG) {
                 int32_t sl[RB];
                 TP p[RB];
@@ -589,6 +592,11 @@ __device__ __forceinline__ void lds_add(T* p, T t) {
 // Side sum (one value per region, in zx_part): side_sq == 0: sum_j zs_j * xt[j] (the m-space Gram
 // error monitor's x_true'(B*q)); side_sq == 1: sum_j zs_j^2 (alpha^2 of the Golub-Kahan step).
 // GK: the row epilogue / zout / side_sq code exists (false: the GMRES family's instruction stream).
+// pn (pending normalisation of q, the m-space AB-GMRES step; internal.h PendNorm, pn.np > 0): q still
+// holds the previous MGS sweep's unnormalised v; every wave re-reduces the sweep's norm partials
+// exactly as k_mgs_normalize does (stride BS, then block_sum_all: the same bits), h = sqrt(sum), and
+// stages q = v / h (v when h = 0, as k_mgs_normalize leaves it) into its LDS slots; workgroup 0
+// publishes h to pn.hdev and H(k+1,k) of the host ring (the MGS sweep that follows writes q back).
 // AM: how the accumulators are updated (AccT: their type; the partials are AccT too):
 //   0  ds_add of T: fp64 ds_add_f64 (the fp64 production form); fp32 ds_add_f32 measured 11.3 ms
 //      at C5 -- the no-return fp32 LDS add runs at a fraction of ds_add_f64's rate on gfx950
@@ -624,7 +632,8 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
                                                      const uint16_t* __restrict__ lidx, const T* __restrict__ q,
                                                      T* __restrict__ zraw, typename AccT<T, AM>::t* __restrict__ part,
                                                      const T* __restrict__ xt, T* __restrict__ zx_part,
-                                                     const T* ev, const T* __restrict__ easq, T* zout, int side_sq) {
+                                                     const T* ev, const T* __restrict__ easq, T* zout, int side_sq,
+                                                     PendNorm<T> pn) {
     static_assert(D >= 2 && D <= 4, "ring depth");
     static_assert(!RP || (PR && NCH == 1 && DBG == 0 && G % 2 == 0), "row pairs: pairs, one chunk");
     constexpr int NA = (RP == 1 || RP == 2) ? 2 : 1;   // private accumulator arrays per wave
@@ -640,25 +649,100 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
     const int ln = threadIdx.x & 63;
     const int64_t pb = reg_base[g];
     const int nr = (int)(reg_base[g + 1] - pb);
-    for (int k = threadIdx.x; k < nr; k += 64 * W) {
-        qloc[k] = q[ray_tab[pb + k]];
-#pragma unroll
-        for (int w = 0; w < W; ++w)
-#pragma unroll
-            for (int h = 0; h < NA; ++h) acc[w][h][k] = TA(0);
-    }
-    if (threadIdx.x < 64) qloc[MAXR - 64 + threadIdx.x] = T(0);
-    // the epilogue coefficient: the bits the host takes from the same sum of squares
-    const T ea = (GK && easq) ? (T)sqrt((double)*easq) : T(0);
+    // Staging: q at the region's rays into LDS, the accumulators zeroed.  All ray_tab loads, then all
+    // q gathers, are issued before any is used (NQ per thread), so the pending-normalisation sum
+    // below overlaps them.
+    // Pending normalisation (pn.np > 0): h = sqrt(sum of pn.parts) in reduce_parts' order for a
+    // BS-thread block (thread t sums parts t, t + BS, ...; wave sums; (s0 + s1) + (s2 + s3)), which
+    // every wave forms by itself for the BS / 64 virtual waves: the bits of k_mgs_normalize's h with
+    // no barrier and no LDS.
+    // the wave's runs (<= 64, the plan checks) in lanes: readlane in the loop, no loads there (a
+    // conditional load makes the compiler wait for every load in flight after it, and scalar loads'
+    // lgkmcnt waits would also wait on the LDS); a range-checked buffer load (zeros past the wave's
+    // runs) issued before the staging, so it is in flight with it (round 6)
     int ua = wrun[g * W + wv];
     const int ub = wrun[g * W + wv + 1];
-    __syncthreads();
+    const int2 runv = __builtin_bit_cast(
+        int2, __builtin_amdgcn_raw_buffer_load_b64(buf_rsrc(runs + ua, (ub - ua) * 8), ln * 8, 0, 0));
+    static_assert(BS == 256 && MAX_PARTS <= 4 * BS, "pending-normalisation sum: four virtual waves");
+    T hq = T(0);
+    auto pend_h = [&]() -> T {
+        // range-checked buffer loads (zeros past np; adding +0 to a sum of squares changes no bit),
+        // all 16 in flight before the sums
+        const __amdgpu_buffer_rsrc_t rpp = buf_rsrc(pn.parts, pn.np * (int)sizeof(T));
+        T pv[4][4];
+#pragma unroll
+        for (int vw = 0; vw < 4; ++vw)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pv[vw][j] = buf_load<T>(rpp, (64 * vw + ln + j * BS) * (int)sizeof(T));
+        T s[4];
+#pragma unroll
+        for (int vw = 0; vw < 4; ++vw) {
+            T a = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a += pv[vw][j];
+            s[vw] = wave_sum(a);
+        }
+        const T h = sqrt((s[0] + s[1]) + (s[2] + s[3]));
+        if (g == 0 && threadIdx.x == 0) {
+            pn.hdev[0] = h;
+            st_sys(pn.hring, h);
+        }
+        return h;
+    };
+    constexpr int NQ = (MAXR - 64 + 64 * W - 1) / (64 * W);   // staging iterations per thread
+    constexpr bool QREG = NQ <= 8;               // the staging loads go out at once (registers)
+    // branch-free: a range-checked buffer load returns ray 0 past nr (q[0] is read, not stored), so
+    // the NQ ray_tab loads and then the NQ gathers each go out with one wait; their stores into the
+    // LDS come after the first batches' row pointers are issued (below), so those are in flight
+    // with the gathers (round 6)
+    T qv[QREG ? NQ : 1];
+    if constexpr (QREG) {
+        const __amdgpu_buffer_rsrc_t rrt = buf_rsrc(ray_tab + pb, nr * 4);
+        int rt[NQ];
+#pragma unroll
+        for (int u = 0; u < NQ; ++u)
+            rt[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(rrt, (int)(threadIdx.x + u * 64 * W) * 4, 0, 0);
+#pragma unroll
+        for (int u = 0; u < NQ; ++u) qv[u] = q[rt[u]];
+    }
+    auto stage = [&]() {
+        if constexpr (QREG) {
+            if (pn.np > 0) hq = pend_h();
+            if (hq != T(0)) {                    // (uniform: no divisions without the pending norm)
+#pragma unroll
+                for (int u = 0; u < NQ; ++u) qv[u] = qv[u] / hq;
+            }
+#pragma unroll
+            for (int u = 0; u < NQ; ++u) {
+                const int k = threadIdx.x + u * 64 * W;
+                if (k < nr) {
+                    qloc[k] = qv[u];
+#pragma unroll
+                    for (int w = 0; w < W; ++w)
+#pragma unroll
+                        for (int h = 0; h < NA; ++h) acc[w][h][k] = TA(0);
+                }
+            }
+        } else {
+            if (pn.np > 0) hq = pend_h();
+            for (int k = threadIdx.x; k < nr; k += 64 * W) {
+                const T qq = q[ray_tab[pb + k]];
+                qloc[k] = hq != T(0) ? qq / hq : qq;
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+#pragma unroll
+                    for (int h = 0; h < NA; ++h) acc[w][h][k] = TA(0);
+            }
+        }
+        if (threadIdx.x < 64) qloc[MAXR - 64 + threadIdx.x] = T(0);
+    };
+    // the epilogue coefficient: the bits the host takes from the same sum of squares
+    const T ea = (GK && easq) ? (T)sqrt((double)*easq) : T(0);
+    // (the barrier that publishes the staging sits after the first batches' loads are issued, below:
+    // their row pointers and entries are in flight with the staging; round 6)
     TA* __restrict__ ac = &acc[wv][0][0];
     constexpr uint32_t POFF = (uint32_t)(MAXR * sizeof(TA));   // (RP) the second array, in bytes
-    // the wave's runs (<= 64, the plan checks) in lanes: readlane in the loop, no loads there
-    // (a conditional load makes the compiler wait for every load in flight after it, and scalar
-    // loads' lgkmcnt waits would also wait on the LDS)
-    const int2 runv = ua + ln < ub ? runs[ua + ln] : make_int2(0, 0);
     int u = ua, o = 0;
     auto next = [&](int& r0, int& cnt) {
         r0 = 0;
@@ -1038,8 +1122,10 @@ __global__ __launch_bounds__(64 * W) void k_fused_rw(const int64_t* __restrict__
         next(a[i], cn[i]);
         r[i] = load_rp(a[i], cn[i]);
     }
+    stage();                                      // (the gathers' waits leave the row pointers in flight)
 #pragma unroll
     for (int i = 0; i < D - 1; ++i) issue(b[i], a[i], cn[i], r[i]);
+    __syncthreads();                              // the staged q and the zeroed accumulators
     do {
 #pragma unroll
         for (int t = 0; t < D; ++t) {
@@ -1870,7 +1956,7 @@ static bool fused_rw_launch(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, co
                    dim3(64 * WV), (const int64_t*)P->reg_base, (const int32_t*)P->ray_tab, (const int32_t*)P->wrun, \
                    (const int2*)P->runs, (const int64_t*)B->rp, (const T*)B->val, (const uint16_t*)P->lidx, fa.q,  \
                    fa.zraw, (typename AccT<T, AMV>::t*)P->part, side ? fa.xt : nullptr,                            \
-                   side ? (T*)P->zx_part : nullptr, fa.ev, fa.easq, fa.zout, fa.side_sq ? 1 : 0);                  \
+                   side ? (T*)P->zx_part : nullptr, fa.ev, fa.easq, fa.zout, fa.side_sq ? 1 : 0, fa.pn);           \
         return true;                                                                                                  \
     }
     if (P->rowpair) {
@@ -2059,9 +2145,17 @@ bool fused_pass(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArg
 #undef HGM_RED
 #endif
     } else {
-        launch(c, true, k_fused_reduce<HGM_FUSED_RG, T>, dim3(rgrid), dim3(BS), P->m, (const int64_t*)P->rs_ptr,
-               (const int32_t*)P->rs_slot, (const T*)P->part, fa.w, (const T*)P->zx_part, (int)P->nreg,
-               side ? fa.side_out : nullptr);
+        // partials per lane: C4 ~14 (RB 16); rank g's shard of an 8-way cut ~1.8 (RB 4: the batch of
+        // 16 issued 8x the loads it adds; round 6)
+        const double ppl = (double)P->nslot / (double)std::max<int64_t>(1, P->m) / HGM_FUSED_RG;
+#define HGM_RED_RB(RBV)                                                                                         \
+    launch(c, true, k_fused_reduce<HGM_FUSED_RG, T, T, RBV>, dim3(rgrid), dim3(BS), P->m,                       \
+           (const int64_t*)P->rs_ptr, (const int32_t*)P->rs_slot, (const T*)P->part, fa.w, (const T*)P->zx_part, \
+           (int)P->nreg, side ? fa.side_out : nullptr)
+        if (ppl <= 4.0) HGM_RED_RB(4);
+        else if (ppl <= 8.0) HGM_RED_RB(8);
+        else HGM_RED_RB(16);
+#undef HGM_RED_RB
     }
     HGM_HIP(hipGetLastError());
     // algorithmic bytes of the fused pass: B's CSR once (values, 32-bit indices, row pointers),
@@ -2078,14 +2172,24 @@ template bool fused_pass<float>(hgm_ctx*, const hgm_mat*, const FusedPlan*, cons
 
 // Bq = B*q (n), ABq = A*(B*q) (m), one pass over B.
 bool fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq,
-              const double* xt, double* zx_out) {
+              const double* xt, double* zx_out, const PendNorm<double>* pn) {
     FusedArgs<double> fa;
     fa.q = q;
     fa.zraw = Bq;
     fa.w = ABq;
     fa.xt = xt;
     fa.side_out = zx_out;
+    if (pn && pn->np > 0) {
+        HGM_REQUIRE(fused_pend_ok(c, P) && pn->hdev && pn->hring && pn->np <= MAX_PARTS,
+                    "fused A*(B*q): pending normalisation needs the row-wave pass");
+        fa.pn = *pn;
+    }
     return fused_pass<double>(c, B, P, fa);
+}
+
+// (the row-wave pass; every wave re-forms reduce_parts' BS-thread order, whatever its waves)
+bool fused_pend_ok(const hgm_ctx* c, const FusedPlan* P) {
+    return P && P->kind == 1 && c->num.fused_dbg == 0;
 }
 
 }  // namespace hgm

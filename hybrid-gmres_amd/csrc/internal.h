@@ -77,7 +77,7 @@ struct Numerics {
     bool gram_err = true;           // Gram error monitor
     double gram_err_min = 0.01;
     bool ring_poll = true;
-    bool pend_norm = true;
+    int pend_norm = 1;              // 1: n-space (SpMV epilogues); 2: also m-space (the one pass)
     int recon_serial = -1;          // -1 automatic, 0 aux stream, 1 main stream
     int64_t recon_serial_n = int64_t(4) << 20;
     int pipe_depth = 2;
@@ -502,8 +502,12 @@ bool fused_ab_eligible(const hgm_ctx* c, const hgm_mat* A, const hgm_mat* B);
 const FusedPlan* fused_ab_plan(hgm_ctx* c, const hgm_mat* A, const hgm_mat* B);
 // With xt and zx_out (the row-wave kernel only; returns whether it did): also *zx_out =
 // x_true'(B*q), the m-space Gram error monitor's side dot, from the row sums as they form.
+// With pn (pn->np > 0, fused_pend_ok): q still holds the unnormalised v of the previous MGS sweep,
+// and the pass applies q = v / h itself (FusedArgs::pn).
 bool fused_ab(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const double* q, double* Bq, double* ABq,
-              const double* xt = nullptr, double* zx_out = nullptr);
+              const double* xt = nullptr, double* zx_out = nullptr, const PendNorm<double>* pn = nullptr);
+// whether the pass takes the pending normalisation of q for this plan (the row-wave kernel)
+bool fused_pend_ok(const hgm_ctx* c, const FusedPlan* P);
 // The general pass (T = double or float; fp32 and every epilogue: the row-wave kernel).  Over B's
 // rows j (pixels) and columns i (rays):
 //   z_j = B(j,:) q ; zs_j = z_j - a ev_j with a = (T)sqrt((double)*easq) (no ev: zs = z) ;
@@ -523,6 +527,9 @@ struct FusedArgs {
     T* zout = nullptr;
     bool side_sq = false;
     T* side_out = nullptr;
+    // pending normalisation of q (pn.np > 0: the row-wave pass, fused_pend_ok): q = v / h
+    // with h = sqrt(sum of pn.parts), published to pn.hdev and pn.hring (fused.hip k_fused_rw)
+    PendNorm<T> pn;
 };
 template <typename T>
 bool fused_pass(hgm_ctx* c, const hgm_mat* B, const FusedPlan* P, const FusedArgs<T>& fa);

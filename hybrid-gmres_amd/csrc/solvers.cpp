@@ -433,15 +433,23 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
     // (m-space: the Gram of Z = B*Q, from H and the strictly lower Q'Q in SQ)
     std::vector<double> GQ(gem ? (size_t)maxit * maxit : 0), cq(maxit, 0.0), gerr(maxit, -1.0);
     std::vector<double> SQ(gem_ab ? (size_t)maxit * maxit : 0);
-    // Pending normalisation (single GPU, n-space, one-reduction MGS): step k
-    // leaves v_{k+1} = Q(:,k+1) undivided and step k+1 applies q = v / H(k+1,k) where it reads
-    // it — A: (A*v)/h, which also publishes h = H(k+1,k); B: B*(A*q) + lambda*q; the MGS dots
-    // kernel writes q back over v — so the sweep needs no scale pass.  Step k's event is then
+    // Pending normalisation (one-reduction MGS): step k leaves v_{k+1} = Q(:,k+1)
+    // undivided and step k+1 applies q = v / H(k+1,k) where it reads it — n-space (single GPU):
+    // A: (A*v)/h, which also publishes h = H(k+1,k); B: B*(A*q) + lambda*q; m-space: the one pass
+    // over B stages q = v/h and publishes h; the MGS dots kernel writes q back over v — so the
+    // sweep needs no scale pass.  Step k's event is then
     // recorded at the end of step k+1.  HGM_OPT_PEND_NORM = 0 keeps the scale pass.
-    const bool pn_ok = nspace && !dist && orth == HGM_MGS && c->num.pend_norm && !parity &&
-                       spmv_pn_ok(A, EPI_DIVH) && spmv_pn_ok(B, EPI_ADDQ);
     // m-space side with B = A' value for value: B*q and A*(B*q) in one pass over B (fused.hip)
     const FusedPlan* fplan = nspace ? nullptr : fused_ab_plan(c, A, B);
+    // (m-space, round 6: the one pass over B applies q = v / h as it stages q, so the m-space sweep
+    // needs no scale pass either; the m-vectors are replicated, so this holds on a communicator too,
+    // every rank forming the same h from the same replicated partials)
+    // (m-space only with HGM_OPT_PEND_NORM = 2: the pass's staging then waits for the division, which
+    // measured ~1.4 % slower at C4 than the scale pass it replaces)
+    const bool pn_ok = !dist && orth == HGM_MGS && c->num.pend_norm >= 1 && !parity &&
+                       (nspace ? spmv_pn_ok(A, EPI_DIVH) && spmv_pn_ok(B, EPI_ADDQ)
+                               : c->num.pend_norm == 2 && std::is_same_v<T, double> && fplan != nullptr &&
+                                     fused_pend_ok(c, fplan) && !krylov_padded(c, ldq));
     PendNorm<T> pend;                                  // np > 0: Q(:,next step) awaits its division
     T* pn_h = c->buf<T>("pn_h", 2);
     // Enqueue Arnoldi step kq: operator application + orthogonalisation (+ Gram column).
@@ -486,8 +494,15 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
                 // (when the column's stride leaves room past m): one collective per step, not two
                 const int64_t wld = (ABQ && orth != HGM_CGS2) ? ldaq : ldq;
                 const bool ride = zxf && dist_n(c) && wld > m;
+                PendNorm<T> pq;                                // q_k = v_k / H(k,k-1) as the pass stages it
+                if (pending_in) {
+                    pq = pend;
+                    pq.hdev = pn_h;
+                    pq.hring = dr + (size_t)(kq - 1) * LH + kq;  // H(kq, kq-1) of step kq-1
+                }
                 if constexpr (std::is_same_v<T, double>)
-                    zx_fused = fused_ab(c, B, fplan, qk, Bq, w, zxf ? xt : nullptr, ride ? w + m : zx_dst);
+                    zx_fused = fused_ab(c, B, fplan, qk, Bq, w, zxf ? xt : nullptr, ride ? w + m : zx_dst,
+                                        pending_in ? &pq : nullptr);
                 zx_rode = ride && zx_fused;
                 if (dist_n(c)) allreduce(c, w, zx_rode ? m + 1 : m);             // (as apply_A)
                 // (the all-reduced side dot goes into the ring with the MGS sweep below)
@@ -548,8 +563,9 @@ int gmres_family(hgm_ctx* c, const GmresSpec& sp, const hgm_opts* o, const hgm_m
         // Step kq-1's column is complete (H(kq,kq-1) came from this step's A product).  The
         // event goes at the end of the step: a marker between two kernels costs a bubble.
         if (poll) return;                                 // the host polls the ring instead
-        if (nspace && pending_in) {
+        if (pending_in) {
             publish((size_t)(kq - 1) * LH, LH);
+            if (gem_ab) publish(offQG + (size_t)(kq - 1) * LQ, (size_t)kq + 2);   // its Gram row
             step_record(c, kq - 1);
         }
         if (pend.np == 0) {                               // else: recorded at the end of step kq+1

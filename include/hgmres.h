@@ -103,7 +103,8 @@ enum hgm_ctx_option {
                                       AB *_bounds solvers when B is the device transpose of A [1] */
     HGM_OPT_GRAM_ERR_MIN = 5,      /* ... used while ||x-x_true||^2/||x_true||^2 >= this [0.01] */
     HGM_OPT_RING_POLL = 6,         /* single GPU: host polls the pinned ring instead of events [1] */
-    HGM_OPT_PEND_NORM = 7,         /* pending normalisation of the Krylov vector [1] */
+    HGM_OPT_PEND_NORM = 7,         /* pending normalisation of the Krylov vector: 0 off, 1 n-space [1],
+                                      2 n-space and m-space (the one pass over B divides) */
     HGM_OPT_RECON_SERIAL = 8,      /* GMRES reconstruction: -1 automatic [-1], 0 aux stream, 1 main stream */
     HGM_OPT_RECON_SERIAL_N = 9,    /* automatic: serialise from this n on [4194304] */
     HGM_OPT_PIPE_DEPTH = 10,       /* speculative Arnoldi steps in flight, 1..6 [2] */

@@ -167,6 +167,38 @@ def test_fused_region_overflow_falls_back(gpu_ctx, kind):
         assert np.array_equal(np.asarray(a_), np.asarray(b_))
 
 
+@pytest.mark.parametrize("N,na", [(512, 30), (256, 47), (100, 17)])
+def test_fused_pending_normalisation_is_bitwise(gpu_ctx, N, na):
+    """Round 6 (HGM_OPT_PEND_NORM = 2, opt-in): on the m-space side the one pass over B stages
+    q_k = v_k / H(k,k-1) itself (every wave re-reduces the previous sweep's norm partials in
+    k_mgs_normalize's order) and the MGS
+    sweep writes q_k back, so the sweep has no scale pass.  The divisions are the same IEEE
+    operations on the same operands, so every output is bit for bit the scale-pass solve's: H, x,
+    both histories, the hybrid (PTR) variant, the shortest pipeline, and a tol stop mid-solve
+    (the speculative steps then hold a pending column that is discarded)."""
+    A, B, b, xt = _device_problem(gpu_ctx, N, na)
+    k = 20
+    runs = {}
+    for pn in (0, 1, 2):                                # 2: the m-space pending normalisation
+        with gpu_ctx.options(fused_ab=1, pend_norm=pn):
+            r = [hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True),
+                 hgmres.ABgmres_hybrid_bounds(A, B, b, xt, 0.0, k, 1e-2, ctx=gpu_ctx, return_H=True)]
+            with gpu_ctx.options(pipe_depth=1):
+                r.append(hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, k, ctx=gpu_ctx, return_H=True))
+            for kk in (1, 2):
+                r.append(hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, 0.0, kk, ctx=gpu_ctx, return_H=True))
+            res = r[0][2]
+            tol = 0.5 * (res[6] + res[7])               # stops after iteration 8 (1-based)
+            r.append(hgmres.ABgmres_nonhybrid_bounds(A, B, b, xt, tol, k, ctx=gpu_ctx, return_H=True))
+            runs[pn] = r
+    assert runs[2][-1][3] == runs[1][-1][3] == runs[0][-1][3] == 8
+    for pn in (1, 2):
+        for a, b_ in zip(runs[pn], runs[0]):
+            for x1, x0 in zip(a, b_):
+                assert np.array_equal(np.asarray(x1), np.asarray(x0))
+    print(f"[pending normalisation N={N} angles={na}] 6 solves bitwise equal to the scale-pass solves")
+
+
 def test_fused_not_taken_for_unmatched_or_reference_order(gpu_ctx):
     """Unmatched B (not A' value for value) and reference-order operators keep the two-pass path:
     the option changes nothing there."""
