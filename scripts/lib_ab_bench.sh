@@ -1,6 +1,6 @@
 # Alternating bench lines of two libraries on one box: HGM_LIB=OLD.so against the in-tree library,
 # per workload, ROUNDS rounds.  -> gpurun_out/libab${AB_TAG}/lib_ab_bench.jsonl
-# usage: bash scripts/lib_ab_bench.sh OLD.so ROUNDS WL [WL ...]
+# usage: bash scripts/lib_ab_bench.sh OLD.so ROUNDS WL [WL ...]   (a WL may carry bench args: "c4 --shard1 ...")
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/libab${AB_TAG:-}; mkdir -p $O
@@ -17,7 +17,7 @@ for r in $(seq "$rounds"); do
       python3 -c "
 import json
 d = json.loads([l for l in open('$O/ab.log') if l.startswith('{')][-1])
-print(json.dumps({'round': $r, 'workload': '$wl', 'side': '$side', 'value': d['value'], 'ms_per_step': d['ms_per_step'],
+print(json.dumps({'round': $r, 'workload': '''$wl''', 'side': '$side', 'value': d['value'], 'ms_per_step': d['ms_per_step'],
                   'kernels': {k: round(v['avg_us'], 2) for k, v in d['kernels'].items()}}))" | tee -a $O/lib_ab_bench.jsonl
     done
   done

@@ -176,6 +176,8 @@ def test_fused_pending_normalisation_is_bitwise(gpu_ctx, N, na):
     operations on the same operands, so every output is bit for bit the scale-pass solve's: H, x,
     both histories, the hybrid (PTR) variant, the shortest pipeline, and a tol stop mid-solve
     (the speculative steps then hold a pending column that is discarded)."""
+    with pytest.raises((ValueError, hgmres.HgmError)):     # 0, 1 or 2
+        gpu_ctx.set_option("pend_norm", 3)
     A, B, b, xt = _device_problem(gpu_ctx, N, na)
     k = 20
     runs = {}
