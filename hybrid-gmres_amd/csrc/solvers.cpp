@@ -212,7 +212,11 @@ struct GmresSpec {
 constexpr uint64_t RING_SENTINEL = 0x7FF4DEADBEEF0001ull;   // a NaN no kernel produces
 // Spin until ring[i] for i in idx are all non-sentinel.  Checks the streams that write them
 // (main and, when it is a different one, aux) for errors, and for all going idle with an entry
-// never written (a bug), once per ms so a fault cannot hang.
+// never written (a bug), every RING_CHECK_MS so a fault cannot hang.  Not more often: a
+// hipStreamQuery on a stream with work queued puts a marker packet behind that work, and the
+// kernel queued after the marker then starts ~5.7 us late (round 6: at the 1 ms interval every
+// Arnoldi step from the fourth on waited so at C4, profiles/r6_hip_api_trace_gaps.txt).
+constexpr int RING_CHECK_MS = 200;
 static void ring_wait(hgm_ctx* c, const double* ring, const std::vector<size_t>& idx, hipStream_t aux = nullptr) {
     const volatile uint64_t* r = reinterpret_cast<const volatile uint64_t*>(ring);
     const auto t0 = std::chrono::steady_clock::now();
@@ -229,7 +233,7 @@ static void ring_wait(hgm_ctx* c, const double* ring, const std::vector<size_t>&
         if (all) break;
         pause();
         const auto now = std::chrono::steady_clock::now();
-        if (now - last > std::chrono::milliseconds(1)) {
+        if (now - last > std::chrono::milliseconds(RING_CHECK_MS)) {
             last = now;
             hipError_t q = hipStreamQuery(c->stream);
             if (q != hipSuccess && q != hipErrorNotReady) HGM_HIP(q);
