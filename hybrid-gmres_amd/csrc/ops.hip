@@ -680,11 +680,39 @@ __global__ __launch_bounds__(BS) void k_pix_unmap(int N, int tile, int super, in
     }
 }
 
+// The same permutation for the default order (tiles of a power-of-two side, no super-blocks,
+// N^2 < 2^32), swept in STORED order with 32-bit index math (round 6): a wave's 64 stored
+// entries are 64 / tile^2 consecutive tiles of one tile column, i.e. tile full runs of 64 / tile
+// consecutive reference entries, so both sides move whole cache lines, and no 64-bit division is
+// left (k_pix_permute walks the reference order and divides in 64 bits: at C4, 67-89 us for the
+// 134 MB each way, on the critical path of every solve's input and output hand-over).
+template <typename T>
+__global__ __launch_bounds__(BS) void k_pix_permute_t(uint32_t N, uint32_t nt, int tsh, const T* __restrict__ in,
+                                                      T* __restrict__ out, int dir, uint32_t n) {
+    const uint32_t tm = (1u << tsh) - 1u, wm = (1u << (2 * tsh)) - 1u;
+    for (uint32_t s = blockIdx.x * BS + threadIdx.x; s < n; s += gridDim.x * BS) {
+        const uint32_t t = s >> (2 * tsh), w = s & wm;            // tile, position in it (column-major)
+        const uint32_t tc = t / nt, tr = t - tc * nt;              // tile-column-major tiles
+        const uint32_t col = (tc << tsh) + (w >> tsh), row = (tr << tsh) + (w & tm);
+        const uint32_t p = row + col * N;
+        if (dir == 0) out[s] = in[p];
+        else out[p] = in[s];
+    }
+}
+
 template <typename T>
 void pix_permute(hgm_ctx* c, const PixOrder& o, const T* in, T* out, int dir) {
     HGM_REQUIRE(!o.trivial(), "pix_permute: trivial order");
     const int64_t n = (int64_t)o.N * o.N;
-    k_pix_permute<T><<<grid_cap(n), BS, 0, c->stream>>>(o.N, o.tile, o.super, in, out, dir);
+    const bool pow2 = o.tile >= 2 && (o.tile & (o.tile - 1)) == 0;
+    if (o.super <= 1 && pow2 && o.N % o.tile == 0 && n < ((int64_t)1 << 32)) {
+        int tsh = 0;
+        while ((1 << tsh) < o.tile) ++tsh;
+        k_pix_permute_t<T><<<grid_cap(n), BS, 0, c->stream>>>((uint32_t)o.N, (uint32_t)(o.N / o.tile), tsh, in, out,
+                                                             dir, (uint32_t)n);
+    } else {
+        k_pix_permute<T><<<grid_cap(n), BS, 0, c->stream>>>(o.N, o.tile, o.super, in, out, dir);
+    }
     HGM_HIP(hipGetLastError());
 }
 template void pix_permute<double>(hgm_ctx*, const PixOrder&, const double*, double*, int);
