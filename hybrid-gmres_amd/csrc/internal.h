@@ -406,6 +406,10 @@ template <typename T> void div_sqrt(hgm_ctx* c, int64_t n, const T* in, T* out, 
 // (optional: the kept A*v_k), t = av - alpha*u, *ss_out = ||t||^2 (alpha = sqrt(*ssa), device)
 template <typename T>
 void gkb_mstep(hgm_ctx* c, int64_t n, const T* w, const T* ssa, const T* u, T* t, T* av, T* ss_out);
+// gkb_mstep, then u = t / sqrt(||t||^2) (nz: a zero norm leaves t, as div_sqrt_nz), the norm's
+// partials re-formed by every block of the division (no k_finalize launch; the same bits)
+template <typename T>
+void gkb_mstep_div(hgm_ctx* c, int64_t n, const T* w, const T* ssa, T* u, T* t, T* av, T* ss_out, bool nz);
 // (one-pass LSQR) A*x and A*w images in double (kernels.hip k_lsqr_img)
 template <typename T>
 void lsqr_img(hgm_ctx* c, int64_t m, const T* wm, const T* ssa, const T* coef, const double* st, int k, double* ax,

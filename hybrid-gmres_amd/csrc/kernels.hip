@@ -1661,6 +1661,47 @@ void gkb_mstep(hgm_ctx* c, int64_t n, const T* w, const T* ssa, const T* u, T* t
 }
 template void gkb_mstep<double>(hgm_ctx*, int64_t, const double*, const double*, const double*, double*, double*,
                                 double*);
+
+// out = in / s with s = (T)sqrt(ss), ss the sum of the np partials of ||in||^2 that every block
+// re-forms in k_finalize's order (reduce_parts: the same bits); block 0 publishes ss to ss_out.
+// NZ: a zero s leaves in (lsmr_solver.m:36, as k_div_sqrt_nz).  Round 6: replaces the
+// k_finalize + k_div_sqrt launch pair of the one-pass Golub-Kahan m-space step.
+template <typename T, bool NZ>
+__global__ __launch_bounds__(BS) void k_div_sqrt_parts(int64_t n, const T* __restrict__ in, T* __restrict__ out,
+                                                       const T* __restrict__ parts, int np, T* ss_out) {
+    __shared__ T sh[4];
+    const T ssv = reduce_parts(parts, np, sh);
+    if (blockIdx.x == 0 && threadIdx.x == 0) st_sys(ss_out, ssv);
+    const T s = (T)sqrt((double)ssv);
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < n; i += (int64_t)gridDim.x * BS)
+        out[i] = (!NZ || s > T(0)) ? in[i] / s : in[i];
+}
+
+// gkb_mstep (t = A*v_k - alpha*u, ||t||^2 -> ss_out) followed by u = t / sqrt(||t||^2) (NZ: as
+// div_sqrt_nz): two launches where the separate calls take three (the same bits).
+template <typename T>
+void gkb_mstep_div(hgm_ctx* c, int64_t n, const T* w, const T* ssa, T* u, T* t, T* av, T* ss_out, bool nz) {
+    const bool fuse = n > SINGLE_MAX && !c->num.parity;
+    if (!fuse) {
+        gkb_mstep<T>(c, n, w, ssa, u, t, av, ss_out);
+        if (nz) div_sqrt_nz<T>(c, n, t, u, ss_out);
+        else div_sqrt<T>(c, n, t, u, ss_out);
+        return;
+    }
+    const int np = parts_for(n);
+    T* parts = c->buf<T>("red_parts", MAX_PARTS);
+    if (al16(w) && al16(u) && al16(t) && (!av || al16(av)))
+        k_gkb_mstep<T, true><<<np, BS, 0, c->stream>>>(n, w, ssa, u, t, av, parts);
+    else
+        k_gkb_mstep<T, false><<<np, BS, 0, c->stream>>>(n, w, ssa, u, t, av, parts);
+    if (nz) k_div_sqrt_parts<T, true><<<grid_for(n), BS, 0, c->stream>>>(n, t, u, parts, np, ss_out);
+    else k_div_sqrt_parts<T, false><<<grid_for(n), BS, 0, c->stream>>>(n, t, u, parts, np, ss_out);
+    HGM_HIP(hipGetLastError());
+}
+template void gkb_mstep_div<double>(hgm_ctx*, int64_t, const double*, const double*, double*, double*, double*,
+                                    double*, bool);
+template void gkb_mstep_div<float>(hgm_ctx*, int64_t, const float*, const float*, float*, float*, float*, float*,
+                                   bool);
 template void gkb_mstep<float>(hgm_ctx*, int64_t, const float*, const float*, const float*, float*, float*, float*);
 
 // (one-pass LSQR) the images of x and w under A, in double, so the exact final residual of

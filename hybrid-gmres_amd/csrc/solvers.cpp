@@ -956,8 +956,7 @@ int lsqr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         for (k = 0; k < maxit && stop == 0;) {
             const int kend = std::min(maxit, k + batch);
             for (; k < kend; ++k) {
-                gkb_mstep<T>(c, m, wm, wm + m, u, t, nullptr, sl + S_BETA);          // :22-23 A*v - alpha*u
-                div_sqrt<T>(c, m, t, u, sl + S_BETA);                                // :24
+                gkb_mstep_div<T>(c, m, wm, wm + m, u, t, nullptr, sl + S_BETA, false);   // :22-24
                 fused_pass<T>(c, At, fp, fa);                                        // :26-27 (+ A*v_hat)
                 if (dist_n(c)) allreduce(c, wm, (ride && k > 0) ? m + 2 : m + 1);
                 if (host_sc) {
@@ -1325,8 +1324,7 @@ int lsmr_t(hgm_ctx* c, const hgm_opts* o, const hgm_mat* A, const hgm_mat* At, c
         for (k = 0; k < maxit && stop == 0;) {
             const int kend = std::min(maxit, k + batch);
             for (; k < kend; ++k) {
-                gkb_mstep<T>(c, m, wm, wm + m, u, r, Av, sl + S_BETA);           // :34-35 (+ kept A*v_k)
-                div_sqrt_nz<T>(c, m, r, u, sl + S_BETA);                          // :36
+                gkb_mstep_div<T>(c, m, wm, wm + m, u, r, Av, sl + S_BETA, true);  // :34-36 (+ kept A*v_k)
                 fa.zraw = Atu1;                                                   // A'*u_{k+1} (kept)
                 fused_pass<T>(c, At, fp, fa);                                     // :38-39 (+ A*v_hat)
                 if (dist_n(c)) allreduce(c, wm, (ride && k > 0) ? m + 1 + ride_n : m + 1);
